@@ -1,0 +1,720 @@
+/*
+ * mq_query.c — the reference operator API (src/include/query.h:20-50) in C on
+ * top of libmq's device layer (include/mq_device.h).
+ *
+ * This file is host control only: it keeps the reference's calling contract
+ * (Column* and Result* in, malloc'd Result out, Status.code), decides what is
+ * device-resident, and moves results between HBM and host memory. Every
+ * row-proportional loop of the reference runs as a gfx950 kernel; there is no
+ * CPU fallback — without a device every entry point sets Status ERROR and
+ * returns NULL, after printing why to stderr.
+ *
+ * Residency:
+ *   - Column rows (column->data, mmap'd host memory in the reference,
+ *     db_manager.c:736-790) are uploaded once and cached by (Column*, data,
+ *     row_count) until mq_column_invalidate(); mq_column_attach() adopts an
+ *     existing HBM copy without any upload.
+ *   - A Result made here keeps a device shadow keyed by its payload pointer, so
+ *     the next operator on it (fetch, sum, avg, select_result, ...) reads HBM.
+ *     The shadow is validated against num_tuples and the first/last element and
+ *     is re-uploaded on mismatch. Shadows are evicted LRU beyond a byte budget
+ *     (MQ_SHADOW_MB, default 65536 MB).
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "mq_query.h"
+
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "mq_device.h"
+
+/* ---- ABI pins: x86-64 layouts of the reference structs ---- */
+_Static_assert(sizeof(Result) == 24, "Result size");
+_Static_assert(offsetof(Result, num_tuples) == 0, "Result.num_tuples");
+_Static_assert(offsetof(Result, data_type) == 8, "Result.data_type");
+_Static_assert(offsetof(Result, payload) == 16, "Result.payload");
+_Static_assert(sizeof(Column) == 128, "Column size");
+_Static_assert(offsetof(Column, data) == 64, "Column.data");
+_Static_assert(offsetof(Column, fd) == 72, "Column.fd");
+_Static_assert(offsetof(Column, row_count) == 80, "Column.row_count");
+_Static_assert(offsetof(Column, sorted) == 88, "Column.sorted");
+_Static_assert(offsetof(Column, clustered) == 89, "Column.clustered");
+_Static_assert(offsetof(Column, has_index) == 90, "Column.has_index");
+_Static_assert(offsetof(Column, index) == 96, "Column.index");
+_Static_assert(offsetof(Column, btree_node) == 104, "Column.btree_node");
+_Static_assert(offsetof(Column, histogram) == 112, "Column.histogram");
+_Static_assert(offsetof(Column, max) == 120, "Column.max");
+_Static_assert(offsetof(Column, min) == 124, "Column.min");
+_Static_assert(sizeof(Status) == 16, "Status size");
+_Static_assert(offsetof(Status, error_message) == 8, "Status.error_message");
+_Static_assert(sizeof(GeneralizedColumn) == 16, "GeneralizedColumn size");
+_Static_assert(offsetof(GeneralizedColumn, column_pointer) == 8, "GeneralizedColumn.pointer");
+_Static_assert(sizeof(SelectOperator) == 136, "SelectOperator size");
+_Static_assert(offsetof(SelectOperator, handle) == 4, "SelectOperator.handle");
+_Static_assert(offsetof(SelectOperator, low) == 68, "SelectOperator.low");
+_Static_assert(offsetof(SelectOperator, high) == 72, "SelectOperator.high");
+_Static_assert(offsetof(SelectOperator, has_low) == 76, "SelectOperator.has_low");
+_Static_assert(offsetof(SelectOperator, has_high) == 80, "SelectOperator.has_high");
+_Static_assert(offsetof(SelectOperator, db) == 88, "SelectOperator.db");
+_Static_assert(offsetof(SelectOperator, column) == 104, "SelectOperator.column");
+_Static_assert(offsetof(SelectOperator, comparator) == 128, "SelectOperator.comparator");
+_Static_assert(sizeof(ColumnIndex) == 16, "ColumnIndex size");
+_Static_assert(INT == 0 && LONG == 1 && FLOAT == 2 && DOUBLE == 3, "DataType values");
+_Static_assert(OK == 0 && ERROR == 1, "StatusCode values");
+
+/* ------------------------------------------------------------------ */
+/* state                                                              */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    const Column* col;
+    const int* host;
+    size_t rows;
+    void* dev;
+    int owned;
+} ColEntry;
+
+typedef struct {
+    const void* host;
+    size_t n;
+    size_t bytes;
+    int32_t head, tail;
+    void* dev;
+    unsigned long long stamp;
+} ShadowEntry;
+
+typedef struct {
+    const ColumnIndex* index;
+    const int* values;
+    const size_t* positions;
+    size_t rows;
+    void* d_values;
+    void* d_positions;
+} IndexEntry;
+
+#define MAX_COLS 1024
+#define MAX_SHADOWS 4096
+#define MAX_INDEXES 256
+
+static ColEntry g_cols[MAX_COLS];
+static int g_ncols;
+static ShadowEntry g_shadows[MAX_SHADOWS];
+static int g_nshadows;
+static size_t g_shadow_bytes;
+static unsigned long long g_stamp;
+static IndexEntry g_idx[MAX_INDEXES];
+static int g_nidx;
+
+static void* g_ws;        /* scan workspace */
+static size_t g_ws_bytes;
+static void* g_scratch;   /* capacity-n int32 output staging */
+static size_t g_scratch_bytes;
+static void* g_small;     /* mq_agg + counts */
+static int g_ready;       /* 1 ok, -1 failed */
+static void* g_stream;
+static double g_xfer_s;
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int fail(Status* st, const char* what, int rc) {
+    fprintf(stderr, "libmq: %s failed (%d): %s\n", what, rc, mq_last_error());
+    if (st) st->code = ERROR;
+    return rc;
+}
+
+static int ready(Status* st) {
+    if (g_ready == 1) return 0;
+    if (g_ready == -1) return fail(st, "device init (earlier)", MQ_ENODEV);
+    const char* env = getenv("MQ_DEVICE");
+    int dev = env ? atoi(env) : 0;
+    int rc = mq_init(dev);
+    if (rc) {
+        g_ready = -1;
+        return fail(st, "device init", rc);
+    }
+    g_stream = mq_default_stream();
+    if (!g_stream) {
+        g_ready = -1;
+        return fail(st, "stream creation", MQ_EHIP);
+    }
+    rc = mq_malloc(&g_small, 4096);
+    if (rc) {
+        g_ready = -1;
+        return fail(st, "small buffer", rc);
+    }
+    g_ready = 1;
+    return 0;
+}
+
+static int grow(void** buf, size_t* have, size_t need) {
+    if (*have >= need && *buf) return 0;
+    if (*buf) mq_free(*buf);
+    *buf = NULL;
+    *have = 0;
+    size_t want = need + need / 8 + 4096;
+    int rc = mq_malloc(buf, want);
+    if (rc) return rc;
+    *have = want;
+    return 0;
+}
+
+static int h2d(void* d, const void* h, size_t bytes) {
+    double t0 = now_s();
+    int rc = mq_memcpy_h2d(d, h, bytes, g_stream);
+    g_xfer_s += now_s() - t0;
+    return rc;
+}
+
+static int d2h(void* h, const void* d, size_t bytes) {
+    double t0 = now_s();
+    int rc = mq_memcpy_d2h(h, d, bytes, g_stream);
+    g_xfer_s += now_s() - t0;
+    return rc;
+}
+
+/* ---- column residency ---- */
+
+static ColEntry* col_find(const Column* c) {
+    for (int i = 0; i < g_ncols; i++)
+        if (g_cols[i].col == c) return &g_cols[i];
+    return NULL;
+}
+
+static void col_drop(ColEntry* e) {
+    if (e->owned && e->dev) mq_free(e->dev);
+    *e = g_cols[--g_ncols];
+}
+
+static int column_device(Column* c, const int32_t** d, Status* st) {
+    ColEntry* e = col_find(c);
+    if (e && e->host == c->data && e->rows == c->row_count) {
+        *d = (const int32_t*)e->dev;
+        return 0;
+    }
+    if (e) col_drop(e);
+    if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
+    size_t bytes = c->row_count * sizeof(int32_t);
+    void* dev = NULL;
+    int rc = mq_malloc(&dev, bytes);
+    if (rc) return fail(st, "column allocation", rc);
+    if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
+        mq_free(dev);
+        return fail(st, "column upload", rc);
+    }
+    g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1};
+    *d = (const int32_t*)dev;
+    return 0;
+}
+
+/* ---- result shadows ---- */
+
+static void shadow_drop(int i) {
+    if (g_shadows[i].dev) mq_free(g_shadows[i].dev);
+    g_shadow_bytes -= g_shadows[i].bytes;
+    g_shadows[i] = g_shadows[--g_nshadows];
+}
+
+static size_t shadow_budget(void) {
+    static size_t budget;
+    if (!budget) {
+        const char* env = getenv("MQ_SHADOW_MB");
+        size_t mb = env ? (size_t)strtoull(env, NULL, 10) : 65536;
+        budget = mb << 20;
+    }
+    return budget;
+}
+
+static void shadow_make_room(size_t bytes) {
+    while (g_nshadows > 0 && (g_nshadows >= MAX_SHADOWS || g_shadow_bytes + bytes > shadow_budget())) {
+        int lru = 0;
+        for (int i = 1; i < g_nshadows; i++)
+            if (g_shadows[i].stamp < g_shadows[lru].stamp) lru = i;
+        shadow_drop(lru);
+    }
+}
+
+static int shadow_find(const void* host) {
+    for (int i = 0; i < g_nshadows; i++)
+        if (g_shadows[i].host == host) return i;
+    return -1;
+}
+
+/* Register dev (owned, n int32) as the shadow of host payload. */
+static void shadow_put(const void* host, size_t n, void* dev) {
+    int i = shadow_find(host);
+    if (i >= 0) shadow_drop(i);
+    size_t bytes = n * sizeof(int32_t);
+    shadow_make_room(bytes);
+    const int32_t* h = (const int32_t*)host;
+    g_shadows[g_nshadows++] = (ShadowEntry){host, n, bytes, n ? h[0] : 0, n ? h[n - 1] : 0, dev,
+                                            ++g_stamp};
+    g_shadow_bytes += bytes;
+}
+
+/* Device view of an int32 Result payload (shadow, or a fresh upload). */
+static int result_device(const Result* r, const int32_t** d, Status* st) {
+    const int32_t* h = (const int32_t*)r->payload;
+    size_t n = r->num_tuples;
+    int i = shadow_find(h);
+    if (i >= 0 && g_shadows[i].n == n && (n == 0 || (g_shadows[i].head == h[0] && g_shadows[i].tail == h[n - 1]))) {
+        g_shadows[i].stamp = ++g_stamp;
+        *d = (const int32_t*)g_shadows[i].dev;
+        return 0;
+    }
+    void* dev = NULL;
+    int rc = mq_malloc(&dev, n * sizeof(int32_t));
+    if (rc) return fail(st, "result allocation", rc);
+    if (n && (rc = h2d(dev, h, n * sizeof(int32_t)))) {
+        mq_free(dev);
+        return fail(st, "result upload", rc);
+    }
+    shadow_put(h, n, dev);
+    *d = (const int32_t*)dev;
+    return 0;
+}
+
+static Result* new_result(DataType t, size_t n, void* payload) {
+    Result* r = (Result*)malloc(sizeof(Result));
+    r->num_tuples = n;
+    r->data_type = t;
+    r->payload = payload;
+    return r;
+}
+
+/* Host Result from n int32 on the device (d_src, staging memory): D2H into a
+ * malloc'd payload and keep an HBM shadow of it. */
+static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
+    int32_t* host = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    int rc;
+    if (n && (rc = d2h(host, d_src, n * sizeof(int32_t)))) {
+        free(host);
+        fail(st, "result download", rc);
+        return NULL;
+    }
+    void* dev = NULL;
+    if ((rc = mq_malloc(&dev, n * sizeof(int32_t)))) {
+        free(host);
+        fail(st, "shadow allocation", rc);
+        return NULL;
+    }
+    if (n && (rc = mq_memcpy_d2d(dev, d_src, n * sizeof(int32_t), g_stream))) {
+        mq_free(dev);
+        free(host);
+        fail(st, "shadow copy", rc);
+        return NULL;
+    }
+    shadow_put(host, n, dev);
+    st->code = OK;
+    return new_result(INT, n, host);
+}
+
+static int read_count(uint64_t* k, Status* st) {
+    int rc = d2h(k, g_small, sizeof(uint64_t));
+    if (rc) return fail(st, "count download", rc);
+    return 0;
+}
+
+static int read_agg(mq_agg* a, Status* st) {
+    int rc = d2h(a, g_small, sizeof(mq_agg));
+    if (rc) return fail(st, "aggregate download", rc);
+    return 0;
+}
+
+static int ensure_ws(size_t n_rows, Status* st) {
+    int rc = grow(&g_ws, &g_ws_bytes, mq_scan_workspace_bytes(n_rows));
+    if (rc) return fail(st, "workspace allocation", rc);
+    rc = grow(&g_scratch, &g_scratch_bytes, (n_rows ? n_rows : 1) * sizeof(int32_t));
+    if (rc) return fail(st, "staging allocation", rc);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* the reference API                                                  */
+/* ------------------------------------------------------------------ */
+
+/* query.c:26-36: the reference returns before logging anything. */
+void log_result(Result* result) { (void)result; }
+
+/* index.c:180-185 — weak: the reference's index.o definition takes precedence. */
+__attribute__((weak)) bool should_use_index(Column* column, int low, int high) {
+    (void)column;
+    (void)low;
+    (void)high;
+    return true;
+}
+
+/* query.c:92-137 */
+Result* select_column_scan(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    size_t n = column->row_count;
+    const int32_t* dcol;
+    if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
+    int rc = mq_select_positions(dcol, NULL, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
+                                 high_pointer != NULL, high_pointer ? *high_pointer : 0,
+                                 (int32_t*)g_scratch, (uint64_t*)g_small, g_ws, g_ws_bytes, g_stream);
+    if (rc) {
+        fail(ret_status, "select_column_scan", rc);
+        return NULL;
+    }
+    uint64_t k;
+    if (read_count(&k, ret_status)) return NULL;
+    return int_result_from_device(g_scratch, (size_t)k, ret_status);
+}
+
+/* query.c:165-198: sorted-index select, in value order. */
+Result* select_column_sorted_index(Column* column, int low, int high, Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    ColumnIndex* ix = column->index;
+    size_t n = column->row_count;
+    IndexEntry* e = NULL;
+    for (int i = 0; i < g_nidx; i++)
+        if (g_idx[i].index == ix) e = &g_idx[i];
+    if (e && (e->values != ix->values || e->positions != ix->positions || e->rows != n)) {
+        mq_free(e->d_values);
+        mq_free(e->d_positions);
+        *e = g_idx[--g_nidx];
+        e = NULL;
+    }
+    if (!e) {
+        if (g_nidx == MAX_INDEXES) {
+            mq_free(g_idx[0].d_values);
+            mq_free(g_idx[0].d_positions);
+            g_idx[0] = g_idx[--g_nidx];
+        }
+        IndexEntry ne = {ix, ix->values, ix->positions, n, NULL, NULL};
+        int rc;
+        if ((rc = mq_malloc(&ne.d_values, n * sizeof(int32_t))) ||
+            (rc = mq_malloc(&ne.d_positions, n * sizeof(uint64_t))) ||
+            (n && (rc = h2d(ne.d_values, ix->values, n * sizeof(int32_t)))) ||
+            (n && (rc = h2d(ne.d_positions, ix->positions, n * sizeof(uint64_t))))) {
+            mq_free(ne.d_values);
+            mq_free(ne.d_positions);
+            fail(ret_status, "index upload", rc);
+            return NULL;
+        }
+        g_idx[g_nidx++] = ne;
+        e = &g_idx[g_nidx - 1];
+    }
+    if (ensure_ws(n, ret_status)) return NULL;
+    int rc = mq_index_select((const int32_t*)e->d_values, (const uint64_t*)e->d_positions, n, low, high,
+                             (int32_t*)g_scratch, (uint64_t*)g_small, g_stream);
+    if (rc) {
+        fail(ret_status, "select_column_sorted_index", rc);
+        return NULL;
+    }
+    uint64_t k;
+    if (read_count(&k, ret_status)) return NULL;
+    return int_result_from_device(g_scratch, (size_t)k, ret_status);
+}
+
+/* query.c:203-220: same dispatch as the reference (clustered or indexed columns
+ * take the sorted-index path, which dereferences both bounds as it does). */
+Result* select_column(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
+    if (column->clustered)
+        return select_column_sorted_index(column, *low_pointer, *high_pointer, ret_status);
+    if (column->has_index && should_use_index(column, *low_pointer, *high_pointer))
+        return select_column_sorted_index(column, *low_pointer, *high_pointer, ret_status);
+    return select_column_scan(column, low_pointer, high_pointer, ret_status);
+}
+
+/* query.c:38-86 */
+Result* select_result(Result* column, Result* prev_position, int* low_pointer, int* high_pointer,
+                      Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    size_t n = column->num_tuples;
+    const int32_t *dval, *dpos;
+    if (result_device(column, &dval, ret_status) || result_device(prev_position, &dpos, ret_status) ||
+        ensure_ws(n, ret_status))
+        return NULL;
+    int rc = mq_select_positions(dval, dpos, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
+                                 high_pointer != NULL, high_pointer ? *high_pointer : 0,
+                                 (int32_t*)g_scratch, (uint64_t*)g_small, g_ws, g_ws_bytes, g_stream);
+    if (rc) {
+        fail(ret_status, "select_result", rc);
+        return NULL;
+    }
+    uint64_t k;
+    if (read_count(&k, ret_status)) return NULL;
+    return int_result_from_device(g_scratch, (size_t)k, ret_status);
+}
+
+/* query.c:223-243 */
+Result* fetch_column(Column* column, Result* position_result, Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    size_t k = position_result->num_tuples;
+    const int32_t *dcol, *dpos;
+    if (column_device(column, &dcol, ret_status) || result_device(position_result, &dpos, ret_status) ||
+        ensure_ws(k, ret_status))
+        return NULL;
+    int rc = mq_fetch(dcol, dpos, k, (int32_t*)g_scratch, g_stream);
+    if (rc) {
+        fail(ret_status, "fetch_column", rc);
+        return NULL;
+    }
+    return int_result_from_device(g_scratch, k, ret_status);
+}
+
+static int reduce_result(Result* r, mq_agg* a, Status* st) {
+    if (ready(st)) return -1;
+    const int32_t* d;
+    if (result_device(r, &d, st) || ensure_ws(0, st)) return -1;
+    int rc = mq_reduce(d, r->num_tuples, (mq_agg*)g_small, g_ws, g_ws_bytes, g_stream);
+    if (rc) return fail(st, "reduce", rc);
+    return read_agg(a, st);
+}
+
+/* query.c:306-323: (double)int64_sum / (double)n; n == 0 gives NaN as there. */
+Result* average(Result* column, Status* ret_status) {
+    mq_agg a;
+    if (reduce_result(column, &a, ret_status)) return NULL;
+    double* out = (double*)malloc(sizeof(double));
+    *out = (double)a.sum / (double)column->num_tuples;
+    ret_status->code = OK;
+    return new_result(DOUBLE, 1, out);
+}
+
+/* query.c:325-354: RESULT or COLUMN, int64 sum. */
+Result* sum(GeneralizedColumn* column, Status* ret_status) {
+    mq_agg a;
+    if (column->column_type == RESULT) {
+        if (reduce_result(column->column_pointer.result, &a, ret_status)) return NULL;
+    } else {
+        if (ready(ret_status)) return NULL;
+        Column* c = column->column_pointer.column;
+        const int32_t* d;
+        if (column_device(c, &d, ret_status) || ensure_ws(0, ret_status)) return NULL;
+        int rc = mq_reduce(d, c->row_count, (mq_agg*)g_small, g_ws, g_ws_bytes, g_stream);
+        if (rc) {
+            fail(ret_status, "sum(column)", rc);
+            return NULL;
+        }
+        if (read_agg(&a, ret_status)) return NULL;
+    }
+    long* out = (long*)malloc(sizeof(long));
+    *out = (long)a.sum;
+    ret_status->code = OK;
+    return new_result(LONG, 1, out);
+}
+
+static Result* elementwise(Result* a, Result* b, Status* st, int is_sub) {
+    if (ready(st)) return NULL;
+    size_t n = a->num_tuples;
+    const int32_t *da, *db;
+    if (result_device(a, &da, st) || result_device(b, &db, st) || ensure_ws(n, st)) return NULL;
+    if (b->num_tuples < n) {
+        fprintf(stderr, "libmq: %s: second operand has %zu < %zu rows\n", is_sub ? "sub" : "add",
+                b->num_tuples, n);
+        st->code = ERROR;
+        return NULL;
+    }
+    int rc = is_sub ? mq_sub(da, db, n, (int32_t*)g_scratch, g_stream)
+                    : mq_add(da, db, n, (int32_t*)g_scratch, g_stream);
+    if (rc) {
+        fail(st, is_sub ? "sub" : "add", rc);
+        return NULL;
+    }
+    return int_result_from_device(g_scratch, n, st);
+}
+
+/* query.c:356-372 */
+Result* add(Result* column_one, Result* column_two, Status* ret_status) {
+    return elementwise(column_one, column_two, ret_status, 0);
+}
+
+/* query.c:374-390 */
+Result* sub(Result* column_one, Result* column_two, Status* ret_status) {
+    return elementwise(column_one, column_two, ret_status, 1);
+}
+
+/* query.c:392-415. The reference reads payload[0] of an empty result (garbage);
+ * libmq returns INT_MAX for an empty input. */
+Result* min(Result* column, Status* ret_status) {
+    mq_agg a;
+    if (reduce_result(column, &a, ret_status)) return NULL;
+    int* out = (int*)malloc(sizeof(int));
+    *out = a.min;
+    ret_status->code = OK;
+    return new_result(INT, 1, out);
+}
+
+/* query.c:417-437 (empty input: INT_MIN, see min) */
+Result* max(Result* column, Status* ret_status) {
+    mq_agg a;
+    if (reduce_result(column, &a, ret_status)) return NULL;
+    int* out = (int*)malloc(sizeof(int));
+    *out = a.max;
+    ret_status->code = OK;
+    return new_result(INT, 1, out);
+}
+
+/* query.c:496-583. As in the reference, every query reads `column` and uses its
+ * low/high fields as given (has_low/has_high are not consulted, query.c:474).
+ * Positions per query are ascending, which is what the reference's thread-order
+ * concatenation (query.c:563-574) produces. */
+Result** shared_select(SelectOperator* operators, int query_count, Column* column, Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    size_t n = column->row_count;
+    const int32_t* dcol;
+    if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
+    Result** out = (Result**)malloc(sizeof(Result*) * (size_t)(query_count > 0 ? query_count : 1));
+    for (int q = 0; q < query_count; q++) {
+        int32_t lo = operators[q].low, hi = operators[q].high;
+        int32_t* dst = (int32_t*)g_scratch;
+        int rc = mq_shared_select(dcol, n, &lo, &hi, 1, &dst, (uint64_t*)g_small, g_ws, g_ws_bytes,
+                                  g_stream);
+        uint64_t k = 0;
+        if (rc || read_count(&k, ret_status) ||
+            !(out[q] = int_result_from_device(g_scratch, (size_t)k, ret_status))) {
+            if (rc) fail(ret_status, "shared_select", rc);
+            for (int j = 0; j < q; j++) {
+                free(out[j]->payload);
+                free(out[j]);
+            }
+            free(out);
+            ret_status->code = ERROR;
+            return NULL;
+        }
+    }
+    ret_status->code = OK;
+    return out;
+}
+
+static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, const int32_t* d2,
+                           const int32_t* dp2, size_t n2, int swap, Status* st) {
+    uint64_t cap = 0, m = 0;
+    int rc;
+    void *o1 = NULL, *o2 = NULL;
+    /* First call sizes the output (cap 0 -> MQ_ECAP with m), second writes it. */
+    rc = mq_hash_join(d1, dp1, n1, d2, dp2, n2, NULL, NULL, 0, &m, g_stream);
+    if (rc && rc != MQ_ECAP) {
+        fail(st, "hash_join", rc);
+        return NULL;
+    }
+    if (m) {
+        cap = m;
+        if ((rc = mq_malloc(&o1, m * sizeof(int32_t))) || (rc = mq_malloc(&o2, m * sizeof(int32_t))) ||
+            (rc = mq_hash_join(d1, dp1, n1, d2, dp2, n2, (int32_t*)o1, (int32_t*)o2, cap, &m, g_stream))) {
+            mq_free(o1);
+            mq_free(o2);
+            fail(st, "hash_join", rc);
+            return NULL;
+        }
+    }
+    Result** out = (Result**)malloc(2 * sizeof(Result*));
+    out[0] = int_result_from_device(swap ? o2 : o1, (size_t)m, st);
+    out[1] = int_result_from_device(swap ? o1 : o2, (size_t)m, st);
+    mq_free(o1);
+    mq_free(o2);
+    if (!out[0] || !out[1]) {
+        st->code = ERROR;
+        return NULL;
+    }
+    st->code = OK;
+    return out;
+}
+
+/* query.c:652-696: build on column_one, probe with column_two; pairs in
+ * probe-major, build-insertion order. */
+Result** hash_join(Result* column_one, Result* position_one, Result* column_two, Result* position_two,
+                   Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    const int32_t *d1, *dp1, *d2, *dp2;
+    if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
+        result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))
+        return NULL;
+    return join_pairs(d1, dp1, column_one->num_tuples, d2, dp2, column_two->num_tuples, 0, ret_status);
+}
+
+/* query.c:585-650: outer column_one x inner column_two, outer-major with inner
+ * ascending — exactly a hash join that builds on the inner side (insertion
+ * order = inner order) and probes with the outer side, outputs swapped. */
+Result** nested_loop_join(Result* column_one, Result* position_one, Result* column_two,
+                          Result* position_two, Status* ret_status) {
+    if (ready(ret_status)) return NULL;
+    const int32_t *d1, *dp1, *d2, *dp2;
+    if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
+        result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))
+        return NULL;
+    return join_pairs(d2, dp2, column_two->num_tuples, d1, dp1, column_one->num_tuples, 1, ret_status);
+}
+
+/* query.c:245-304: host string formatting (stays on the CPU).
+ * Same formats and separators; an all-empty input yields "" (the reference
+ * returns an unterminated malloc(0) buffer there, query.c:253). */
+char* print(Result** results, int result_num, Status* ret_status) {
+    size_t total = 0;
+    for (int i = 0; i < result_num; i++) total += results[i]->num_tuples;
+    size_t cap = total * 24 + (size_t)result_num + 1;
+    char* s = (char*)malloc(cap);
+    size_t at = 0;
+    s[0] = '\0';
+    for (int i = 0; i < result_num; i++) {
+        Result* r = results[i];
+        if (i > 0) at += (size_t)snprintf(s + at, cap - at, ",");
+        for (size_t j = 0; j < r->num_tuples; j++) {
+            switch (r->data_type) {
+                case INT: at += (size_t)snprintf(s + at, cap - at, "%d", ((int*)r->payload)[j]); break;
+                case LONG: at += (size_t)snprintf(s + at, cap - at, "%ld", ((long*)r->payload)[j]); break;
+                case FLOAT: at += (size_t)snprintf(s + at, cap - at, "%.2f", (double)((float*)r->payload)[j]); break;
+                case DOUBLE: at += (size_t)snprintf(s + at, cap - at, "%.2f", ((double*)r->payload)[j]); break;
+            }
+            if (j != r->num_tuples - 1) at += (size_t)snprintf(s + at, cap - at, "\n");
+        }
+    }
+    ret_status->code = OK;
+    return s;
+}
+
+/* ------------------------------------------------------------------ */
+/* residency control                                                  */
+/* ------------------------------------------------------------------ */
+
+int mq_column_attach(Column* column, const int32_t* d_data) {
+    Status st = {OK, NULL};
+    if (ready(&st)) return MQ_ENODEV;
+    ColEntry* e = col_find(column);
+    if (e) col_drop(e);
+    if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
+    g_cols[g_ncols++] = (ColEntry){column, column->data, column->row_count, (void*)d_data, 0};
+    return MQ_OK;
+}
+
+int mq_column_upload(Column* column) {
+    Status st = {OK, NULL};
+    if (ready(&st)) return MQ_ENODEV;
+    const int32_t* d;
+    return column_device(column, &d, &st) ? MQ_EHIP : MQ_OK;
+}
+
+void mq_column_invalidate(Column* column) {
+    ColEntry* e = col_find(column);
+    if (e) col_drop(e);
+}
+
+const void* mq_result_device_ptr(const Result* result) {
+    int i = shadow_find(result->payload);
+    return i >= 0 ? g_shadows[i].dev : NULL;
+}
+
+void mq_release_all(void) {
+    while (g_ncols) col_drop(&g_cols[g_ncols - 1]);
+    while (g_nshadows) shadow_drop(g_nshadows - 1);
+    while (g_nidx) {
+        mq_free(g_idx[g_nidx - 1].d_values);
+        mq_free(g_idx[g_nidx - 1].d_positions);
+        g_nidx--;
+    }
+}
+
+double mq_transfer_seconds(int reset) {
+    double t = g_xfer_s;
+    if (reset) g_xfer_s = 0;
+    return t;
+}

@@ -1,0 +1,306 @@
+#!/usr/bin/env python3
+"""bench.py — rows/s and HBM roofline of the 1B-row int32 select+sum (BASELINE.json).
+
+A step is one pass of the hot path over one batch: range select [N/4, N/4 + N/100)
+(1 % selectivity) + count + exact int64 sum over a 1e9-row int32 column that is
+already resident in HBM (libmq mq_select_agg: k_scan + k_final). N=1 is
+BASELINE configs[1]; with --gpus G each rank scans its own 1e9-row column
+(seeds 42..42+G-1, configs[3]) and the per-rank {count, sum} are combined by one
+RCCL all-reduce inside the step ("weak" scaling). Data are synthetic
+(SURVEY.md §8(c) generator), generated on the device.
+
+  python bench.py [--gpus N --steps K --warmup W] [--rows R] [--no-cpu] [--no-extra]
+
+Rank 0 prints ONE JSON line. Roofline: algorithmic bytes 4N per scan launch ÷ the
+scan kernel's mean duration from HIP events on the launch stream. cpu_baseline:
+the reference's own query.c (oracle/_ref/libref.so) select_column -> fetch_column
+-> sum on a bounded sample, single thread, on this box's host.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import importlib.util
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "analytical-database_amd")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _load(name, path):
+    if name not in sys.modules:
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+    return sys.modules[name]
+
+
+def cpu_baseline(rows: int) -> dict:
+    """Reference CPU path on a bounded sample of the same workload (rank 0, N=1)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refcpu  # checker / baseline only
+    from refapi import Api, make_column
+
+    ns = min(rows, 250_000_000)
+    lo, hi = int(0.25 * ns), int(0.25 * ns) + int(0.01 * ns)
+    d = refcpu.gen_uniform(ns, 42, nthreads=16)
+    kind = "reference" if refcpu.have_reference() else "port"
+    times = []
+    if kind == "reference":
+        api = Api(refcpu.reference())
+        col = make_column(d)
+        for _ in range(3):
+            t0 = time.perf_counter()
+            pos = api.select_column(col, lo, hi)
+            vals = api.fetch_column(col, pos)
+            s = api.sum_result(vals)
+            times.append(time.perf_counter() - t0)
+    else:
+        for _ in range(3):
+            t0 = time.perf_counter()
+            pos = refcpu.select_scan(d, lo, hi)
+            s = refcpu.agg(refcpu.fetch(d, pos))["sum"]
+            times.append(time.perf_counter() - t0)
+    t1 = statistics.median(times)
+    # host-cores variant: row-balanced pthreads restatement (16 = this box's CPU share)
+    mt = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        c, s2 = refcpu.count_sum(d, lo, hi, nthreads=16)
+        mt.append(time.perf_counter() - t0)
+    assert s2 == s
+    return {"value": ns / t1, "unit": "rows/s", "cores": 1, "kind": kind,
+            "sample": f"{ns} rows int32 uniform [0,{ns}) seed 42, select [{lo},{hi}) -> "
+                      f"fetch -> sum, {'oracle/_ref/libref.so (reference query.c, gcc -O2)' if kind == 'reference' else 'oracle/refcpu.c -O2'}, "
+                      f"median of 3 = {t1:.3f} s",
+            "host_cores_variant": {"value": ns / statistics.median(mt), "cores": 16,
+                                   "kind": "port", "what": "refcpu rc_select_count_sum, 16 pthreads"},
+            "nproc": os.cpu_count()}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=1_000_000_000)
+    ap.add_argument("--sel", type=float, default=0.01)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the positions/config-3 legs")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    mq = _load("mq_binding", os.path.join(PKG, "mq.py"))
+    mqd = _load("mq_dist", os.path.join(PKG, "dist.py"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lib = mq.load()
+    mq.check(lib.mq_init(local), "mq_init")
+    stream = torch.cuda.Stream(device=dev)
+    sp = mq.stream_of(stream)
+    n = args.rows
+    seed = 42 + rank
+    lo = int(0.25 * n)
+    hi = lo + int(args.sel * n)
+
+    with torch.cuda.stream(stream):
+        col = torch.empty(n, dtype=torch.int32, device=dev)
+        ws_bytes = lib.mq_scan_workspace_bytes(n)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        agg = mqd.agg_tensor(dev)
+        mq.check(lib.mq_gen_uniform(col.data_ptr(), n, seed, n, sp), "gen")
+        nblk = C.c_uint32()
+
+        def step(ev0=None, ev1=None):
+            if ev0 is not None:
+                ev0.record(stream)
+            mq.check(lib.mq_select_partials(col.data_ptr(), n, 1, lo, 1, hi, ws.data_ptr(),
+                                            ws_bytes, C.byref(nblk), sp), "scan")
+            if ev1 is not None:
+                ev1.record(stream)
+            mq.check(lib.mq_combine_partials(ws.data_ptr(), nblk.value, agg.data_ptr(), sp),
+                     "combine")
+            mqd.combine_count_sum(agg)
+
+        for _ in range(args.warmup):
+            step()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(*evs[i])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kernel_ms = [a.elapsed_time(b) for a, b in evs]
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([statistics.mean(kernel_ms)], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        k_mean_ms = float(km.item())
+    else:
+        k_mean_ms = statistics.mean(kernel_ms)
+
+    # parity of the last step against the reference goldens (tests/golden/goldens.json)
+    res = mqd.unpack(agg)
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "goldens.json")))
+    parity = None
+    if n == 1_000_000_000 and abs(args.sel - 0.01) < 1e-12:
+        rows = {r["seed"]: r for r in gold["config4"]}
+        want_k = sum(rows[s]["k"] for s in range(42, 42 + world))
+        want_s = sum(rows[s]["sum"] for s in range(42, 42 + world))
+        parity = (res["count"], res["sum"]) == (want_k, want_s)
+
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold)
+
+    if rank == 0:
+        ms_step = 1e3 * elapsed / args.steps
+        gbs = 4.0 * n / (k_mean_ms * 1e-3) / 1e9
+        out = {
+            "metric": "rows/sec scanned + HBM GB/s (% of roofline), 1B-row int32 select+sum",
+            "value": world * n * args.steps / elapsed,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {"workload": ("1B-row single int32 column, range select + sum"
+                                    if world == 1 else
+                                    f"{world}x independent 1B-row select+sum, one per GPU, "
+                                    "RCCL all-reduce of {count,sum}"),
+                       "rows_per_gpu": n, "selectivity": args.sel, "low": lo, "high": hi,
+                       "parallelism": f"shard-by-query x{world}" if world > 1 else "single GPU"},
+            "hbm_gbs_step": 4.0 * n * world / (elapsed / args.steps) / 1e9 / world,
+            "roofline": {"bound": "hbm", "kernel": "k_scan<false,false,true> (mq_select_partials)",
+                         "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
+                         "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),
+                         "algorithmic_bytes_per_launch": 4 * n},
+            "parity": {"ok": parity, "count": res["count"], "sum": res["sum"]},
+            "extra": extra,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(n)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def traffic_per_launch(n: int):
+    """HBM bytes per k_scan launch from the committed rocprofv3 PMC summary (if one
+    exists for this N): FETCH_SIZE x 2 (gfx950 halving, MI355X_MICROARCH.md §HBM) +
+    WRITE_SIZE, collected in separate --pmc passes by tools/pmc_traffic.py."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        row = d.get("k_scan", {})
+        if int(row.get("rows", -1)) == n:
+            return row.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) -> dict:
+    """Secondary measurements (rank 0, N=1): the API path with positions
+    materialized (config 2's 4N+4K), and config 3 (select col0 -> fetch col1 ->
+    avg) both as the three-operator chain and fused."""
+    sp = mq.stream_of(stream)
+    out = {}
+    with torch.cuda.stream(stream):
+        pos = torch.empty(n, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        col1 = torch.empty(n, dtype=torch.int32, device=dev)
+        mq.check(lib.mq_gen_uniform(col1.data_ptr(), n, 43, n, sp), "gen")
+        agg = torch.zeros(4, dtype=torch.int64, device=dev)
+
+        def timed(fn, reps=10):
+            for _ in range(2):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps
+
+        def positions():
+            mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, lo, 1, hi, pos.data_ptr(),
+                                             cnt.data_ptr(), ws.data_ptr(), ws_bytes, sp))
+
+        t_pos = timed(positions)
+        k = int(cnt.item())
+        vals = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+
+        def chain():
+            positions()
+            mq.check(lib.mq_fetch(col1.data_ptr(), pos.data_ptr(), k, vals.data_ptr(), sp))
+            mq.check(lib.mq_reduce(vals.data_ptr(), k, agg.data_ptr(), ws.data_ptr(), ws_bytes, sp))
+
+        t_chain = timed(chain)
+        a = agg.cpu()
+        c3 = [r for r in gold["config3"] if r["n"] == n]
+        chain_ok = bool(c3) and (int(a[0]), int(a[1])) == (c3[0]["k"], c3[0]["sum"])
+
+        def fused():
+            mq.check(lib.mq_select_fetch_agg(col.data_ptr(), col1.data_ptr(), n, 1, lo, 1, hi,
+                                             agg.data_ptr(), ws.data_ptr(), ws_bytes, sp))
+
+        t_fused = timed(fused)
+        a2 = agg.cpu()
+        fused_ok = bool(c3) and (int(a2[0]), int(a2[1])) == (c3[0]["k"], c3[0]["sum"])
+        out["config2_positions"] = {
+            "ms": t_pos, "rows_per_s": n / (t_pos * 1e-3), "k": k,
+            "algorithmic_bytes": 4 * n + 4 * k,
+            "gbs_algorithmic": (4 * n + 4 * k) / (t_pos * 1e-3) / 1e9,
+            "hbm_bytes_design": 4 * n + n // 4 + 4 * k,
+            "note": "k_scan<mask> (4N read + N/8 bit write) + k_compact (N/8 read + 4K write)"}
+        out["config3_chain"] = {
+            "ms": t_chain, "rows_per_s": n / (t_chain * 1e-3), "parity": chain_ok,
+            "avg": (int(a[1]) / int(a[0])) if int(a[0]) else None,
+            "algorithmic_bytes": 4 * n + 12 * k}
+        out["config3_fused"] = {
+            "ms": t_fused, "rows_per_s": n / (t_fused * 1e-3), "parity": fused_ok,
+            "algorithmic_bytes": 4 * n + 8 * k,
+            "note": "select col0 + gather col1 at matches, one kernel"}
+        del pos, col1, vals
+    return out
+
+
+if __name__ == "__main__":
+    main()

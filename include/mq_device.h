@@ -1,0 +1,134 @@
+/*
+ * mq_device.h — device-level C-ABI of libmq (MI355X / gfx950 column-scan executor).
+ *
+ * Plain pointers, sizes and a `void* stream` (a hipStream_t; NULL = the HIP null
+ * stream; mq_default_stream() returns the library's own non-blocking stream). Every column / position pointer below is a DEVICE
+ * pointer into HBM. All functions return 0 (MQ_OK) on success or a negative
+ * MQ_E* code; mq_last_error() returns a message for the calling thread's last
+ * failure. Nothing here falls back to the CPU: without a usable gfx950 device
+ * every entry point returns MQ_ENODEV.
+ *
+ * Predicates are the reference's half-open range select: a row v matches when
+ * (!has_low || v >= low) && (!has_high || v < high)  (src/query.c:97-127).
+ *
+ * The reference-facing drop-in (select_column, fetch_column, sum, ...) is in
+ * mq_query.h; it is implemented in C on top of these entry points.
+ */
+#ifndef MQ_DEVICE_H
+#define MQ_DEVICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    MQ_OK = 0,
+    MQ_ENODEV = -1,   /* no gfx950 device / HIP runtime unusable */
+    MQ_EINVAL = -2,   /* bad argument (NULL, misaligned, size out of range) */
+    MQ_EHIP = -3,     /* a HIP runtime call or kernel launch failed */
+    MQ_ENOMEM = -4,   /* device allocation failed */
+    MQ_ECAP = -5      /* output capacity exceeded (join) */
+};
+
+/* Aggregates returned by the reductions (device-resident, 32 bytes). */
+typedef struct mq_agg {
+    uint64_t count;   /* rows that matched */
+    int64_t sum;      /* exact int64 sum of the matched int32 values (query.c:325-354) */
+    int32_t min;      /* INT32_MAX when count == 0 */
+    int32_t max;      /* INT32_MIN when count == 0 */
+    uint64_t _pad;
+} mq_agg;
+
+/* ---- runtime ---- */
+int mq_init(int device);                 /* select/initialise a device; idempotent */
+int mq_device_count(void);
+const char* mq_last_error(void);
+const char* mq_version(void);
+int mq_malloc(void** dptr, size_t bytes);
+int mq_free(void* dptr);
+int mq_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int mq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+int mq_memset(void* dptr, int value, size_t bytes, void* stream);
+int mq_stream_sync(void* stream);
+void* mq_default_stream(void);
+
+/* Workspace (device bytes) needed by the scan entry points for n rows. */
+size_t mq_scan_workspace_bytes(uint64_t n);
+/* The library's grid for a scan of n rows: blocks launched and rows per block. */
+void mq_scan_geometry(uint64_t n, uint32_t* blocks, uint64_t* rows_per_block);
+
+/* ---- synthetic data (bench/tests; SURVEY.md §8(c) generator) ---- */
+/* out[i] = (int32)(sm64(seed*0x100000001B3 + i) % modulus) */
+int mq_gen_uniform(int32_t* d_out, uint64_t n, uint64_t seed, uint64_t modulus, void* stream);
+/* hash-join keys of SURVEY §8(c) config 5 (kind 0 = build mix31(i), 1 = probe) and iota */
+int mq_gen_join_keys(int32_t* d_out, uint64_t n, int kind, void* stream);
+int mq_gen_iota(int32_t* d_out, uint64_t n, void* stream);
+
+/* ---- S1/S7 fused: count + int64 sum (+min/max) of rows of d_col in range ----
+ * One HBM pass over d_col (4n bytes). *d_out receives the aggregate. */
+int mq_select_agg(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                  int32_t high, mq_agg* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
+/* The two launches of mq_select_agg, for callers that time the scan kernel alone:
+ * mq_select_partials writes one partial per block into d_ws (and *nblocks);
+ * mq_combine_partials folds nblocks partials from d_ws into *d_out. */
+int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                       int32_t high, void* d_ws, size_t ws_bytes, uint32_t* nblocks, void* stream);
+int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream);
+
+/* Config-3 fused: aggregate of d_val[i] over rows i where d_sel[i] is in range. */
+int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,
+                        int32_t low, int has_high, int32_t high, mq_agg* d_out, void* d_ws,
+                        size_t ws_bytes, void* stream);
+
+/* ---- S1 select_column_scan / S4 select_result: ordered compaction ----
+ * Writes, in ascending i, d_payload ? d_payload[i] : i for every i whose d_col[i]
+ * is in range, into d_pos_out (capacity n). *d_count receives K.
+ * n must be < 2^31 (positions are int32, query.c:94). */
+int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int has_low,
+                        int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
+                        uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream);
+
+/* ---- S6 select_column_sorted_index (query.c:143-198) ----
+ * d_values: n int32 sorted ascending; d_positions: n size_t row ids. Restates the
+ * reference's binary_search + run adjustment exactly (including its low == high
+ * quirk), writes the run's positions (as int32) to d_pos_out, K to *d_count. */
+int mq_index_select(const int32_t* d_values, const uint64_t* d_positions, uint64_t n, int32_t low,
+                    int32_t high, int32_t* d_pos_out, uint64_t* d_count, void* stream);
+
+/* ---- S5 fetch_column: d_out[i] = d_col[d_pos[i]] ---- */
+int mq_fetch(const int32_t* d_col, const int32_t* d_pos, uint64_t k, int32_t* d_out, void* stream);
+
+/* ---- S7/S8/S9 over a values vector (sum/avg/min/max of a Result) ---- */
+int mq_reduce(const int32_t* d_vals, uint64_t n, mq_agg* d_out, void* d_ws, size_t ws_bytes,
+              void* stream);
+
+/* ---- S10 add / sub (int32, two's-complement wrap) ---- */
+int mq_add(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
+int mq_sub(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
+
+/* ---- S11 shared_select: q range predicates over one column ----
+ * d_lows/d_highs: q int32 bounds (device), has_low/has_high ignored as in
+ * query.c:472-479. d_pos_out[j] (host array of q device pointers, each capacity n)
+ * receives query j's ascending positions; d_counts[j] (device) its K_j. */
+size_t mq_shared_select_workspace_bytes(uint64_t n, int q);
+int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
+                     const int32_t* h_highs, int q, int32_t* const* d_pos_out,
+                     uint64_t* d_counts, void* d_ws, size_t ws_bytes, void* stream);
+
+/* ---- J1 hash_join: build on (c1,p1) (n1 rows), probe with (c2,p2) (n2 rows) ----
+ * Output pairs (out1[m], out2[m]) = (build position, probe position) in
+ * probe-major, build-insertion order (query.c:652-696). *h_m receives M.
+ * Returns MQ_ECAP (with *h_m = M) when M > cap. Allocates its own scratch. */
+int mq_hash_join(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, const int32_t* d_c2,
+                 const int32_t* d_p2, uint64_t n2, int32_t* d_out1, int32_t* d_out2,
+                 uint64_t cap, uint64_t* h_m, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,149 @@
+/*
+ * mq_query.h — libmq's drop-in for the reference's operator API.
+ *
+ * libmq exports exactly the symbols of siyaoL1/Analytical-Database
+ * src/include/query.h:20-50, with identical C signatures and struct layouts, so
+ * the reference's server.o parse.o client_context.o db_manager.o index.o utils.o
+ * link against libmq.so in place of query.o multimap.o (src/Makefile:62).
+ * Each entry point below cites the reference function it replaces.
+ *
+ * The types are re-declared here layout-for-layout from
+ * src/include/cs165_api.h:77-92,110-116,152-215 and src/include/db_manager.h:95-108;
+ * mq_query.c pins every size and offset with _Static_assert (x86-64 SysV).
+ * The reference's own headers stay authoritative for its translation units;
+ * this header is what libmq itself is compiled against.
+ *
+ * Ownership (reference contract, client_context.c:31-90, server.c:432):
+ * every returned Result / Result** and every payload is malloc'd host memory
+ * that the caller frees with free(). Inputs are borrowed.
+ * Device residency: a Column's rows are uploaded to HBM on first use and cached
+ * until mq_column_invalidate(); Results produced by libmq keep a device shadow
+ * so a following fetch/sum/avg/select_result on them does not re-upload.
+ */
+#ifndef MQ_QUERY_H
+#define MQ_QUERY_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference ABI types (cs165_api.h) ---- */
+#define MQ_MAX_SIZE_NAME 64
+#define MQ_HANDLE_MAX_SIZE 64
+
+typedef enum DataType { INT, LONG, FLOAT, DOUBLE } DataType;          /* cs165_api.h:110-115 */
+
+typedef struct ColumnIndex {                                          /* cs165_api.h:117-120 */
+    int* values;
+    size_t* positions;
+} ColumnIndex;
+
+struct Node;       /* btree node, opaque here (btree.h) */
+struct Histogram;  /* opaque here (cs165_api.h:123-127) */
+
+typedef struct Column {                                               /* cs165_api.h:129-144 */
+    char name[MQ_MAX_SIZE_NAME];
+    int* data;
+    int fd;
+    size_t row_count;
+    bool sorted;
+    bool clustered;
+    bool has_index;
+    ColumnIndex* index;
+    struct Node* btree_node;
+    struct Histogram* histogram;
+    int max;
+    int min;
+} Column;
+
+typedef enum StatusCode { OK, ERROR } StatusCode;                    /* cs165_api.h:204-209 */
+
+typedef struct Status {                                               /* cs165_api.h:212-215 */
+    StatusCode code;
+    char* error_message;
+} Status;
+
+typedef struct Result {                                               /* cs165_api.h:231-235 */
+    size_t num_tuples;
+    DataType data_type;
+    void* payload;
+} Result;
+
+typedef enum GeneralizedColumnType { RESULT, COLUMN } GeneralizedColumnType;  /* :240-243 */
+
+typedef union GeneralizedColumnPointer {                              /* cs165_api.h:247-250 */
+    Result* result;
+    Column* column;
+} GeneralizedColumnPointer;
+
+typedef struct GeneralizedColumn {                                    /* cs165_api.h:255-258 */
+    GeneralizedColumnType column_type;
+    GeneralizedColumnPointer column_pointer;
+} GeneralizedColumn;
+
+/* db_manager.h:95-108; only low/high/column are read by libmq (shared_select). */
+typedef struct SelectOperator {
+    int select_type;            /* SelectType enum */
+    char handle[MQ_HANDLE_MAX_SIZE];
+    int low;
+    int high;
+    int has_low;
+    int has_high;
+    void* db;
+    void* table;
+    Column* column;
+    Result* col_result;
+    Result* pos_result;
+    void* comparator;
+} SelectOperator;
+
+/* ---- the reference operator API (query.h:20-50) ---- */
+Result* select_result(Result* column, Result* position, int* low_pointer, int* high_pointer,
+                      Status* ret_status);                          /* query.c:38-86   */
+Result* select_column(Column* column, int* low, int* high, Status* ret_status); /* :203-220 */
+Result* fetch_column(Column* column, Result* position_result, Status* ret_status); /* :223-243 */
+char* print(Result** result, int result_num, Status* ret_status);  /* query.c:245-304 */
+Result* average(Result* column, Status* ret_status);                /* query.c:306-323 */
+Result* sum(GeneralizedColumn* column, Status* ret_status);          /* query.c:325-354 */
+Result* add(Result* column_one, Result* column_two, Status* ret_status);   /* :356-372 */
+Result* sub(Result* column_one, Result* column_two, Status* ret_status);   /* :374-390 */
+Result* min(Result* column, Status* ret_status);                    /* query.c:392-415 */
+Result* max(Result* column, Status* ret_status);                    /* query.c:417-437 */
+Result** shared_select(SelectOperator* operators, int query_count, Column* column,
+                       Status* ret_status);                         /* query.c:496-583 */
+Result** nested_loop_join(Result* column_one, Result* position_one, Result* column_two,
+                          Result* position_two, Status* ret_status); /* query.c:585-650 */
+Result** hash_join(Result* column_one, Result* position_one, Result* column_two,
+                   Result* position_two, Status* ret_status);       /* query.c:652-696 */
+void log_result(Result* result);                                    /* query.c:26-36   */
+/* also global (undeclared in query.h) in the reference: */
+Result* select_column_scan(Column* column, int* low_pointer, int* high_pointer,
+                           Status* ret_status);                     /* query.c:92-137  */
+Result* select_column_sorted_index(Column* column, int low, int high,
+                                   Status* ret_status);             /* query.c:165-198 */
+/* index.c:180-185 — exported weak so the reference's index.o definition wins. */
+bool should_use_index(Column* column, int low, int high);
+
+/* ---- libmq residency control (not in the reference) ---- */
+/* Use an existing device copy of column->data (row_count int32 rows in HBM); the
+ * caller keeps ownership of d_data and must keep it alive while attached. */
+int mq_column_attach(Column* column, const int32_t* d_data);
+/* Upload column->data now (otherwise done lazily on first use). */
+int mq_column_upload(Column* column);
+/* Forget the device copy (call after insert_row / reorder / remap of the column). */
+void mq_column_invalidate(Column* column);
+/* Device pointer of a libmq-produced Result's shadow copy, or NULL. */
+const void* mq_result_device_ptr(const Result* result);
+/* Drop every cached device copy. */
+void mq_release_all(void);
+/* Seconds spent in host<->device copies by the query API since the last reset. */
+double mq_transfer_seconds(int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,499 @@
+/*
+ * refcpu.c — CPU restatement of siyaoL1/Analytical-Database's select / fetch /
+ * aggregate / join hot path. ORACLE AND CPU BASELINE ONLY: this file is test
+ * infrastructure (tests/, __graft_entry__.smoke(), bench.py cpu_baseline). It is
+ * never linked into libmq and the product path never calls it.
+ *
+ * Each function cites the reference loop it restates (paths relative to the
+ * reference repository root). Semantics kept exactly:
+ *   - select is half-open  low <= v < high, NULL bound = unbounded
+ *     (src/query.c:97-127), positions are int32 in ascending row order;
+ *   - sum accumulates int32 into a 64-bit `long` (src/query.c:325-354);
+ *   - avg = (double)int64_sum / (double)n (src/query.c:306-323);
+ *   - hash_join emits (build_pos, probe_pos) in probe-major, build-insertion
+ *     order (src/query.c:652-696 over src/multimap.c:41-102).
+ * The restatement is pinned against oracle/_ref/libref.so (the reference's own
+ * query.c/multimap.c compiled by oracle/Makefile) by tests/test_oracle.py.
+ */
+#define _GNU_SOURCE
+#include "refcpu.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* synthetic data: SURVEY.md §8(c)                                     */
+/* ------------------------------------------------------------------ */
+
+uint64_t rc_sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+uint32_t rc_mix31(uint32_t x) {
+    const uint32_t M = 0x7FFFFFFFu;
+    x &= M;
+    x = (uint32_t)(((uint64_t)x * 0x2545F491u) & M);
+    x ^= x >> 15;
+    x = (uint32_t)(((uint64_t)x * 0x4F6CDD1Du) & M);
+    x ^= x >> 13;
+    x = (uint32_t)(((uint64_t)x * 0x6A09E667u) & M);
+    x ^= x >> 16;
+    return x;
+}
+
+typedef struct {
+    int32_t* out;
+    size_t lo, hi;
+    uint64_t base, modulus;
+} gen_arg;
+
+static void* gen_worker(void* p) {
+    gen_arg* a = (gen_arg*)p;
+    for (size_t i = a->lo; i < a->hi; i++)
+        a->out[i] = (int32_t)(rc_sm64(a->base + (uint64_t)i) % a->modulus);
+    return NULL;
+}
+
+void rc_gen_uniform(int32_t* out, size_t n, uint64_t seed, uint64_t modulus, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    gen_arg args[256];
+    uint64_t base = seed * 0x100000001B3ull;
+    size_t chunk = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * chunk, hi = lo + chunk;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        args[t] = (gen_arg){out, lo, hi, base, modulus};
+        pthread_create(&th[t], NULL, gen_worker, &args[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+void rc_gen_join_build(int32_t* out, size_t n) {
+    for (size_t i = 0; i < n; i++) out[i] = (int32_t)rc_mix31((uint32_t)i);
+}
+
+void rc_gen_join_probe(int32_t* out, size_t n) {
+    uint64_t mask = 2 * (uint64_t)n - 1;
+    for (size_t j = 0; j < n; j++)
+        out[j] = (int32_t)rc_mix31((uint32_t)(rc_sm64((7ull << 40) | (uint64_t)j) & mask));
+}
+
+void rc_iota(int32_t* out, size_t n) {
+    for (size_t i = 0; i < n; i++) out[i] = (int32_t)i;
+}
+
+uint64_t rc_fnv1a64(const void* p, size_t bytes) {
+    const unsigned char* b = (const unsigned char*)p;
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < bytes; i++) {
+        h ^= b[i];
+        h *= 0x100000001B3ull;
+    }
+    return h;
+}
+
+uint64_t rc_fnv1a64_pairs(const int32_t* a, const int32_t* b, size_t m) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < m; i++) {
+        int32_t pr[2] = {a[i], b[i]};
+        const unsigned char* c = (const unsigned char*)pr;
+        for (int k = 0; k < 8; k++) {
+            h ^= c[k];
+            h *= 0x100000001B3ull;
+        }
+    }
+    return h;
+}
+
+/* ------------------------------------------------------------------ */
+/* select                                                              */
+/* ------------------------------------------------------------------ */
+
+/* src/query.c:92-137 select_column_scan: four bound cases, positions in row order. */
+size_t rc_select_scan(const int32_t* data, size_t n, const int32_t* low, const int32_t* high,
+                      int32_t* pos_out) {
+    size_t k = 0;
+    if (low && high) {                               /* query.c:97-104 */
+        int32_t lo = *low, hi = *high;
+        for (size_t i = 0; i < n; i++)
+            if (data[i] >= lo && data[i] < hi) pos_out[k++] = (int32_t)i;
+    } else if (!low && high) {                       /* query.c:105-112 */
+        int32_t hi = *high;
+        for (size_t i = 0; i < n; i++)
+            if (data[i] < hi) pos_out[k++] = (int32_t)i;
+    } else if (low && !high) {                       /* query.c:113-120 */
+        int32_t lo = *low;
+        for (size_t i = 0; i < n; i++)
+            if (data[i] >= lo) pos_out[k++] = (int32_t)i;
+    } else {                                         /* query.c:121-127 */
+        for (size_t i = 0; i < n; i++) pos_out[i] = (int32_t)i;
+        k = n;
+    }
+    return k;
+}
+
+typedef struct {
+    const int32_t* data;
+    size_t lo, hi;
+    const int32_t *low, *high;
+    int32_t* buf;
+    size_t k;
+} scan_arg;
+
+static void* scan_worker(void* p) {
+    scan_arg* a = (scan_arg*)p;
+    size_t k = rc_select_scan(a->data + a->lo, a->hi - a->lo, a->low, a->high, a->buf);
+    for (size_t i = 0; i < k; i++) a->buf[i] += (int32_t)a->lo;
+    a->k = k;
+    return NULL;
+}
+
+/* Row-balanced nthreads split of select_column_scan; per-thread lists are
+ * concatenated in thread order, as shared_select does (query.c:563-574). */
+size_t rc_select_scan_mt(const int32_t* data, size_t n, const int32_t* low, const int32_t* high,
+                         int32_t* pos_out, int nthreads) {
+    if (nthreads <= 1) return rc_select_scan(data, n, low, high, pos_out);
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    scan_arg args[256];
+    size_t chunk = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * chunk, hi = lo + chunk;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        /* thread t writes into pos_out+lo (its rows' own slice), compacted below */
+        args[t] = (scan_arg){data, lo, hi, low, high, pos_out + lo, 0};
+        pthread_create(&th[t], NULL, scan_worker, &args[t]);
+    }
+    size_t k = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (pos_out + k != args[t].buf) memmove(pos_out + k, args[t].buf, args[t].k * sizeof(int32_t));
+        k += args[t].k;
+    }
+    return k;
+}
+
+/* src/query.c:38-86 select_result: filter fetched values, emit the matching prior positions. */
+size_t rc_select_result(const int32_t* vals, const int32_t* prev_pos, size_t n,
+                        const int32_t* low, const int32_t* high, int32_t* pos_out) {
+    size_t k = 0;
+    if (low && high) {                               /* query.c:45-52 */
+        int32_t lo = *low, hi = *high;
+        for (size_t i = 0; i < n; i++)
+            if (vals[i] >= lo && vals[i] < hi) pos_out[k++] = prev_pos[i];
+    } else if (!low && high) {                       /* query.c:53-60 */
+        int32_t hi = *high;
+        for (size_t i = 0; i < n; i++)
+            if (vals[i] < hi) pos_out[k++] = prev_pos[i];
+    } else if (low && !high) {                       /* query.c:61-68 */
+        int32_t lo = *low;
+        for (size_t i = 0; i < n; i++)
+            if (vals[i] >= lo) pos_out[k++] = prev_pos[i];
+    } else {                                         /* query.c:69-75 */
+        for (size_t i = 0; i < n; i++) pos_out[i] = prev_pos[i];
+        k = n;
+    }
+    return k;
+}
+
+/* ------------------------------------------------------------------ */
+/* fetch / aggregates / elementwise                                    */
+/* ------------------------------------------------------------------ */
+
+/* src/query.c:223-243 fetch_column: values[i] = column->data[position[i]] */
+void rc_fetch(const int32_t* col, const int32_t* pos, size_t k, int32_t* out) {
+    for (size_t i = 0; i < k; i++) out[i] = col[pos[i]];
+}
+
+/* src/query.c:325-354 sum: `long` (int64) accumulator over int32 */
+int64_t rc_sum(const int32_t* v, size_t n) {
+    int64_t s = 0;
+    for (size_t i = 0; i < n; i++) s += v[i];
+    return s;
+}
+
+/* src/query.c:306-323 average: one double division of the int64 sum (n=0 -> NaN) */
+double rc_avg(const int32_t* v, size_t n) {
+    int64_t s = rc_sum(v, n);
+    return (double)s / (double)n;
+}
+
+/* src/query.c:392-415 min. The reference seeds from payload[0] even when n == 0
+ * (reads uninitialised memory); the restatement returns INT32_MAX for n == 0. */
+int32_t rc_min(const int32_t* v, size_t n) {
+    if (n == 0) return INT32_MAX;
+    int32_t m = v[0];
+    for (size_t i = 0; i < n; i++)
+        if (m > v[i]) m = v[i];
+    return m;
+}
+
+/* src/query.c:417-437 max (n == 0: INT32_MIN, see rc_min) */
+int32_t rc_max(const int32_t* v, size_t n) {
+    if (n == 0) return INT32_MIN;
+    int32_t m = v[0];
+    for (size_t i = 0; i < n; i++)
+        if (m < v[i]) m = v[i];
+    return m;
+}
+
+/* src/query.c:356-372 add (two's-complement wrap; the reference's signed overflow is UB) */
+void rc_add(const int32_t* a, const int32_t* b, size_t n, int32_t* out) {
+    for (size_t i = 0; i < n; i++) out[i] = (int32_t)((uint32_t)a[i] + (uint32_t)b[i]);
+}
+
+/* src/query.c:374-390 sub (wrap, as rc_add) */
+void rc_sub(const int32_t* a, const int32_t* b, size_t n, int32_t* out) {
+    for (size_t i = 0; i < n; i++) out[i] = (int32_t)((uint32_t)a[i] - (uint32_t)b[i]);
+}
+
+typedef struct {
+    const int32_t* data;
+    size_t lo, hi;
+    int has_lo, has_hi;
+    int32_t low, high;
+    uint64_t count;
+    int64_t sum;
+} cs_arg;
+
+static void* cs_worker(void* p) {
+    cs_arg* a = (cs_arg*)p;
+    uint64_t c = 0;
+    int64_t s = 0;
+    for (size_t i = a->lo; i < a->hi; i++) {
+        int32_t v = a->data[i];
+        int ok = (!a->has_lo || v >= a->low) && (!a->has_hi || v < a->high);
+        if (ok) {
+            c++;
+            s += v;
+        }
+    }
+    a->count = c;
+    a->sum = s;
+    return NULL;
+}
+
+/* The composition select_column_scan -> fetch_column -> sum over the same
+ * column (query.c:92-137, 223-243, 325-354) collapsed into one pass. */
+void rc_select_count_sum(const int32_t* data, size_t n, const int32_t* low, const int32_t* high,
+                         uint64_t* count, int64_t* sum, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    cs_arg args[256];
+    size_t chunk = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * chunk, hi = lo + chunk;
+        if (lo > n) lo = n;
+        if (hi > n) hi = n;
+        args[t] = (cs_arg){data, lo, hi, low != NULL, high != NULL, low ? *low : 0, high ? *high : 0, 0, 0};
+        if (nthreads == 1) cs_worker(&args[t]);
+        else pthread_create(&th[t], NULL, cs_worker, &args[t]);
+    }
+    uint64_t c = 0;
+    int64_t s = 0;
+    for (int t = 0; t < nthreads; t++) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        c += args[t].count;
+        s += args[t].sum;
+    }
+    *count = c;
+    *sum = s;
+}
+
+/* ------------------------------------------------------------------ */
+/* shared_select (batched scan)                                        */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    const int32_t* data;
+    size_t lo, hi;
+    const int32_t *lows, *highs;
+    int q;
+    int32_t** bufs;  /* q buffers of (hi-lo) entries */
+    size_t* ks;
+} ss_arg;
+
+/* src/query.c:450-494 select_task: row-major loop, q predicates per value
+ * (has_low/has_high are ignored there; lows/highs are used as given). */
+static void* ss_worker(void* p) {
+    ss_arg* a = (ss_arg*)p;
+    for (int qq = 0; qq < a->q; qq++) a->ks[qq] = 0;
+    for (size_t row = a->lo; row < a->hi; row++) {
+        int32_t v = a->data[row];
+        for (int qq = 0; qq < a->q; qq++)
+            if (v >= a->lows[qq] && v < a->highs[qq]) a->bufs[qq][a->ks[qq]++] = (int32_t)row;
+    }
+    return NULL;
+}
+
+/* src/query.c:496-583 shared_select. split=1 reproduces the value-range split
+ * of query.c:506-522 (3 tasks of (max-min)/3 rows, the last to row_count);
+ * split=0 uses nthreads row-balanced tasks. Results concatenate in task
+ * order (query.c:563-574), i.e. ascending rows. Returns 0, or -1 on an
+ * invalid value-range split (the reference reads past the column there). */
+int rc_shared_select(const int32_t* data, size_t n, const int32_t* lows, const int32_t* highs,
+                     int q, int32_t** pos_out, size_t* counts, int nthreads, int split,
+                     int32_t col_min, int32_t col_max) {
+    size_t starts[257], ends[257];
+    int T;
+    if (split == 1) {
+        T = 3;
+        size_t task = (size_t)((col_max - col_min) / 3);
+        size_t cur = 0;
+        for (int t = 0; t < T; t++) {
+            starts[t] = cur;
+            cur += task;
+            ends[t] = (t == T - 1) ? n : cur;
+            if (starts[t] > n || ends[t] > n || ends[t] < starts[t]) return -1;
+        }
+    } else {
+        T = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+        size_t chunk = (n + (size_t)T - 1) / (size_t)T;
+        for (int t = 0; t < T; t++) {
+            starts[t] = (size_t)t * chunk;
+            ends[t] = starts[t] + chunk;
+            if (starts[t] > n) starts[t] = n;
+            if (ends[t] > n) ends[t] = n;
+        }
+    }
+    pthread_t th[256];
+    ss_arg args[256];
+    int32_t** bufs = (int32_t**)malloc(sizeof(int32_t*) * (size_t)T * (size_t)q);
+    size_t* ks = (size_t*)calloc((size_t)T * (size_t)q, sizeof(size_t));
+    for (int t = 0; t < T; t++) {
+        for (int qq = 0; qq < q; qq++)
+            bufs[t * q + qq] = (int32_t*)malloc(sizeof(int32_t) * (ends[t] - starts[t] + 1));
+        args[t] = (ss_arg){data, starts[t], ends[t], lows, highs, q, bufs + t * q, ks + t * q};
+        pthread_create(&th[t], NULL, ss_worker, &args[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    for (int qq = 0; qq < q; qq++) {
+        size_t cur = 0;
+        for (int t = 0; t < T; t++) {
+            memcpy(pos_out[qq] + cur, bufs[t * q + qq], ks[t * q + qq] * sizeof(int32_t));
+            cur += ks[t * q + qq];
+        }
+        counts[qq] = cur;
+    }
+    for (int i = 0; i < T * q; i++) free(bufs[i]);
+    free(bufs);
+    free(ks);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* joins                                                               */
+/* ------------------------------------------------------------------ */
+
+/* src/multimap.c:15-27 prime(): trial division; n < 2 counts as prime there. */
+static int is_prime(int32_t n) {
+    if (n < 2) return 1;
+    for (int64_t i = 2; i * i <= n; i++)
+        if (n % i == 0) return 0;
+    return 1;
+}
+
+/* src/multimap.c:30-38 get_proper_size: smallest prime >= (int)(1.3 * n) */
+int32_t rc_multimap_size(int32_t tuple_num) {
+    int32_t s = (int32_t)(1.3 * tuple_num);
+    while (!is_prime(s)) s++;
+    return s;
+}
+
+/* src/multimap.c:60-63 hash = key % size; the reference's negative index for a
+ * negative key is UB, the restatement wraps it into [0, size). */
+static inline int32_t mm_hash(int32_t key, int32_t size) {
+    int32_t h = key % size;
+    return h < 0 ? h + size : h;
+}
+
+/* src/query.c:652-696 hash_join over src/multimap.c:41-102. The multimap's
+ * per-slot growable lists are restated as one CSR array filled in insertion
+ * order, which preserves lookup_multimap's value order exactly. */
+size_t rc_hash_join(const int32_t* c1, const int32_t* p1, size_t n1,
+                    const int32_t* c2, const int32_t* p2, size_t n2,
+                    int32_t* out1, int32_t* out2, size_t cap) {
+    if (n1 == 0 || n2 == 0) return 0;
+    int32_t size = rc_multimap_size((int32_t)n1);
+    int32_t* keys = (int32_t*)malloc(sizeof(int32_t) * (size_t)size);
+    uint32_t* cnt = (uint32_t*)calloc((size_t)size, sizeof(uint32_t));
+    int32_t* slot_of = (int32_t*)malloc(sizeof(int32_t) * n1);
+    for (size_t i = 0; i < n1; i++) {                 /* insert_multimap, multimap.c:74-89 */
+        int32_t h = mm_hash(c1[i], size);
+        while (cnt[h] != 0 && keys[h] != c1[i]) h = (h + 1) % size;  /* find_index :65-71 */
+        keys[h] = c1[i];
+        cnt[h]++;
+        slot_of[i] = h;
+    }
+    uint32_t* off = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)size + 1));
+    uint32_t acc = 0;
+    for (int32_t s = 0; s < size; s++) {
+        off[s] = acc;
+        acc += cnt[s];
+    }
+    off[size] = acc;
+    int32_t* vals = (int32_t*)malloc(sizeof(int32_t) * n1);
+    uint32_t* cur = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)size);
+    memcpy(cur, off, sizeof(uint32_t) * (size_t)size);
+    for (size_t i = 0; i < n1; i++) vals[cur[slot_of[i]]++] = p1[i];
+    free(cur);
+    free(slot_of);
+    size_t m = 0;
+    int overflow = 0;
+    for (size_t j = 0; j < n2; j++) {                 /* probe loop, query.c:669-681 */
+        int32_t h = mm_hash(c2[j], size);
+        /* find_index (multimap.c:65-71) never terminates when every slot is taken
+         * and the key is absent (size == n1 for n1 <= 3 distinct keys); the
+         * restatement stops after one lap: the key is not in the map. */
+        int32_t steps = 0;
+        while (cnt[h] != 0 && keys[h] != c2[j] && steps < size) {
+            h = (h + 1) % size;
+            steps++;
+        }
+        if (steps == size || keys[h] != c2[j]) continue;
+        for (uint32_t e = off[h]; e < off[h] + cnt[h]; e++) {
+            if (out1) {
+                if (m >= cap) {
+                    overflow = 1;
+                    break;
+                }
+                out1[m] = vals[e];
+                out2[m] = p2[j];
+            }
+            m++;
+        }
+        if (overflow) break;
+    }
+    free(keys);
+    free(cnt);
+    free(off);
+    free(vals);
+    return overflow ? (size_t)-1 : m;
+}
+
+/* src/query.c:585-650 nested_loop_join: outer column_one, inner column_two. */
+size_t rc_nested_loop_join(const int32_t* c1, const int32_t* p1, size_t n1,
+                           const int32_t* c2, const int32_t* p2, size_t n2,
+                           int32_t* out1, int32_t* out2, size_t cap) {
+    size_t m = 0;
+    for (size_t i = 0; i < n1; i++)
+        for (size_t j = 0; j < n2; j++)
+            if (c1[i] == c2[j]) {
+                if (out1) {
+                    if (m >= cap) return (size_t)-1;
+                    out1[m] = p1[i];
+                    out2[m] = p2[j];
+                }
+                m++;
+            }
+    return m;
+}

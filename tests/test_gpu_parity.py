@@ -1,0 +1,345 @@
+"""libmq's HIP path vs the oracle — bit-exact (integer/index work) — on gfx950.
+
+Every test calls through the C-ABI (include/mq_device.h, include/mq_query.h):
+  * device API on seeded inputs at oracle-sized N, edge cases (empty, ragged,
+    unaligned, NULL bounds, inverted/empty/full ranges, INT32 extremes);
+  * the committed golden fixtures (tests/golden/, produced by the reference);
+  * the drop-in query API side by side with the reference's own compiled
+    query.c (oracle/_ref/libref.so) where that library is present;
+  * at BASELINE's full size (1e9 rows): goldens plus size-independent
+    properties (range additivity, sortedness, fetch-in-range).
+"""
+import ctypes as C
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from devbuf import Dev
+from refapi import Api, make_column, mq
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+I32MIN, I32MAX = -(2 ** 31), 2 ** 31 - 1
+BOUNDS = [(None, None), (10, None), (None, 10), (-5, 5), (5, 5), (7, 3), (I32MIN, I32MAX),
+          (I32MIN, None), (None, I32MAX), (I32MAX, None), (None, I32MIN), (0, 1), (-20, 20)]
+SIZES = [0, 1, 3, 5, 1023, 1024, 1025, 4096 * 4 + 3, 65536 + 7, 1 << 20, 3_000_001]
+
+
+def dbits(x):
+    return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    L = mq.load()
+    mq.check(L.mq_init(0), "mq_init")
+    return L
+
+
+def _agg(L, dcol_ptr, n, lo, hi, fused_val_ptr=None):
+    ws = Dev(L.mq_scan_workspace_bytes(n))
+    out = Dev(32)
+    hl, l, hh, h = mq.bounds(lo, hi)
+    if fused_val_ptr is None:
+        mq.check(L.mq_select_agg(dcol_ptr, n, hl, l, hh, h, out.ptr, ws.ptr, ws.nbytes, None))
+    else:
+        mq.check(L.mq_select_fetch_agg(dcol_ptr, fused_val_ptr, n, hl, l, hh, h, out.ptr, ws.ptr,
+                                       ws.nbytes, None))
+    return mq.MqAgg.from_buffer_copy(out.get(np.uint8, 32).tobytes())
+
+
+def _positions(L, dcol_ptr, n, lo, hi, payload_ptr=None):
+    ws = Dev(L.mq_scan_workspace_bytes(n))
+    pos = Dev(max(n, 1) * 4)
+    cnt = Dev(8)
+    hl, l, hh, h = mq.bounds(lo, hi)
+    mq.check(L.mq_select_positions(dcol_ptr, payload_ptr, n, hl, l, hh, h, pos.ptr, cnt.ptr, ws.ptr,
+                                   ws.nbytes, None))
+    k = int(cnt.get(np.uint64, 1)[0])
+    return pos.get(np.int32, k)
+
+
+def _data(n, seed):
+    rng = np.random.default_rng(seed)
+    d = rng.integers(-25, 25, n, dtype=np.int32)
+    if n > 8:
+        d[1], d[2], d[n - 1] = I32MIN, I32MAX, I32MAX - 1
+    return d
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_select_agg_and_positions_vs_oracle(lib, refcpu, n):
+    d = _data(n, n)
+    for off in (0, 1):  # 16-B aligned column and an unaligned (+4 B) one
+        dd = Dev.of(d, offset_elems=off)
+        for lo, hi in BOUNDS:
+            want = refcpu.select_scan(d, lo, hi)
+            got = _positions(lib, dd.ptr, n, lo, hi)
+            assert np.array_equal(got, want), (n, off, lo, hi)
+            a = _agg(lib, dd.ptr, n, lo, hi)
+            vals = d[want]
+            assert a.count == len(want), (n, off, lo, hi)
+            assert a.sum == int(vals.astype(np.int64).sum()), (n, off, lo, hi)
+            if len(vals):
+                assert (a.min, a.max) == (int(vals.min()), int(vals.max()))
+            else:
+                assert (a.min, a.max) == (I32MAX, I32MIN)
+
+
+@pytest.mark.parametrize("n", [0, 7, 4097, 200_003])
+def test_select_result_payload_vs_oracle(lib, refcpu, n):
+    rng = np.random.default_rng(n + 1)
+    vals = rng.integers(-100, 100, n, dtype=np.int32)
+    prev = np.sort(rng.choice(10 ** 7, n, replace=False)).astype(np.int32)
+    dv, dp = Dev.of(vals), Dev.of(prev)
+    for lo, hi in BOUNDS:
+        assert np.array_equal(_positions(lib, dv.ptr, n, lo, hi, dp.ptr),
+                              refcpu.select_result(vals, prev, lo, hi)), (n, lo, hi)
+
+
+@pytest.mark.parametrize("k", [0, 1, 5, 4096, 100_003])
+def test_fetch_vs_oracle(lib, refcpu, k):
+    rng = np.random.default_rng(k)
+    col = rng.integers(I32MIN, I32MAX, 500_000, dtype=np.int32)
+    pos = np.sort(rng.integers(0, len(col), k)).astype(np.int32)
+    dc, dpos, out = Dev.of(col), Dev.of(pos), Dev(max(k, 1) * 4)
+    mq.check(lib.mq_fetch(dc.ptr, dpos.ptr, k, out.ptr, None))
+    assert np.array_equal(out.get(np.int32, k), refcpu.fetch(col, pos))
+    # unaligned positions / output pointers take the scalar path
+    if k > 1:
+        dpos2 = Dev.of(pos, offset_elems=1)
+        out2 = Dev(k * 4 + 8)
+        mq.check(lib.mq_fetch(dc.ptr, dpos2.ptr, k, out2.ptr + 4, None))
+        assert np.array_equal(out2.get(np.int32, k, byte_offset=4), refcpu.fetch(col, pos))
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 1001, 1 << 18])
+def test_add_sub_vs_oracle(lib, refcpu, n):
+    rng = np.random.default_rng(n)
+    a = rng.integers(I32MIN, I32MAX, n, dtype=np.int32)
+    b = rng.integers(I32MIN, I32MAX, n, dtype=np.int32)
+    da, db, out = Dev.of(a), Dev.of(b), Dev(max(n, 1) * 4)
+    mq.check(lib.mq_add(da.ptr, db.ptr, n, out.ptr, None))
+    assert np.array_equal(out.get(np.int32, n), refcpu.add(a, b))
+    mq.check(lib.mq_sub(da.ptr, db.ptr, n, out.ptr, None))
+    assert np.array_equal(out.get(np.int32, n), refcpu.sub(a, b))
+
+
+def test_fused_select_fetch_agg_vs_oracle(lib, refcpu):
+    n = 2_000_003
+    d0, d1 = refcpu.gen_uniform(n, 42), refcpu.gen_uniform(n, 43)
+    D0, D1 = Dev.of(d0), Dev.of(d1)
+    for lo, hi in ((500_000, 520_000), (None, 1000), (0, None), (5, 5)):
+        pos = refcpu.select_scan(d0, lo, hi)
+        vals = d1[pos]
+        a = _agg(lib, D0.ptr, n, lo, hi, fused_val_ptr=D1.ptr)
+        assert a.count == len(pos) and a.sum == int(vals.astype(np.int64).sum())
+
+
+def test_generators_match_oracle(lib, refcpu):
+    n = 1 << 20
+    out = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(out.ptr, n, 42, n, None))
+    assert np.array_equal(out.get(np.int32, n), refcpu.gen_uniform(n, 42))
+    for kind, name in ((0, "build"), (1, "probe")):
+        mq.check(lib.mq_gen_join_keys(out.ptr, n, kind, None))
+        assert np.array_equal(out.get(np.int32, n), refcpu.gen_join(n, name))
+
+
+def test_golden_fixture_64k(lib):
+    d = np.fromfile(os.path.join(GOLD, "col_n65536_s42.bin"), dtype=np.int32)
+    dd = Dev.of(d)
+    for sel in (0.01, 0.5, 1.0):
+        want = np.fromfile(os.path.join(GOLD, f"pos_n65536_s42_sel{sel}.bin"), dtype=np.int32)
+        lo = int(0.25 * 65536)
+        assert np.array_equal(_positions(lib, dd.ptr, 65536, lo, lo + int(sel * 65536)), want)
+
+
+def _device_chain(lib, refcpu, n, seed, lo, hi, fetch_seed=None):
+    """select_column_scan -> fetch_column -> reduce, all on the device."""
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, seed, n, None))
+    ws = Dev(lib.mq_scan_workspace_bytes(n))
+    pos, cnt = Dev(n * 4), Dev(8)
+    mq.check(lib.mq_select_positions(col.ptr, None, n, 1, lo, 1, hi, pos.ptr, cnt.ptr, ws.ptr,
+                                     ws.nbytes, None))
+    k = int(cnt.get(np.uint64, 1)[0])
+    src = col
+    if fetch_seed is not None:
+        src = Dev(n * 4)
+        mq.check(lib.mq_gen_uniform(src.ptr, n, fetch_seed, n, None))
+    vals = Dev(max(k, 1) * 4)
+    mq.check(lib.mq_fetch(src.ptr, pos.ptr, k, vals.ptr, None))
+    out = Dev(32)
+    mq.check(lib.mq_reduce(vals.ptr, k, out.ptr, ws.ptr, ws.nbytes, None))
+    a = mq.MqAgg.from_buffer_copy(out.get(np.uint8, 32).tobytes())
+    fnv = refcpu.fnv1a64(pos.get(np.int32, k))
+    # fused paths must agree with the chain
+    fa = _agg(lib, col.ptr, n, lo, hi, None if fetch_seed is None else src.ptr)
+    assert (fa.count, fa.sum, fa.min, fa.max) == (k, a.sum, a.min, a.max)
+    return k, fnv, a
+
+
+def _check_row(r, k, fnv, a):
+    assert k == r["k"]
+    if "pos_fnv1a64" in r:
+        assert f"{fnv:016x}" == r["pos_fnv1a64"]
+    assert a.sum == r["sum"] and a.min == r["min"] and a.max == r["max"]
+    assert f"{dbits(a.sum / k):016x}" == r["avg_bits"]  # query.c:314, one double division
+
+
+def test_goldens_10m(lib, refcpu, goldens):
+    for r in goldens["select"]:
+        if r["n"] == 10_000_000:
+            _check_row(r, *_device_chain(lib, refcpu, r["n"], r["seed"], r["low"], r["high"]))
+    for r in goldens["config3"]:
+        if r["n"] == 10_000_000:
+            _check_row(r, *_device_chain(lib, refcpu, r["n"], r["seed"], r["low"], r["high"],
+                                         fetch_seed=r["fetch_seed"]))
+    n = 10_000_000
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, 42, n, None))
+    a = _agg(lib, col.ptr, n, None, None)
+    assert a.sum == goldens["column_sum"][str(n)]
+
+
+@pytest.mark.big
+def test_goldens_1e9(lib, refcpu, goldens):
+    for r in goldens["select"]:
+        if r["n"] == 1_000_000_000:
+            _check_row(r, *_device_chain(lib, refcpu, r["n"], r["seed"], r["low"], r["high"]))
+    for r in goldens["config3"]:
+        if r["n"] == 1_000_000_000:
+            _check_row(r, *_device_chain(lib, refcpu, r["n"], r["seed"], r["low"], r["high"],
+                                         fetch_seed=r["fetch_seed"]))
+
+
+@pytest.mark.big
+def test_config4_per_seed_and_combined_1e9(lib, goldens):
+    n = 1_000_000_000
+    col = Dev(n * 4)
+    tk = ts = 0
+    for r in goldens["config4"]:
+        mq.check(lib.mq_gen_uniform(col.ptr, n, r["seed"], n, None))
+        a = _agg(lib, col.ptr, n, r["low"], r["high"])
+        assert (a.count, a.sum) == (r["k"], r["sum"]), r["seed"]
+        tk += a.count
+        ts += a.sum
+    c = goldens["config4_combined"]
+    assert (tk, ts) == (c["k"], c["sum"])
+
+
+@pytest.mark.big
+def test_full_size_properties_1e9(lib):
+    """Size-independent checks at BASELINE's N: range additivity of count and sum,
+    strictly ascending positions, every fetched value inside the range."""
+    n = 1_000_000_000
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, 42, n, None))
+    whole = _agg(lib, col.ptr, n, 100_000_000, 900_000_000)
+    left = _agg(lib, col.ptr, n, 100_000_000, 400_000_000)
+    right = _agg(lib, col.ptr, n, 400_000_000, 900_000_000)
+    assert whole.count == left.count + right.count and whole.sum == left.sum + right.sum
+    everything = _agg(lib, col.ptr, n, None, None)
+    assert everything.count == n and everything.min >= 0 and everything.max < n
+    lo, hi = 123_456_789, 133_456_789
+    pos = _positions(lib, col.ptr, n, lo, hi)
+    assert len(pos) == _agg(lib, col.ptr, n, lo, hi).count
+    assert np.all(np.diff(pos.astype(np.int64)) > 0)
+    dp, vals = Dev.of(pos), Dev(len(pos) * 4)
+    mq.check(lib.mq_fetch(col.ptr, dp.ptr, len(pos), vals.ptr, None))
+    v = vals.get(np.int32, len(pos))
+    assert v.min() >= lo and v.max() < hi
+
+
+# ---------------------------------------------------------------------------
+# the drop-in query API (mq_query.c) against the reference's own query.c
+# ---------------------------------------------------------------------------
+needs_ref = pytest.mark.skipif(not os.path.exists(os.path.join(
+    os.path.dirname(HERE), "oracle", "_ref", "libref.so")), reason="oracle/_ref not built")
+
+
+@needs_ref
+@pytest.mark.parametrize("n", [5, 1025, 100_000])
+def test_query_api_vs_reference(lib, refcpu, n):
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    d = _data(n, 7 * n)
+    col = make_column(d)
+    for lo, hi in BOUNDS:
+        p_ref, p_mine = ref.select_column(col, lo, hi), mine.select_column(col, lo, hi)
+        assert np.array_equal(p_ref, p_mine), (n, lo, hi)
+        if not len(p_ref):
+            continue
+        v_ref, v_mine = ref.fetch_column(col, p_ref), mine.fetch_column(col, p_mine)
+        assert np.array_equal(v_ref, v_mine)
+        assert ref.sum_result(v_ref) == mine.sum_result(v_mine)
+        assert dbits(ref.average(v_ref)) == dbits(mine.average(v_mine))
+        assert ref.min(v_ref) == mine.min(v_mine) and ref.max(v_ref) == mine.max(v_mine)
+        assert np.array_equal(ref.select_result(v_ref, p_ref, -3, 3),
+                              mine.select_result(v_mine, p_mine, -3, 3))
+        assert np.array_equal(ref.add(v_ref, v_ref), mine.add(v_mine, v_mine))
+        assert np.array_equal(ref.sub(v_ref, p_ref), mine.sub(v_mine, p_mine))
+    assert ref.sum_column(col) == mine.sum_column(col)
+
+
+@needs_ref
+def test_query_api_shared_select_vs_reference(lib, refcpu):
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    n = 50_000
+    d = refcpu.gen_uniform(n, 5, modulus=n)
+    col = make_column(d)
+    rng = np.random.default_rng(2)
+    lows = rng.integers(0, n, 25).astype(np.int32)
+    highs = (lows + rng.integers(0, n // 4, 25)).astype(np.int32)
+    for a, b in zip(ref.shared_select(col, lows, highs), mine.shared_select(col, lows, highs)):
+        assert np.array_equal(a, b)
+
+
+@needs_ref
+def test_query_api_sorted_index_vs_reference(lib, refcpu):
+    """select_column on an indexed column takes the sorted-index path (query.c:165-220)."""
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    rng = np.random.default_rng(4)
+    d = rng.integers(0, 500, 20_000, dtype=np.int32)
+    order = np.argsort(d, kind="stable")
+    values = np.ascontiguousarray(d[order])
+    positions = np.ascontiguousarray(order.astype(np.uint64))
+    ix = mq.ColumnIndex()
+    ix.values = values.ctypes.data_as(C.POINTER(C.c_int))
+    ix.positions = positions.ctypes.data_as(C.POINTER(C.c_size_t))
+    col = make_column(d)
+    col.has_index = True
+    col.index = C.pointer(ix)
+    # low >= values[0] (the reference reads out of bounds below that)
+    for lo, hi in ((0, 10), (3, 3), (7, 2), (100, 499), (250, 251), (0, 1000), (499, 600)):
+        assert np.array_equal(ref.select_column(col, lo, hi), mine.select_column(col, lo, hi)), \
+            (lo, hi)
+
+
+@needs_ref
+@pytest.mark.parametrize("kind", ["hash", "nested"])
+def test_query_api_join_vs_reference(lib, refcpu, kind):
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    rng = np.random.default_rng(11)
+    for n1, n2, kr in ((4, 9, 3), (100, 257, 10), (3000, 2000, 50), (513, 4000, 5)):
+        c1 = rng.integers(0, kr, n1, dtype=np.int32)
+        c2 = rng.integers(0, kr, n2, dtype=np.int32)
+        p1 = rng.integers(0, 10 ** 6, n1, dtype=np.int32)
+        p2 = rng.integers(0, 10 ** 6, n2, dtype=np.int32)
+        w1, w2 = ref.join(c1, p1, c2, p2, kind)
+        g1, g2 = mine.join(c1, p1, c2, p2, kind)
+        assert np.array_equal(g1, w1) and np.array_equal(g2, w2), (kind, n1, n2, kr)
+
+
+def test_query_api_print_and_empty(lib):
+    mine = Api(lib)
+    assert mine.print([(np.array([3, -7, 12], np.int32), mq.INT),
+                       (np.array([1234567890123], np.int64), mq.LONG),
+                       (np.array([2.0 / 3.0], np.float64), mq.DOUBLE)]) == "3\n-7\n12,1234567890123,0.67"
+    assert mine.print([(np.array([], np.int32), mq.INT)]) == ""
+    col = make_column(np.arange(100, dtype=np.int32))
+    assert len(mine.select_column(col, 500, 600)) == 0
