@@ -1,0 +1,44 @@
+// mq_common.h — internal (not exported) runtime shared by libmq's HIP sources.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mq_device.h"
+
+namespace mqi {
+
+constexpr int kMaxDev = 64;
+
+struct DevState {
+    bool ready;
+    int cus;                 // compute units (256 on MI355X)
+    int scan_blocks_per_cu;  // resident k_scan blocks per CU
+    hipStream_t stream;      // library stream (mq_default_stream)
+};
+
+// Records a message for mq_last_error() and returns code.
+int set_err(int code, const char* fmt, ...);
+int current_device(int* dev);
+// Device checks (gfx950) and per-device constants, once per device.
+int ensure_ready(DevState** out);
+// Grid for a grid-stride streaming kernel of 256-thread blocks.
+uint32_t stream_grid(const DevState* s, uint64_t work_items);
+
+}  // namespace mqi
+
+#define HIPCHK(expr)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return mqi::set_err(MQ_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));     \
+    } while (0)
+
+#define LAUNCHCHK(what)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess)                                                                \
+            return mqi::set_err(MQ_EHIP, "launch of %s failed: %s", what,                    \
+                                hipGetErrorString(e_));                                      \
+    } while (0)

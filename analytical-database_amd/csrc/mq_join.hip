@@ -1,0 +1,582 @@
+// mq_join.hip — hash join (src/query.c:652-696 over src/multimap.c) for gfx950.
+//
+// Output contract (the reference's, verified in SURVEY.md §8(a) row J1): pairs
+// (build position, probe position) in probe-major order and, for one probe row,
+// in build-insertion order.
+//
+// Build (one of two paths):
+//   * unique keys (the common FK case, and config 5): every build row CAS-inserts
+//     its key into an open-addressing table (linear probing, power-of-two size
+//     >= 2 x rows, 64-bit slot words {key, occupied}); slot -> (row, 1). A second
+//     sighting of a key raises a flag and the build restarts on the general path.
+//   * duplicate keys: a stable LSD radix sort of (key, position) pairs makes each
+//     key's rows one contiguous run in insertion order; run heads insert
+//     key -> run start and run tails store the run length.
+// Probe: one lookup per probe row -> (start, len); an exclusive scan of len gives
+// each probe row's output offset; the write kernel copies the run.
+// No CPU work per row anywhere; the host only reads back the duplicate flag and M.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "mq_common.h"
+#include "mq_device.h"
+
+namespace {
+
+using namespace mqi;
+
+constexpr int kTPB = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kTPB * kScanItems;  // 4096
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kTPB * kSortItems;  // 4096
+constexpr int kRadix = 256;
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 wave_incl_scan(u64 v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u64 y = __shfl_up(v, off, 64);
+        if (lane >= off) v += y;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan: Tin[n] -> u64[n] (reduce-then-scan over 4096-element tiles)
+// ---------------------------------------------------------------------------
+template <typename Tin>
+__global__ __launch_bounds__(kTPB) void k_tile_sum(const Tin* in, uint64_t n, u64* sums) {
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
+        if (i < n) acc += (u64)in[i];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    __shared__ u64 ws[kTPB / 64];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// in and out may alias (every element is read into LDS before any is written).
+template <typename Tin>
+__global__ __launch_bounds__(kTPB) void k_tile_scan(const Tin* in, u64* out, uint64_t n,
+                                                    const u64* offs) {
+    __shared__ u64 tile[kScanTile];
+    __shared__ u64 ws[kTPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kTPB + tid;
+        tile[k * kTPB + tid] = i < n ? (u64)in[i] : 0ull;
+    }
+    __syncthreads();
+    u64 v[kScanItems];
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        v[k] = tile[tid * kScanItems + k];
+        acc += v[k];
+    }
+    const u64 incl = wave_incl_scan(acc, lane);
+    if (lane == 63) ws[wave] = incl;
+    __syncthreads();
+    u64 run = incl - acc + (offs ? offs[blockIdx.x] : 0ull);
+    for (int w = 0; w < wave; w++) run += ws[w];
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        tile[tid * kScanItems + k] = run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kTPB + tid;
+        if (i < n) out[i] = tile[k * kTPB + tid];
+    }
+}
+
+uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+// u64 elements of scratch needed by scan_exclusive(n).
+uint64_t scan_scratch_elems(uint64_t n) {
+    uint64_t total = 0;
+    while (n > (uint64_t)kScanTile) {
+        n = ceil_div(n, kScanTile);
+        total += n;
+    }
+    return total + 1;
+}
+
+template <typename Tin>
+int scan_exclusive(const Tin* in, u64* out, uint64_t n, u64* scratch, hipStream_t st) {
+    if (n == 0) return MQ_OK;
+    if (n <= (uint64_t)kScanTile) {
+        hipLaunchKernelGGL(k_tile_scan<Tin>, dim3(1), dim3(kTPB), 0, st, in, out, n,
+                           (const u64*)nullptr);
+        LAUNCHCHK("k_tile_scan");
+        return MQ_OK;
+    }
+    const uint64_t nb = ceil_div(n, kScanTile);
+    hipLaunchKernelGGL(k_tile_sum<Tin>, dim3((uint32_t)nb), dim3(kTPB), 0, st, in, n, scratch);
+    LAUNCHCHK("k_tile_sum");
+    int rc = scan_exclusive<u64>(scratch, scratch, nb, scratch + nb, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tile_scan<Tin>, dim3((uint32_t)nb), dim3(kTPB), 0, st, in, out, n,
+                       (const u64*)scratch);
+    LAUNCHCHK("k_tile_scan");
+    return MQ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// stable LSD radix sort of (u32 key, u32 value), 8-bit digits
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTPB) void k_sort_hist(const uint32_t* __restrict__ keys, uint64_t n,
+                                                    int shift, uint32_t* __restrict__ hist,
+                                                    uint32_t ntiles) {
+    __shared__ uint32_t h[kRadix];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Tile = 4 waves x 16 items x 64 lanes; wave w owns tile rows [w*1024, (w+1)*1024),
+// item k of lane l is row w*1024 + k*64 + l, so (w, k, l) order = input order.
+// Within a wave, equal digits are ranked with 8 ballots (stable); per-wave digit
+// counters in LDS carry the rank across items; a per-digit prefix over the 4
+// waves and the global offset of (digit, tile) give the destination.
+__global__ __launch_bounds__(kTPB) void k_sort_scatter(const uint32_t* __restrict__ kin,
+                                                       const uint32_t* __restrict__ vin,
+                                                       uint32_t* __restrict__ kout,
+                                                       uint32_t* __restrict__ vout, uint64_t n,
+                                                       int shift, const u64* __restrict__ goff,
+                                                       uint32_t ntiles) {
+    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    __syncthreads();
+    const uint64_t seg = (uint64_t)blockIdx.x * kSortTile + (uint64_t)wave * (64 * kSortItems);
+    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t key[kSortItems], val[kSortItems], dr[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const bool valid = i < n;
+        key[k] = valid ? kin[i] : 0u;
+        val[k] = valid ? vin[i] : 0u;
+        const uint32_t d = (key[k] >> shift) & 0xFF;
+        u64 peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const u64 m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t cur = wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[k] = (d << 16) | (cur + lt);
+    }
+    __syncthreads();
+    {  // exclusive prefix of the per-wave counts, per digit (thread tid = digit)
+        uint32_t off = 0;
+#pragma unroll
+        for (int w = 0; w < kTPB / 64; w++) {
+            const uint32_t c = wcnt[w][tid];
+            wcnt[w][tid] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        if (i < n) {
+            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
+            const u64 dest = goff[(uint64_t)d * ntiles + blockIdx.x] + wcnt[wave][d] + r;
+            kout[dest] = key[k];
+            vout[dest] = val[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// hash table: 64-bit slot words {key (low 32), occupied (bit 32)}, linear probing
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hash32(uint32_t k) {  // murmur3 finaliser
+    k ^= k >> 16;
+    k *= 0x85EBCA6Bu;
+    k ^= k >> 13;
+    k *= 0xC2B2AE35u;
+    k ^= k >> 16;
+    return k;
+}
+
+__device__ __forceinline__ u64 pack_key(int key) { return (u64)(uint32_t)key | (1ull << 32); }
+
+// Claim (or find) key's slot. Returns slot; *fresh = true if this call claimed it.
+__device__ __forceinline__ uint64_t ht_claim(u64* words, uint64_t mask, int key, bool* fresh) {
+    const u64 w = pack_key(key);
+    uint64_t h = hash32((uint32_t)key) & mask;
+    for (uint64_t step = 0; step <= mask; step++) {
+        const u64 old = atomicCAS(&words[h], 0ull, w);
+        if (old == 0ull) {
+            *fresh = true;
+            return h;
+        }
+        if (old == w) {
+            *fresh = false;
+            return h;
+        }
+        h = (h + 1) & mask;
+    }
+    *fresh = false;
+    return ~0ull;  // unreachable: the table is at most half full
+}
+
+__device__ __forceinline__ uint64_t ht_find(const u64* words, uint64_t mask, int key) {
+    const u64 w = pack_key(key);
+    uint64_t h = hash32((uint32_t)key) & mask;
+    for (uint64_t step = 0; step <= mask; step++) {
+        const u64 cur = words[h];
+        if (cur == w) return h;
+        if (cur == 0ull) return ~0ull;
+        h = (h + 1) & mask;
+    }
+    return ~0ull;
+}
+
+__global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict__ keys, uint64_t n,
+                                                           u64* words, uint32_t* __restrict__ start,
+                                                           uint32_t* __restrict__ len, uint64_t mask,
+                                                           uint32_t* __restrict__ dup) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        bool fresh;
+        const uint64_t h = ht_claim(words, mask, keys[i], &fresh);
+        if (fresh) {
+            start[h] = (uint32_t)i;
+            len[h] = 1;
+        } else {
+            *dup = 1;
+        }
+    }
+}
+
+// sorted keys are (key ^ 0x80000000); a run head claims its slot and stores the start
+__global__ __launch_bounds__(kTPB) void k_ht_insert_heads(const uint32_t* __restrict__ skeys,
+                                                          uint64_t n, u64* words,
+                                                          uint32_t* __restrict__ start,
+                                                          uint64_t mask) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = skeys[i];
+        if (i == 0 || skeys[i - 1] != k) {
+            bool fresh;
+            const uint64_t h = ht_claim(words, mask, (int)(k ^ 0x80000000u), &fresh);
+            start[h] = (uint32_t)i;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_ht_set_len(const uint32_t* __restrict__ skeys, uint64_t n,
+                                                     const u64* words,
+                                                     const uint32_t* __restrict__ start,
+                                                     uint32_t* __restrict__ len, uint64_t mask) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const uint32_t k = skeys[i];
+        if (i == n - 1 || skeys[i + 1] != k) {
+            const uint64_t h = ht_find(words, mask, (int)(k ^ 0x80000000u));
+            len[h] = (uint32_t)(i + 1 - start[h]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_flip_keys(const int* __restrict__ in, uint64_t n,
+                                                    uint32_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
+        out[i] = (uint32_t)in[i] ^ 0x80000000u;
+}
+
+__global__ __launch_bounds__(kTPB) void k_ht_probe(const int* __restrict__ pkeys, uint64_t n2,
+                                                   const u64* words,
+                                                   const uint32_t* __restrict__ start,
+                                                   const uint32_t* __restrict__ len, uint64_t mask,
+                                                   uint32_t* __restrict__ pstart,
+                                                   uint32_t* __restrict__ plen) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
+        const uint64_t h = ht_find(words, mask, pkeys[j]);
+        const bool hit = h != ~0ull;
+        pstart[j] = hit ? start[h] : 0u;
+        plen[j] = hit ? len[h] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict__ pstart,
+                                                     const uint32_t* __restrict__ plen,
+                                                     const u64* __restrict__ offs,
+                                                     const int* __restrict__ p2,
+                                                     const int* __restrict__ bpos, uint64_t n2,
+                                                     int* __restrict__ out1, int* __restrict__ out2) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
+        const uint32_t L = plen[j];
+        if (!L) continue;
+        const u64 o = offs[j];
+        const uint32_t s = pstart[j];
+        const int pp = p2[j];
+        for (uint32_t t = 0; t < L; t++) {
+            out1[o + t] = bpos[s + t];
+            out2[o + t] = pp;
+        }
+    }
+}
+
+}  // namespace
+
+// ===========================================================================
+// handle
+// ===========================================================================
+struct mq_join {
+    int device;
+    uint64_t n1, mask;
+    u64* words;
+    uint32_t* start;
+    uint32_t* len;
+    const int* bpos;       // build positions in run order (p1 itself, or sorted copy)
+    void* owned[8];        // device allocations owned by the handle
+    int nowned;
+    // probe state
+    uint64_t n2, m;
+    uint32_t* pstart;
+    uint32_t* plen;
+    u64* offs;
+    u64* scan_scratch;
+};
+
+namespace {
+
+int jalloc(mq_join* j, void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess)
+        return set_err(MQ_ENOMEM, "join: hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    j->owned[j->nowned++] = *p;
+    return MQ_OK;
+}
+
+void jfree_all(mq_join* j) {
+    for (int i = 0; i < j->nowned; i++) (void)hipFree(j->owned[i]);
+    j->nowned = 0;
+}
+
+int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, uint32_t** vals_out,
+               hipStream_t st, const DevState* s) {
+    // buffers: keys/vals double buffers, histogram, its scan, scan scratch
+    uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *hist = nullptr;
+    u64 *hscan = nullptr, *scratch = nullptr;
+    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t nh = ntiles * kRadix;
+    auto fail = [&](int rc) {
+        (void)hipFree(k1);
+        (void)hipFree(v1);
+        (void)hipFree(hist);
+        (void)hipFree(hscan);
+        (void)hipFree(scratch);
+        (void)hipFree(k0);
+        (void)hipFree(v0);
+        return rc;
+    };
+    if (hipMalloc(&k0, n * 4) || hipMalloc(&v0, n * 4) || hipMalloc(&k1, n * 4) ||
+        hipMalloc(&v1, n * 4) || hipMalloc(&hist, nh * 4) || hipMalloc(&hscan, nh * 8) ||
+        hipMalloc(&scratch, scan_scratch_elems(nh) * 8))
+        return fail(set_err(MQ_ENOMEM, "join: sort buffers (%llu rows)", (unsigned long long)n));
+    hipLaunchKernelGGL(k_flip_keys, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, n, k0);
+    if (hipMemcpyAsync(v0, p1, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(set_err(MQ_EHIP, "join: copy positions"));
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = 8 * pass;
+        hipLaunchKernelGGL(k_sort_hist, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, n, shift,
+                           hist, (uint32_t)ntiles);
+        int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
+        if (rc) return fail(rc);
+        hipLaunchKernelGGL(k_sort_scatter, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, v0, k1,
+                           v1, n, shift, hscan, (uint32_t)ntiles);
+        if (hipGetLastError() != hipSuccess) return fail(set_err(MQ_EHIP, "join: sort launch"));
+        uint32_t* t = k0;
+        k0 = k1;
+        k1 = t;
+        t = v0;
+        v0 = v1;
+        v1 = t;
+    }
+    (void)hipFree(k1);
+    (void)hipFree(v1);
+    (void)hipFree(hist);
+    (void)hipFree(hscan);
+    (void)hipFree(scratch);
+    *keys_out = k0;
+    *vals_out = v0;
+    return MQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join** out,
+                  void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!out || (n1 && (!d_c1 || !d_p1))) return set_err(MQ_EINVAL, "mq_join_build: NULL pointer");
+    if (n1 > 0x7FFFFFFFull) return set_err(MQ_EINVAL, "mq_join_build: build side over 2^31 rows");
+    hipStream_t st = (hipStream_t)stream;
+    mq_join* j = new mq_join();
+    std::memset(j, 0, sizeof(*j));
+    HIPCHK(hipGetDevice(&j->device));
+    j->n1 = n1;
+    uint64_t slots = 64;
+    while (slots < 2 * n1) slots <<= 1;
+    j->mask = slots - 1;
+    uint32_t* dflag = nullptr;
+    if ((rc = jalloc(j, (void**)&j->words, slots * 8)) ||
+        (rc = jalloc(j, (void**)&j->start, slots * 4)) ||
+        (rc = jalloc(j, (void**)&j->len, slots * 4)) || (rc = jalloc(j, (void**)&dflag, 16))) {
+        jfree_all(j);
+        delete j;
+        return rc;
+    }
+    j->bpos = d_p1;
+    if (n1) {
+        HIPCHK(hipMemsetAsync(j->words, 0, slots * 8, st));
+        HIPCHK(hipMemsetAsync(dflag, 0, 4, st));
+        hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, d_c1,
+                           n1, j->words, j->start, j->len, j->mask, dflag);
+        LAUNCHCHK("k_ht_insert_unique");
+        uint32_t dup = 0;
+        HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (dup) {  // general path: stable sort by key, runs in insertion order
+            uint32_t *skeys, *svals;
+            if ((rc = sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) {
+                jfree_all(j);
+                delete j;
+                return rc;
+            }
+            j->owned[j->nowned++] = skeys;
+            j->owned[j->nowned++] = svals;
+            j->bpos = reinterpret_cast<const int*>(svals);
+            HIPCHK(hipMemsetAsync(j->words, 0, slots * 8, st));
+            hipLaunchKernelGGL(k_ht_insert_heads, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys,
+                               n1, j->words, j->start, j->mask);
+            LAUNCHCHK("k_ht_insert_heads");
+            hipLaunchKernelGGL(k_ht_set_len, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys, n1,
+                               j->words, j->start, j->len, j->mask);
+            LAUNCHCHK("k_ht_set_len");
+        }
+    }
+    *out = j;
+    return MQ_OK;
+}
+
+int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!j || !h_m || (n2 && !d_c2)) return set_err(MQ_EINVAL, "mq_join_probe: bad argument");
+    hipStream_t st = (hipStream_t)stream;
+    (void)hipFree(j->pstart);
+    (void)hipFree(j->plen);
+    (void)hipFree(j->offs);
+    (void)hipFree(j->scan_scratch);
+    j->pstart = j->plen = nullptr;
+    j->offs = j->scan_scratch = nullptr;
+    j->n2 = n2;
+    j->m = 0;
+    *h_m = 0;
+    if (n2 == 0 || j->n1 == 0) return MQ_OK;
+    if (hipMalloc(&j->pstart, n2 * 4) || hipMalloc(&j->plen, n2 * 4) ||
+        hipMalloc(&j->offs, n2 * 8) || hipMalloc(&j->scan_scratch, scan_scratch_elems(n2) * 8))
+        return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
+    hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2, j->words,
+                       j->start, j->len, j->mask, j->pstart, j->plen);
+    LAUNCHCHK("k_ht_probe");
+    if ((rc = scan_exclusive<uint32_t>(j->plen, j->offs, n2, j->scan_scratch, st))) return rc;
+    u64 last_off = 0;
+    uint32_t last_len = 0;
+    HIPCHK(hipMemcpyAsync(&last_off, j->offs + (n2 - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last_len, j->plen + (n2 - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    j->m = last_off + last_len;
+    *h_m = j->m;
+    return MQ_OK;
+}
+
+int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_out2, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!j) return set_err(MQ_EINVAL, "mq_join_write: NULL handle");
+    if (j->m == 0) return MQ_OK;
+    if (!d_p2 || !d_out1 || !d_out2) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
+    hipLaunchKernelGGL(k_join_write, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
+                       j->pstart, j->plen, j->offs, d_p2, j->bpos, j->n2, d_out1, d_out2);
+    LAUNCHCHK("k_join_write");
+    return MQ_OK;
+}
+
+int mq_join_free(mq_join* j) {
+    if (!j) return MQ_OK;
+    (void)hipFree(j->pstart);
+    (void)hipFree(j->plen);
+    (void)hipFree(j->offs);
+    (void)hipFree(j->scan_scratch);
+    jfree_all(j);
+    delete j;
+    return MQ_OK;
+}
+
+int mq_hash_join(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, const int32_t* d_c2,
+                 const int32_t* d_p2, uint64_t n2, int32_t* d_out1, int32_t* d_out2,
+                 uint64_t cap, uint64_t* h_m, void* stream) {
+    if (!h_m) return set_err(MQ_EINVAL, "mq_hash_join: NULL h_m");
+    mq_join* j = nullptr;
+    int rc = mq_join_build(d_c1, d_p1, n1, &j, stream);
+    if (rc) return rc;
+    if ((rc = mq_join_probe(j, d_c2, n2, h_m, stream))) {
+        mq_join_free(j);
+        return rc;
+    }
+    if (*h_m > cap || !d_out1 || !d_out2) {
+        mq_join_free(j);
+        return *h_m == 0 ? MQ_OK : MQ_ECAP;
+    }
+    rc = mq_join_write(j, d_p2, d_out1, d_out2, stream);
+    if (!rc) rc = mq_stream_sync(stream);
+    mq_join_free(j);
+    return rc;
+}
+
+}  // extern "C"

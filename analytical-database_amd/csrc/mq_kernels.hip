@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "mq_common.h"
 #include "mq_device.h"
 
 namespace {
@@ -490,14 +491,19 @@ __global__ __launch_bounds__(kTPB) void k_gen_join(int* __restrict__ out, uint64
     const uint64_t mask = 2 * n - 1;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
         if (kind == 0) out[i] = (int)mix31((uint32_t)i);
-        else if (kind == 1) out[i] = (int)mix31((uint32_t)(sm64((7ull << 40) | i) & mask));
-        else out[i] = (int)i;
+        else out[i] = (int)mix31((uint32_t)(sm64((7ull << 40) | i) & mask));
     }
 }
 
-// ---------------------------------------------------------------------------
-// host side
-// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTPB) void k_iota(int* __restrict__ out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] = (int)i;
+}
+
+}  // namespace
+
+// host runtime shared with mq_join.hip (mq_common.h)
+namespace mqi {
 thread_local char g_err[512] = "";
 
 int set_err(int code, const char* fmt, ...) {
@@ -508,27 +514,6 @@ int set_err(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIPCHK(expr)                                                                       \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
-            return set_err(MQ_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
-    } while (0)
-
-#define LAUNCHCHK(what)                                                                    \
-    do {                                                                                   \
-        hipError_t e_ = hipGetLastError();                                                 \
-        if (e_ != hipSuccess)                                                              \
-            return set_err(MQ_EHIP, "launch of %s failed: %s", what, hipGetErrorString(e_)); \
-    } while (0)
-
-constexpr int kMaxDev = 64;
-struct DevState {
-    bool ready;
-    int cus;
-    int scan_blocks_per_cu;
-    hipStream_t stream;
-};
 DevState g_dev[kMaxDev];
 
 int current_device(int* dev) {
@@ -563,6 +548,18 @@ int ensure_ready(DevState** out) {
     return MQ_OK;
 }
 
+uint32_t stream_grid(const DevState* s, uint64_t work_items) {
+    uint64_t g = (work_items + kTPB - 1) / kTPB;
+    const uint64_t cap = (uint64_t)s->cus * 8;
+    if (g > cap) g = cap;
+    return (uint32_t)(g == 0 ? 1 : g);
+}
+
+}  // namespace mqi
+
+namespace {
+using namespace mqi;
+
 // Fold (has_low, low, has_high, high) into one unsigned range compare.
 // Returns false for an empty range.
 bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
@@ -594,12 +591,6 @@ size_t mask_bytes(uint64_t n) {
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-uint32_t stream_grid(const DevState* s, uint64_t work_items) {
-    uint64_t g = (work_items + kTPB - 1) / kTPB;
-    const uint64_t cap = (uint64_t)s->cus * 8;
-    if (g > cap) g = cap;
-    return (uint32_t)(g == 0 ? 1 : g);
-}
 
 int empty_agg(mq_agg* d_out, hipStream_t st) {
     mq_agg e;
@@ -777,9 +768,8 @@ int mq_gen_iota(int32_t* d_out, uint64_t n, void* stream) {
     if (rc) return rc;
     if (n == 0) return MQ_OK;
     if (!d_out) return set_err(MQ_EINVAL, "mq_gen_iota: NULL output");
-    hipLaunchKernelGGL(k_gen_join, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream,
-                       d_out, n, 2);
-    LAUNCHCHK("k_gen_join");
+    hipLaunchKernelGGL(k_iota, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream, d_out, n);
+    LAUNCHCHK("k_iota");
     return MQ_OK;
 }
 
@@ -1001,12 +991,5 @@ int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
     return MQ_OK;
 }
 
-int mq_hash_join(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, const int32_t* d_c2,
-                 const int32_t* d_p2, uint64_t n2, int32_t* d_out1, int32_t* d_out2,
-                 uint64_t cap, uint64_t* h_m, void* stream) {
-    (void)d_c1; (void)d_p1; (void)n1; (void)d_c2; (void)d_p2; (void)n2;
-    (void)d_out1; (void)d_out2; (void)cap; (void)h_m; (void)stream;
-    return set_err(MQ_EINVAL, "mq_hash_join: not built yet");
-}
 
 }  // extern "C"

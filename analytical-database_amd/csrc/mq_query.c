@@ -588,28 +588,26 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
 
 static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, const int32_t* d2,
                            const int32_t* dp2, size_t n2, int swap, Status* st) {
-    uint64_t cap = 0, m = 0;
-    int rc;
+    mq_join* jn = NULL;
+    uint64_t m = 0;
     void *o1 = NULL, *o2 = NULL;
-    /* First call sizes the output (cap 0 -> MQ_ECAP with m), second writes it. */
-    rc = mq_hash_join(d1, dp1, n1, d2, dp2, n2, NULL, NULL, 0, &m, g_stream);
-    if (rc && rc != MQ_ECAP) {
+    int rc = mq_join_build(d1, dp1, n1, &jn, g_stream);
+    if (!rc) rc = mq_join_probe(jn, d2, n2, &m, g_stream);
+    if (!rc && m) {
+        if (!(rc = mq_malloc(&o1, m * sizeof(int32_t))) && !(rc = mq_malloc(&o2, m * sizeof(int32_t))))
+            rc = mq_join_write(jn, dp2, (int32_t*)o1, (int32_t*)o2, g_stream);
+    }
+    mq_join_free(jn);
+    if (rc) {
+        mq_free(o1);
+        mq_free(o2);
         fail(st, "hash_join", rc);
         return NULL;
-    }
-    if (m) {
-        cap = m;
-        if ((rc = mq_malloc(&o1, m * sizeof(int32_t))) || (rc = mq_malloc(&o2, m * sizeof(int32_t))) ||
-            (rc = mq_hash_join(d1, dp1, n1, d2, dp2, n2, (int32_t*)o1, (int32_t*)o2, cap, &m, g_stream))) {
-            mq_free(o1);
-            mq_free(o2);
-            fail(st, "hash_join", rc);
-            return NULL;
-        }
     }
     Result** out = (Result**)malloc(2 * sizeof(Result*));
     out[0] = int_result_from_device(swap ? o2 : o1, (size_t)m, st);
     out[1] = int_result_from_device(swap ? o1 : o2, (size_t)m, st);
+    mq_stream_sync(g_stream);
     mq_free(o1);
     mq_free(o2);
     if (!out[0] || !out[1]) {

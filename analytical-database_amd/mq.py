@@ -120,6 +120,10 @@ _SIGS = {
     "mq_shared_select": (_int, [_vp, _u64, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
     "mq_hash_join": (_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, C.POINTER(_u64),
                             _vp]),
+    "mq_join_build": (_int, [_vp, _vp, _u64, C.POINTER(_vp), _vp]),
+    "mq_join_probe": (_int, [_vp, _vp, _u64, C.POINTER(_u64), _vp]),
+    "mq_join_write": (_int, [_vp, _vp, _vp, _vp, _vp]),
+    "mq_join_free": (_int, [_vp]),
     # reference API (query.h:20-50)
     "select_result": (_PR, [_PR, _PR, C.POINTER(_int), C.POINTER(_int), _PS]),
     "select_column": (_PR, [C.POINTER(Column), C.POINTER(_int), C.POINTER(_int), _PS]),

@@ -299,7 +299,64 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
             "algorithmic_bytes": 4 * n + 8 * k,
             "note": "select col0 + gather col1 at matches, one kernel"}
         del pos, col1, vals
+    out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold)
     return out
+
+
+def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28) -> dict:
+    """Config 5: 2^28 x 2^28 hash join (build + probe + pair write), keys of
+    SURVEY.md §8(c); parity = M and the FNV-1a-64 of the pairs vs the reference."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu  # checker only (pair hash)
+    n = 1 << logn
+    sp = mq.stream_of(stream)
+    with torch.cuda.stream(stream):
+        a = torch.empty(n, dtype=torch.int32, device=dev)
+        b = torch.empty(n, dtype=torch.int32, device=dev)
+        p = torch.empty(n, dtype=torch.int32, device=dev)
+        mq.check(lib.mq_gen_join_keys(a.data_ptr(), n, 0, sp))
+        mq.check(lib.mq_gen_join_keys(b.data_ptr(), n, 1, sp))
+        mq.check(lib.mq_gen_iota(p.data_ptr(), n, sp))
+        times, m = [], 0
+        o1 = o2 = None
+        for rep in range(4):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            h = C.c_void_p()
+            mq.check(lib.mq_join_build(a.data_ptr(), p.data_ptr(), n, C.byref(h), sp), "join_build")
+            mm = C.c_uint64()
+            mq.check(lib.mq_join_probe(h, b.data_ptr(), n, C.byref(mm), sp), "join_probe")
+            m = mm.value
+            if o1 is None:
+                o1 = torch.empty(m, dtype=torch.int32, device=dev)
+                o2 = torch.empty(m, dtype=torch.int32, device=dev)
+            mq.check(lib.mq_join_write(h, p.data_ptr(), o1.data_ptr(), o2.data_ptr(), sp))
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            mq.check(lib.mq_join_free(h))
+        t = statistics.median(times[1:])
+        want = [r for r in gold["join_survey"] if r["n"] == n]
+        fnv = refcpu.fnv1a64_pairs(o1.cpu().numpy(), o2.cpu().numpy())
+        ok = bool(want) and (m, f"{fnv:016x}") == (want[0]["m"], want[0]["pairs_fnv1a64"])
+        del a, b, p, o1, o2
+    res = {"n_build": n, "n_probe": n, "m": m, "ms": 1e3 * t,
+           "rows_per_s": 2 * n / t, "algorithmic_bytes": 8 * n + 8 * n + 8 * m,
+           "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9, "parity": ok,
+           "note": "wall time of build+probe+write incl. 2 host syncs (dup flag, M); "
+                   "unique-key build path (keys are a bijection)"}
+    if refcpu.have_reference():  # the reference's own join, at a size it finishes quickly
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from refapi import Api
+        api = Api(refcpu.reference())
+        k = 1 << 20
+        ka, kb, kp = refcpu.gen_join(k, "build"), refcpu.gen_join(k, "probe"), refcpu.gen_join(k, "iota")
+        t0 = time.perf_counter()
+        api.join(ka, kp, kb, kp, "hash")
+        tr = time.perf_counter() - t0
+        res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1,
+                                     "kind": "reference"}
+    return res
 
 
 if __name__ == "__main__":

@@ -120,7 +120,19 @@ int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
                      const int32_t* h_highs, int q, int32_t* const* d_pos_out,
                      uint64_t* d_counts, void* d_ws, size_t ws_bytes, void* stream);
 
-/* ---- J1 hash_join: build on (c1,p1) (n1 rows), probe with (c2,p2) (n2 rows) ----
+/* ---- J1 hash_join as three steps on a handle (lets the caller size the output) ----
+ * build: table over (c1, p1); p1 must stay valid until mq_join_free.
+ * probe: per-probe match counts + output offsets for keys c2; *h_m = M.
+ * write: the M pairs (out1 = build positions, out2 = probe positions p2). */
+typedef struct mq_join mq_join;
+int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join** out,
+                  void* stream);
+int mq_join_probe(mq_join* join, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, void* stream);
+int mq_join_write(mq_join* join, const int32_t* d_p2, int32_t* d_out1, int32_t* d_out2,
+                  void* stream);
+int mq_join_free(mq_join* join);
+
+/* ---- J1 hash_join in one call: build on (c1,p1) (n1 rows), probe with (c2,p2) (n2 rows) ----
  * Output pairs (out1[m], out2[m]) = (build position, probe position) in
  * probe-major, build-insertion order (query.c:652-696). *h_m receives M.
  * Returns MQ_ECAP (with *h_m = M) when M > cap. Allocates its own scratch. */

@@ -172,6 +172,14 @@ def main() -> None:
                             "m": int(len(o1)),
                             "pairs_fnv1a64": f"{refcpu.fnv1a64_pairs(o1, o2):016x}"})
         print("join", out["join"][-1], flush=True)
+    # 2^24 / 2^28 joins take the reference minutes to hours (per-slot mallocs); their
+    # values come from SURVEY.md §8(c) (computed there by the reference) and are
+    # re-derived by the oracle restatement in tests/test_oracle.py (2^24).
+    out["join_survey"] = [{"n": n, "kind": "hash", "m": m, "pairs_fnv1a64": f"{h:016x}",
+                           "source": "SURVEY.md §8(c), reference query.c"}
+                          for n, (m, h) in sorted({**SURVEY_JOIN,
+                                                   1 << 28: (134232477, 0x93EDF69D334A9827)}.items())
+                          if n >= 1 << 24]
     path = os.path.join(HERE, "goldens.json")
     if os.path.exists(path) and not args.big:
         old = json.load(open(path))

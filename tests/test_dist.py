@@ -1,0 +1,123 @@
+"""Multi-process (gloo, world size 2) tests of the sharded combine.
+
+The combine code (analytical-database_amd/dist.py) is the same on RCCL and gloo; here
+each rank's device aggregate is stood in for by the oracle's value for its shard,
+so the test checks the exchange itself:
+  * config 4 style: one column per rank, {count, sum} all-reduced, avg as one
+    double division -> equal to the single-process result over all columns;
+  * row sharding of one column: per-rank partials combine to the whole-column
+    aggregate (count, sum, min, max, avg bit-exact), and the per-rank position
+    lists (local row + shard base) concatenated in rank order equal the
+    single-process ascending list.
+"""
+import importlib.util
+import os
+import struct
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dist_mod():
+    spec = importlib.util.spec_from_file_location(
+        "mq_dist", os.path.join(ROOT, "analytical-database_amd", "dist.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _agg_from(count, total, mn, mx):
+    t = torch.zeros(4, dtype=torch.int64)
+    t[0], t[1] = count, total
+    t[2:3].view(torch.int32)[0] = mn
+    t[2:3].view(torch.int32)[1] = mx
+    return t
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mqd = _dist_mod()
+    out = {}
+    # config 4: rank r scans its own column (seed 42 + r)
+    n = 200_000
+    lo, hi = n // 4, n // 4 + n // 100
+    d = refcpu.gen_uniform(n, 42 + rank)
+    pos = refcpu.select_scan(d, lo, hi)
+    v = d[pos]
+    agg = _agg_from(len(pos), int(v.astype(np.int64).sum()), int(v.min()), int(v.max()))
+    out["cfg4"] = mqd.combine_full(agg)
+    # row sharding of one column
+    N = 300_001
+    col = refcpu.gen_uniform(N, 7)
+    a, b = mqd.shard_rows(N, rank, world)
+    shard = col[a:b]
+    p = refcpu.select_scan(shard, 1000, 90_000) + a
+    sv = shard[p - a]
+    agg2 = _agg_from(len(p), int(sv.astype(np.int64).sum()), int(sv.min()), int(sv.max()))
+    out["rows"] = mqd.combine_full(agg2)
+    lists = [None] * world
+    dist.all_gather_object(lists, p.tolist())
+    out["positions"] = [x for part in lists for x in part]
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_combine_matches_single_process(refcpu):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process expectations
+    n = 200_000
+    lo, hi = n // 4, n // 4 + n // 100
+    tk = ts = 0
+    mn, mx = 2 ** 31, -(2 ** 31)
+    for seed in (42, 43):
+        d = refcpu.gen_uniform(n, seed)
+        pos = refcpu.select_scan(d, lo, hi)
+        tk += len(pos)
+        ts += int(d[pos].astype(np.int64).sum())
+        mn, mx = min(mn, int(d[pos].min())), max(mx, int(d[pos].max()))
+    for r in (0, 1):
+        c = res[r]["cfg4"]
+        assert (c["count"], c["sum"], c["min"], c["max"]) == (tk, ts, mn, mx)
+        assert struct.pack("<d", c["avg"]) == struct.pack("<d", ts / tk)
+    N = 300_001
+    col = refcpu.gen_uniform(N, 7)
+    pos = refcpu.select_scan(col, 1000, 90_000)
+    a = refcpu.agg(col[pos])
+    for r in (0, 1):
+        c = res[r]["rows"]
+        assert (c["count"], c["sum"], c["min"], c["max"]) == (a["count"], a["sum"], a["min"],
+                                                              a["max"])
+        assert struct.pack("<d", c["avg"]) == struct.pack("<d", a["avg"])
+        assert np.array_equal(np.array(res[r]["positions"], dtype=np.int32), pos)
+
+
+def test_shard_rows_cover_exactly():
+    mqd = _dist_mod()
+    for n in (0, 1, 1023, 1024, 10 ** 6 + 3):
+        for w in (1, 2, 3, 8):
+            spans = [mqd.shard_rows(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b

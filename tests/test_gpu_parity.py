@@ -148,6 +148,8 @@ def test_generators_match_oracle(lib, refcpu):
     for kind, name in ((0, "build"), (1, "probe")):
         mq.check(lib.mq_gen_join_keys(out.ptr, n, kind, None))
         assert np.array_equal(out.get(np.int32, n), refcpu.gen_join(n, name))
+    mq.check(lib.mq_gen_iota(out.ptr, n, None))
+    assert np.array_equal(out.get(np.int32, n), np.arange(n, dtype=np.int32))
 
 
 def test_golden_fixture_64k(lib):
@@ -343,3 +345,84 @@ def test_query_api_print_and_empty(lib):
     assert mine.print([(np.array([], np.int32), mq.INT)]) == ""
     col = make_column(np.arange(100, dtype=np.int32))
     assert len(mine.select_column(col, 500, 600)) == 0
+
+
+# ---------------------------------------------------------------------------
+# J1 hash join (device API) vs the oracle and the reference goldens
+# ---------------------------------------------------------------------------
+def _dev_join(lib, c1, p1, c2, p2):
+    n1, n2 = len(c1), len(c2)
+    D = [Dev.of(x) for x in (c1, p1, c2, p2)]
+    h = C.c_void_p()
+    mq.check(lib.mq_join_build(D[0].ptr, D[1].ptr, n1, C.byref(h), None), "join_build")
+    m = C.c_uint64()
+    mq.check(lib.mq_join_probe(h, D[2].ptr, n2, C.byref(m), None), "join_probe")
+    m = m.value
+    o1, o2 = Dev(max(m, 1) * 4), Dev(max(m, 1) * 4)
+    mq.check(lib.mq_join_write(h, D[3].ptr, o1.ptr, o2.ptr, None), "join_write")
+    mq.check(lib.mq_join_free(h), "join_free")
+    return o1.get(np.int32, m), o2.get(np.int32, m)
+
+
+@pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty"])
+def test_hash_join_vs_oracle(lib, refcpu, case):
+    rng = np.random.default_rng(hash(case) % 1000)
+    if case == "unique":
+        c1 = rng.permutation(200_000).astype(np.int32)
+        c2 = rng.integers(0, 400_000, 150_000, dtype=np.int32)
+    elif case == "dups":
+        c1 = rng.integers(0, 5000, 100_000, dtype=np.int32)
+        c2 = rng.integers(0, 6000, 30_000, dtype=np.int32)
+    elif case == "skew":  # one huge group plus a long tail
+        c1 = np.where(rng.random(50_000) < 0.5, 7, rng.integers(0, 10 ** 6, 50_000)).astype(np.int32)
+        c2 = np.concatenate([[7, 7, 3], rng.integers(0, 10 ** 6, 2000)]).astype(np.int32)
+    elif case == "neg":
+        c1 = rng.integers(-(2 ** 31), 2 ** 31 - 1, 20_000, dtype=np.int64).astype(np.int32)
+        c1[:4] = [-(2 ** 31), 2 ** 31 - 1, 0, -1]
+        c2 = np.concatenate([c1[::3], rng.integers(-100, 100, 500)]).astype(np.int32)
+    elif case == "tiny":  # the reference's full-table hang shapes (multimap.c:65-71)
+        c1 = np.array([5, 9], dtype=np.int32)
+        c2 = np.array([1, 9, 5, 5, 2], dtype=np.int32)
+    else:
+        c1 = np.array([], dtype=np.int32)
+        c2 = np.array([1, 2], dtype=np.int32)
+    p1 = rng.integers(0, 10 ** 7, len(c1), dtype=np.int32)
+    p2 = rng.integers(0, 10 ** 7, len(c2), dtype=np.int32)
+    g1, g2 = _dev_join(lib, c1, p1, c2, p2)
+    w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
+    assert np.array_equal(g1, w1) and np.array_equal(g2, w2), case
+    if len(c2) and len(c1):  # swapped roles (nested_loop_join's build side)
+        h1, h2 = _dev_join(lib, c2, p2, c1, p1)
+        v1, v2 = refcpu.hash_join(c1, p1, c2, p2, nested=True)
+        assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
+
+
+def _join_golden(lib, refcpu, n):
+    D = {k: Dev(n * 4) for k in ("a", "b", "p")}
+    mq.check(lib.mq_gen_join_keys(D["a"].ptr, n, 0, None))
+    mq.check(lib.mq_gen_join_keys(D["b"].ptr, n, 1, None))
+    mq.check(lib.mq_gen_iota(D["p"].ptr, n, None))
+    h = C.c_void_p()
+    mq.check(lib.mq_join_build(D["a"].ptr, D["p"].ptr, n, C.byref(h), None))
+    m = C.c_uint64()
+    mq.check(lib.mq_join_probe(h, D["b"].ptr, n, C.byref(m), None))
+    m = m.value
+    o1, o2 = Dev(m * 4), Dev(m * 4)
+    mq.check(lib.mq_join_write(h, D["p"].ptr, o1.ptr, o2.ptr, None))
+    mq.check(lib.mq_join_free(h))
+    return m, refcpu.fnv1a64_pairs(o1.get(np.int32, m), o2.get(np.int32, m))
+
+
+def test_hash_join_goldens(lib, refcpu, goldens):
+    rows = [r for r in goldens["join"] if "dup" not in r] + \
+           [r for r in goldens["join_survey"] if r["n"] <= 1 << 24]
+    for r in rows:
+        m, h = _join_golden(lib, refcpu, r["n"])
+        assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"]), r["n"]
+
+
+@pytest.mark.big
+def test_hash_join_golden_2e28(lib, refcpu, goldens):
+    r = [x for x in goldens["join_survey"] if x["n"] == 1 << 28][0]
+    m, h = _join_golden(lib, refcpu, r["n"])
+    assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"])

@@ -89,6 +89,15 @@ def test_oracle_matches_join_goldens(refcpu, goldens):
         assert f"{refcpu.fnv1a64_pairs(o1, o2):016x}" == r["pairs_fnv1a64"]
 
 
+def test_oracle_reproduces_survey_join_2e24(refcpu, goldens):
+    r = [x for x in goldens["join_survey"] if x["n"] == 1 << 24][0]
+    n = r["n"]
+    p = refcpu.gen_join(n, "iota")
+    o1, o2 = refcpu.hash_join(refcpu.gen_join(n, "build"), p, refcpu.gen_join(n, "probe"), p)
+    assert len(o1) == r["m"]
+    assert f"{refcpu.fnv1a64_pairs(o1, o2):016x}" == r["pairs_fnv1a64"]
+
+
 # ---------------------------------------------------------------------------
 # restatement vs the reference build on edge cases
 # ---------------------------------------------------------------------------
