@@ -14,7 +14,6 @@ constexpr int kMaxDev = 64;
 struct DevState {
     bool ready;
     int cus;                 // compute units (256 on MI355X)
-    int scan_blocks_per_cu;  // resident k_scan blocks per CU
     hipStream_t stream;      // library stream (mq_default_stream)
 };
 

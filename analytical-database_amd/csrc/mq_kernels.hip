@@ -29,6 +29,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "mq_common.h"
@@ -39,11 +40,9 @@ namespace {
 constexpr int kTPB = 256;                 // scan block: 4 wave64
 constexpr int kWaves = kTPB / 64;
 constexpr int kTileRows = kTPB * 4;       // 1024 rows per tile (one dwordx4 per lane)
-constexpr int kUnroll = 4;                // tiles in flight per thread
+constexpr int kUnroll = 8;                // tiles in flight per thread (128 B/lane)
 constexpr int kCompactTPB = 1024;         // compaction block: 16 wave64
 constexpr int kCompactWaves = kCompactTPB / 64;
-constexpr int kGroupsPerBatch = 16;       // 16 groups (256 rows each) per wave load
-constexpr int kBatchesPerWave = 8;        // 128 groups per wave per round
 constexpr int kMaxBlocks = 8192;
 
 struct Partial {                          // 32 B, layout-identical to mq_agg
@@ -62,10 +61,8 @@ struct Pred {
     uint32_t wm1;
 };
 
-__device__ __forceinline__ bool match(int v, Pred p) { return ((uint32_t)v - p.lo) <= p.wm1; }
-
 template <bool VEC>
-__device__ __forceinline__ int4 load4(const int* __restrict__ p) {
+__device__ __forceinline__ int4 load4(const int* __restrict__ p) {  // cached (fetch / add / sub)
     if constexpr (VEC) {
         return *reinterpret_cast<const int4*>(p);
     } else {
@@ -120,16 +117,53 @@ __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long
 
 // ---------------------------------------------------------------------------
 // k_scan: one streaming pass over a contiguous chunk of the column.
-//   MASK = false: count / int64 sum / min / max of the matching values — or, with
-//                 AUX, of aux[row] for the matching rows (select -> fetch -> agg
-//                 fused, config 3). Implements query.c:92-137 + 223-243 + 306-354.
-//   MASK = true : count per block + one predicate bit per row (first half of the
-//                 ordered compaction).
+//   kSum   : count + int64 sum of the matching values (select + sum, the metric)
+//   kAgg   : count + sum + min + max                       (query.c:306-354, 392-437)
+//   kAux   : the same aggregates of aux[row] over the rows whose col[row] matches
+//            (select -> fetch -> agg fused, config 3; query.c:92-137 + 223-243)
+//   kMask  : count per block + one predicate bit per row (first half of the
+//            ordered compaction)
+// Loads are non-temporal dwordx4 (global_load_dwordx4 ... nt): the column is read
+// once, and keeping it out of the caches measured 0.586 vs 0.631 ms per 1e9 rows.
+// Arithmetic runs on d = v - low (unsigned): a row matches iff d <= wm1, so
+//   sum = sum(d) + count * low,  min = low + min(d),  max = low + wm1 - min(wm1 - d)
+// where the min()s run over ALL rows of a full tile unmasked: a non-matching row
+// has d > wm1 and wm1 - d > wm1, so it can never win.
 // Mask word layout: masks[(tile*4 + wave)*4 + e] bit l = row tile*1024 + wave*256
 // + 4*l + e, so a chunk's 256-row groups are contiguous 32-byte records.
 // ---------------------------------------------------------------------------
-template <bool MASK, bool AUX, bool VEC>
-__global__ __launch_bounds__(kTPB) void k_scan(const int* __restrict__ col,
+enum ScanMode { kSum = 0, kAgg = 1, kAux = 2, kMask = 3 };
+
+// Mask layout: per 8192-row super-tile S and wave w, a 32-word (256-B) record;
+// word u*4 + e, bit l <-> row S*8192 + u*1024 + w*256 + 4*l + e. Returns the record
+// start for the super-tile holding 1024-row tile T.
+__device__ __forceinline__ uint64_t mask_word(uint64_t T, int wave) {
+    return ((T >> 3) * kWaves + (uint64_t)wave) * 32;
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+template <bool VEC>
+__device__ __forceinline__ int4 load4_nt(const int* __restrict__ p) {
+    if constexpr (VEC) {
+        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+        return make_int4(t.x, t.y, t.z, t.w);
+    } else {
+        return make_int4(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
+                         __builtin_nontemporal_load(p + 2), __builtin_nontemporal_load(p + 3));
+    }
+}
+
+// Per-mode tiles in flight and occupancy target (waves per SIMD): 8 waves/SIMD
+// means <= 64 VGPRs, chosen where it fits without spills.
+template <int MODE>
+struct ScanTraits {
+    static constexpr int kUnrollM = MODE == kAux ? 4 : (MODE == kAgg ? 6 : kUnroll);
+    static constexpr int kMinWaves = MODE == kAux ? 4 : 8;
+};
+
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(const int* __restrict__ col,
                                                const int* __restrict__ aux, uint64_t n,
                                                uint64_t rows_per_block, Pred pred,
                                                Partial* __restrict__ part,
@@ -137,16 +171,22 @@ __global__ __launch_bounds__(kTPB) void k_scan(const int* __restrict__ col,
     const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
     uint64_t end = start + rows_per_block;
     if (end > n) end = n;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t lo = pred.lo, wm1 = pred.wm1;
 
     unsigned int cnt = 0;
-    long long sum = 0;
-    int mn = INT_MAX, mx = INT_MIN;
+    unsigned long long sumd = 0;       // kSum/kAgg: sum of d over matches
+    uint32_t mind = 0xFFFFFFFFu;       // kAgg: min d
+    uint32_t maxr = 0xFFFFFFFFu;       // kAgg: min (wm1 - d)
+    long long sumv = 0;                // kAux: sum of aux values
+    int mnv = INT_MAX, mxv = INT_MIN;  // kAux
 
+    // FULL: all 4 rows valid (no per-row bound check, unmasked min()s)
     auto consume = [&](int4 v, uint64_t tile_row, bool full) {
         const uint64_t row = tile_row + (uint64_t)tid * 4;
-        bool p0 = match(v.x, pred), p1 = match(v.y, pred), p2 = match(v.z, pred),
-             p3 = match(v.w, pred);
+        const uint32_t d0 = (uint32_t)v.x - lo, d1 = (uint32_t)v.y - lo, d2 = (uint32_t)v.z - lo,
+                       d3 = (uint32_t)v.w - lo;
+        bool p0 = d0 <= wm1, p1 = d1 <= wm1, p2 = d2 <= wm1, p3 = d3 <= wm1;
         if (!full) {
             p0 = p0 && (row + 0 < end);
             p1 = p1 && (row + 1 < end);
@@ -154,46 +194,49 @@ __global__ __launch_bounds__(kTPB) void k_scan(const int* __restrict__ col,
             p3 = p3 && (row + 3 < end);
         }
         cnt += (unsigned)p0 + (unsigned)p1 + (unsigned)p2 + (unsigned)p3;
-        if constexpr (MASK) {
-            const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
-                                     m3 = __ballot(p3);
-            if (lane < 4) {
-                const unsigned long long m = lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
-                masks[((tile_row / kTileRows) * kWaves + wave) * 4 + lane] = m;
-            }
+        if constexpr (MODE == kMask) {
+            (void)lane;  // the mask pass is k_mask; k_scan<kMask> is not instantiated
+                } else if constexpr (MODE == kAux) {
+            const int a0 = p0 ? aux[row + 0] : 0, a1 = p1 ? aux[row + 1] : 0,
+                      a2 = p2 ? aux[row + 2] : 0, a3 = p3 ? aux[row + 3] : 0;
+            sumv += (long long)a0 + (long long)a1 + (long long)a2 + (long long)a3;
+            mnv = min(mnv, min(min(p0 ? a0 : INT_MAX, p1 ? a1 : INT_MAX),
+                               min(p2 ? a2 : INT_MAX, p3 ? a3 : INT_MAX)));
+            mxv = max(mxv, max(max(p0 ? a0 : INT_MIN, p1 ? a1 : INT_MIN),
+                               max(p2 ? a2 : INT_MIN, p3 ? a3 : INT_MIN)));
         } else {
-            int a0 = v.x, a1 = v.y, a2 = v.z, a3 = v.w;
-            if constexpr (AUX) {
-                a0 = p0 ? aux[row + 0] : 0;
-                a1 = p1 ? aux[row + 1] : 0;
-                a2 = p2 ? aux[row + 2] : 0;
-                a3 = p3 ? aux[row + 3] : 0;
+            sumd += (unsigned long long)(p0 ? d0 : 0u) + (unsigned long long)(p1 ? d1 : 0u) +
+                    (unsigned long long)(p2 ? d2 : 0u) + (unsigned long long)(p3 ? d3 : 0u);
+            if constexpr (MODE == kAgg) {
+                if (full) {
+                    mind = min(mind, min(min(d0, d1), min(d2, d3)));
+                    maxr = min(maxr, min(min(wm1 - d0, wm1 - d1), min(wm1 - d2, wm1 - d3)));
+                } else {
+                    mind = min(mind, min(min(p0 ? d0 : ~0u, p1 ? d1 : ~0u), min(p2 ? d2 : ~0u, p3 ? d3 : ~0u)));
+                    maxr = min(maxr, min(min(p0 ? wm1 - d0 : ~0u, p1 ? wm1 - d1 : ~0u),
+                                         min(p2 ? wm1 - d2 : ~0u, p3 ? wm1 - d3 : ~0u)));
+                }
             }
-            sum += (long long)(p0 ? a0 : 0) + (long long)(p1 ? a1 : 0) +
-                   (long long)(p2 ? a2 : 0) + (long long)(p3 ? a3 : 0);
-            mn = min(mn, min(min(p0 ? a0 : INT_MAX, p1 ? a1 : INT_MAX),
-                             min(p2 ? a2 : INT_MAX, p3 ? a3 : INT_MAX)));
-            mx = max(mx, max(max(p0 ? a0 : INT_MIN, p1 ? a1 : INT_MIN),
-                             max(p2 ? a2 : INT_MIN, p3 ? a3 : INT_MIN)));
         }
     };
 
+    constexpr int U = ScanTraits<MODE>::kUnrollM;
     uint64_t t = start;
-    // Full groups of kUnroll tiles: all loads issued before the first use.
-    for (; t + (uint64_t)kUnroll * kTileRows <= end; t += (uint64_t)kUnroll * kTileRows) {
-        int4 v[kUnroll];
+    // Full groups of U tiles: all loads issued before the first use.
+    for (; t + (uint64_t)U * kTileRows <= end; t += (uint64_t)U * kTileRows) {
+        int4 v[U];
 #pragma unroll
-        for (int u = 0; u < kUnroll; u++)
-            v[u] = load4<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
+        for (int u = 0; u < U; u++)
+            v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
 #pragma unroll
-        for (int u = 0; u < kUnroll; u++) consume(v[u], t + (uint64_t)u * kTileRows, true);
+        for (int u = 0; u < U; u++) consume(v[u], t + (uint64_t)u * kTileRows, true);
     }
     // Remaining tiles (the chunk tail), bounds-checked per row.
     for (; t < end; t += kTileRows) {
         const uint64_t row = t + (uint64_t)tid * 4;
         int4 v;
         if (row + 3 < end) {
-            v = load4<VEC>(col + row);
+            v = load4_nt<VEC>(col + row);
         } else {
             v.x = row + 0 < end ? col[row + 0] : 0;
             v.y = row + 1 < end ? col[row + 1] : 0;
@@ -202,7 +245,99 @@ __global__ __launch_bounds__(kTPB) void k_scan(const int* __restrict__ col,
         }
         consume(v, t, row + 3 < end);
     }
+    // Back from d-space to values (exact: low + d never wraps for a matching row).
+    long long sum;
+    int mn = INT_MAX, mx = INT_MIN;
+    if constexpr (MODE == kAux) {
+        sum = sumv;
+        mn = mnv;
+        mx = mxv;
+    } else {
+        sum = (long long)sumd + (long long)cnt * (long long)(int32_t)lo;
+        if (MODE == kAgg && cnt) {
+            mn = (int)(lo + mind);
+            mx = (int)(lo + (wm1 - maxr));
+        }
+    }
     block_store_partial(cnt, sum, mn, mx, part);
+}
+
+// ---------------------------------------------------------------------------
+// k_mask: first half of the ordered compaction. Streams the chunk like k_scan
+// (nt dwordx4, 8 tiles in flight) and writes one predicate bit per row plus a
+// count per block. Per 8-tile super-tile each lane holds 32 predicate bits
+// (bit 4u+e = its row u*1024 + 4*tid + e); 32 ballots transpose them so that
+// lane k of the wave holds record word k, written back with v_writelane, and the
+// wave stores its 256-byte record with one instruction.
+// ---------------------------------------------------------------------------
+// Transpose: returns, in lane k < 32, the 64-bit ballot of bit k of every lane's pbits.
+__device__ __forceinline__ unsigned long long transpose_bits(uint32_t pbits, int lane) {
+    unsigned long long w = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        const unsigned long long m = __ballot((pbits >> k) & 1u);
+        w = lane == k ? m : w;
+    }
+    return w;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kTPB, 8) void k_mask(const int* __restrict__ col, uint64_t n,
+                                                  uint64_t rows_per_block, Pred pred,
+                                                  Partial* __restrict__ part,
+                                                  unsigned long long* __restrict__ masks) {
+    const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
+    uint64_t end = start + rows_per_block;
+    if (end > n) end = n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t lo = pred.lo, wm1 = pred.wm1;
+    unsigned int cnt = 0;
+    uint64_t t = start;  // 8192-row aligned (geometry granule)
+    // The record of super-tile i is stored after super-tile i+1's loads are issued:
+    // vmcnt counts stores and loads in order, so a store issued before the loads
+    // would add its write round trip to every iteration.
+    unsigned long long pending = 0;
+    uint64_t pending_at = ~0ull;
+    for (; t + 8ull * kTileRows <= end; t += 8ull * kTileRows) {
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
+        if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;
+        uint32_t pbits = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t b = (((uint32_t)v[u].x - lo) <= wm1 ? 1u : 0u) |
+                               (((uint32_t)v[u].y - lo) <= wm1 ? 2u : 0u) |
+                               (((uint32_t)v[u].z - lo) <= wm1 ? 4u : 0u) |
+                               (((uint32_t)v[u].w - lo) <= wm1 ? 8u : 0u);
+            pbits |= b << (4 * u);
+        }
+        cnt += (unsigned int)__popc(pbits);
+        pending = transpose_bits(pbits, lane);
+        pending_at = mask_word(t / kTileRows, wave);
+    }
+    if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;
+    for (; t < end; t += kTileRows) {  // the last chunk's tail, tile by tile
+        const uint64_t row = t + (uint64_t)tid * 4;
+        int4 v;
+        v.x = row + 0 < end ? col[row + 0] : 0;
+        v.y = row + 1 < end ? col[row + 1] : 0;
+        v.z = row + 2 < end ? col[row + 2] : 0;
+        v.w = row + 3 < end ? col[row + 3] : 0;
+        const bool p0 = ((uint32_t)v.x - lo) <= wm1 && row + 0 < end,
+                   p1 = ((uint32_t)v.y - lo) <= wm1 && row + 1 < end,
+                   p2 = ((uint32_t)v.z - lo) <= wm1 && row + 2 < end,
+                   p3 = ((uint32_t)v.w - lo) <= wm1 && row + 3 < end;
+        cnt += (unsigned)p0 + (unsigned)p1 + (unsigned)p2 + (unsigned)p3;
+        const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
+                                 m3 = __ballot(p3);
+        const uint64_t T = t / kTileRows;
+        if (lane < 4)
+            masks[mask_word(T, wave) + (T & 7) * 4 + lane] =
+                lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
+    }
+    block_store_partial(cnt, 0, INT_MAX, INT_MIN, part);
 }
 
 // One block combines the per-block partials into the final aggregate.
@@ -244,12 +379,12 @@ __global__ __launch_bounds__(kTPB) void k_final(const Partial* __restrict__ part
 
 // ---------------------------------------------------------------------------
 // k_compact: predicate bits -> ascending position list (second half of the
-// ordered compaction). Block b re-walks the chunk of scan block b. Its output
-// offset is the sum of the counts of blocks 0..b-1. Inside the block, 16 waves
-// take contiguous runs of 256-row groups; a wave loads 16 groups (64 mask words)
-// per instruction, popcounts them, and a wave-wide scan gives each group's
-// offset. Every lane then writes its own rows' positions (or payload[row], for
-// select_result's prior positions, query.c:38-86) in ascending row order.
+// ordered compaction). Block b re-walks the chunk of scan block b; its output
+// base is the sum of the counts of blocks 0..b-1. One LANE per 256-row group:
+// the lane loads its group's four mask words (32 contiguous bytes), a block-wide
+// scan of the popcounts gives each group's offset, and the lane emits its rows in
+// ascending order (row = group + 4*l + e for bit l of word e). The mask stream is
+// N/8 bytes; the work per lane is its group's match count.
 // ---------------------------------------------------------------------------
 template <bool PAYLOAD>
 __global__ __launch_bounds__(kCompactTPB) void k_compact(
@@ -258,9 +393,8 @@ __global__ __launch_bounds__(kCompactTPB) void k_compact(
     unsigned long long* __restrict__ d_count) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ unsigned long long s_red[kCompactWaves];
-    __shared__ unsigned long long s_wtot[kCompactWaves];
+    __shared__ unsigned int s_wtot[kCompactWaves];
 
-    // Output base = sum of the counts of the preceding blocks.
     unsigned long long acc = 0;
     for (uint32_t i = tid; i < blockIdx.x; i += kCompactTPB) acc += part[i].count;
     acc = wave_sum_u64(acc);
@@ -277,77 +411,266 @@ __global__ __launch_bounds__(kCompactTPB) void k_compact(
     uint64_t end = start + rows_per_block;
     if (end > n) end = n;
     const uint64_t ngroups = ((end - start + kTileRows - 1) / kTileRows) * kWaves;
-    const unsigned long long* cmask = masks + (start / kTileRows) * kWaves * 4;
-    constexpr uint64_t kGroupsPerWave = (uint64_t)kGroupsPerBatch * kBatchesPerWave;
-    constexpr uint64_t kGroupsPerRound = kGroupsPerWave * kCompactWaves;
-
+    const uint64_t T0 = start / kTileRows;  // first 1024-row tile of the chunk
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     unsigned long long running = base;
-    for (uint64_t r0 = 0; r0 < ngroups; r0 += kGroupsPerRound) {
-        const uint64_t g0 = r0 + (uint64_t)wave * kGroupsPerWave;
-        // Phase A: this wave's match total over its 128 groups (8 loads in flight).
-        unsigned long long wtot = 0;
-#pragma unroll
-        for (int bb = 0; bb < kBatchesPerWave; bb++) {
-            const uint64_t g = g0 + (uint64_t)bb * kGroupsPerBatch + (uint64_t)(lane >> 2);
-            const unsigned long long w = g < ngroups ? cmask[g * 4 + (lane & 3)] : 0ull;
-            wtot += (unsigned long long)__popcll(w);
+    for (uint64_t g0 = 0; g0 < ngroups; g0 += kCompactTPB) {
+        // group g (row order) = tile T0 + g/4, wave g%4
+        const uint64_t g = g0 + (uint64_t)tid;
+        unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        if (g < ngroups) {
+            const uint64_t T = T0 + (g >> 2);
+            const unsigned long long* rec = masks + mask_word(T, (int)(g & 3)) + (T & 7) * 4;
+            const ulonglong2 a = reinterpret_cast<const ulonglong2*>(rec)[0];
+            const ulonglong2 b = reinterpret_cast<const ulonglong2*>(rec)[1];
+            w0 = a.x;
+            w1 = a.y;
+            w2 = b.x;
+            w3 = b.y;
         }
-        wtot = wave_sum_u64(wtot);
-        __syncthreads();  // s_wtot reuse across rounds
-        if (lane == 0) s_wtot[wave] = wtot;
+        const unsigned int c = (unsigned int)(__popcll(w0) + __popcll(w1) + __popcll(w2) + __popcll(w3));
+        unsigned int incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) s_wtot[wave] = incl;
         __syncthreads();
-        unsigned long long woff = running, rtot = 0;
+        unsigned long long woff = 0, rtot = 0;
 #pragma unroll
         for (int w = 0; w < kCompactWaves; w++) {
-            const unsigned long long x = s_wtot[w];
+            const unsigned int x = s_wtot[w];
             if (w < wave) woff += x;
             rtot += x;
         }
+        __syncthreads();  // s_wtot is rewritten next round
+        const unsigned long long o = running + woff + (incl - c);
         running += rtot;
-        if (wtot == 0) continue;  // uniform within the wave
-
-        // Phase B: write positions, batch by batch (mask words re-read from cache).
-        for (int bb = 0; bb < kBatchesPerWave; bb++) {
-            const uint64_t gb = g0 + (uint64_t)bb * kGroupsPerBatch;
-            if (gb >= ngroups) break;
-            const uint64_t g = gb + (uint64_t)(lane >> 2);
-            const unsigned long long w = g < ngroups ? cmask[g * 4 + (lane & 3)] : 0ull;
-            const unsigned int c = (unsigned int)__popcll(w);
-            // inclusive scan of c across the 64 lanes (group-major, word-minor)
-            unsigned int incl = c;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned int y = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += y;
-            }
-            const unsigned int btot = __shfl(incl, 63, 64);
-            if (btot == 0) continue;
-            const unsigned long long ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-            for (int j = 0; j < kGroupsPerBatch; j++) {
-                const unsigned int gend = __shfl(incl, 4 * j + 3, 64);
-                const unsigned int gbeg = (j == 0) ? 0u : __shfl(incl, 4 * j - 1, 64);
-                if (gend == gbeg) continue;
-                const unsigned long long w0 = __shfl(w, 4 * j + 0, 64);
-                const unsigned long long w1 = __shfl(w, 4 * j + 1, 64);
-                const unsigned long long w2 = __shfl(w, 4 * j + 2, 64);
-                const unsigned long long w3 = __shfl(w, 4 * j + 3, 64);
-                const unsigned int b0 = (unsigned int)(w0 >> lane) & 1u;
-                const unsigned int b1 = (unsigned int)(w1 >> lane) & 1u;
-                const unsigned int b2 = (unsigned int)(w2 >> lane) & 1u;
-                const unsigned int b3 = (unsigned int)(w3 >> lane) & 1u;
-                const unsigned int pre = (unsigned int)(__popcll(w0 & ltmask) + __popcll(w1 & ltmask) +
-                                                        __popcll(w2 & ltmask) + __popcll(w3 & ltmask));
-                const uint64_t gidx = gb + (uint64_t)j;
-                const uint64_t row = start + (gidx >> 2) * kTileRows + (gidx & 3) * 256 +
-                                     (uint64_t)lane * 4;
-                int* o = out + woff + gbeg + pre;
+        const uint64_t row0 = start + (g >> 2) * kTileRows + (g & 3) * 256;
+        const unsigned int wave_total = __shfl(incl, 63, 64);
+        if (wave_total > 1024) {
+            // dense: the whole wave writes one group at a time (lane l -> rows 4l+e)
+            for (int j = 0; j < 64; j++) {
+                if (__shfl(c, j, 64) == 0) continue;
+                const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
+                                         x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
+                const unsigned long long oj = __shfl(o, j, 64);
+                const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
+                const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
+                                                        __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
+                int* q = out + oj + pre;
                 unsigned int k = 0;
-                if (b0) o[k++] = PAYLOAD ? payload[row + 0] : (int)(row + 0);
-                if (b1) o[k++] = PAYLOAD ? payload[row + 1] : (int)(row + 1);
-                if (b2) o[k++] = PAYLOAD ? payload[row + 2] : (int)(row + 2);
-                if (b3) o[k++] = PAYLOAD ? payload[row + 3] : (int)(row + 3);
+                if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 0] : (int)(rj + 0);
+                if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 1] : (int)(rj + 1);
+                if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 2] : (int)(rj + 2);
+                if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 3] : (int)(rj + 3);
             }
-            woff += btot;
+        } else if (c) {
+            // sparse: each lane emits its own group's rows in order
+            unsigned long long oo = o;
+            unsigned long long m = w0 | w1 | w2 | w3;
+            while (m) {
+                const int l = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const uint64_t r = row0 + 4 * (uint64_t)l;
+                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0);
+                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1);
+                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2);
+                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_select_lb: ordered compaction in ONE pass (32768-row tiles read as 8 passes) (select_column_scan / select_result,
+// query.c:38-137) by decoupled look-back over in-order tiles.
+//   * persistent blocks take 8192-row tiles from an atomic ticket, one at a time,
+//     when they can start them; a block only ever waits on tiles with lower
+//     tickets, all held by running blocks, so progress does not depend on how
+//     many blocks are resident;
+//   * each tile publishes its match count as a 64-bit status word {flag:2, value:62}
+//     with one relaxed agent-scope atomic store (the data is the flag: no separate
+//     payload, no fence — MI355X_MICROARCH.md §visibility, granule form);
+//   * wave 0 looks back 64 status words per step (relaxed agent-scope loads) to the
+//     nearest inclusive prefix, then the tile publishes its own inclusive prefix;
+//   * rows are written in ascending order: (sub-tile u, wave, lane, element) order
+//     is row order, ranks come from ballots.
+// HBM traffic 4N (nt loads) + 4K (+ payload gathers for select_result).
+// Spins are bounded (err flag set, never a hang).
+// ---------------------------------------------------------------------------
+constexpr int kLbUnroll = 4;                       // dwordx4 per lane per pass
+constexpr int kLbPassRows = kTPB * 4 * kLbUnroll;  // 4096 rows per pass
+constexpr int kLbPasses = 8;                       // passes per tile (bits kept in LDS)
+constexpr int kLbTileRows = kLbPassRows * kLbPasses;  // 32768 rows per ticket
+constexpr unsigned long long kStA = 1ull << 62;    // aggregate published
+constexpr unsigned long long kStP = 2ull << 62;    // inclusive prefix published
+constexpr unsigned long long kStVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ void st_status(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_status(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One pass = kLbUnroll dwordx4 per lane; bit 4u+e of its predicate word is row
+// pass_base + u*1024 + tid*4 + e.
+template <bool VEC>
+__device__ __forceinline__ void pass_load(int4 (&v)[kLbUnroll], const int* __restrict__ col,
+                                          uint64_t pass_base, uint64_t n, int tid) {
+#pragma unroll
+    for (int u = 0; u < kLbUnroll; u++) {
+        const uint64_t row = pass_base + (uint64_t)u * kTileRows + (uint64_t)tid * 4;
+        if (row + 3 < n) {
+            v[u] = load4_nt<VEC>(col + row);
+        } else {
+            v[u].x = row + 0 < n ? col[row + 0] : 0;
+            v[u].y = row + 1 < n ? col[row + 1] : 0;
+            v[u].z = row + 2 < n ? col[row + 2] : 0;
+            v[u].w = row + 3 < n ? col[row + 3] : 0;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t pass_bits(const int4 (&v)[kLbUnroll], uint64_t pass_base,
+                                              uint64_t n, uint32_t lo, uint32_t wm1, int tid) {
+    uint32_t pbits = 0;
+#pragma unroll
+    for (int u = 0; u < kLbUnroll; u++) {
+        const uint64_t row = pass_base + (uint64_t)u * kTileRows + (uint64_t)tid * 4;
+        const bool full = row + 3 < n;
+        const uint32_t b = (((uint32_t)v[u].x - lo) <= wm1 && (full || row + 0 < n) ? 1u : 0u) |
+                           (((uint32_t)v[u].y - lo) <= wm1 && (full || row + 1 < n) ? 2u : 0u) |
+                           (((uint32_t)v[u].z - lo) <= wm1 && (full || row + 2 < n) ? 4u : 0u) |
+                           (((uint32_t)v[u].w - lo) <= wm1 && (full || row + 3 < n) ? 8u : 0u);
+        pbits |= b << (4 * u);
+    }
+    return pbits;
+}
+
+__device__ __forceinline__ void count_pass(uint32_t pbits, int ps, int tid, int lane, int wave,
+                                           uint32_t (*s_bits)[kTPB], unsigned int* s_cnt) {
+    s_bits[ps][tid] = pbits;
+#pragma unroll
+    for (int u = 0; u < kLbUnroll; u++) {
+        const uint32_t b = pbits >> (4 * u);
+        const unsigned int c = (unsigned int)(__popcll(__ballot(b & 1u)) + __popcll(__ballot(b & 2u)) +
+                                              __popcll(__ballot(b & 4u)) + __popcll(__ballot(b & 8u)));
+        if (lane == 0) s_cnt[(ps * kLbUnroll + u) * kWaves + wave] = c;
+    }
+}
+
+template <bool PAYLOAD, bool VEC>
+__global__ __launch_bounds__(kTPB, 7) void k_select_lb(
+    const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, Pred pred,
+    unsigned long long* status, unsigned int* ticket, uint32_t ntiles, int* __restrict__ out,
+    unsigned long long* __restrict__ d_count, unsigned int* __restrict__ err) {
+    constexpr int kGroups = kLbPasses * kLbUnroll;  // (pass, u) sub-tiles of 1024 rows
+    __shared__ unsigned int s_tile;
+    __shared__ unsigned int s_cnt[kGroups * kWaves];
+    __shared__ uint32_t s_bits[kLbPasses][kTPB];
+    __shared__ unsigned long long s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t lo = pred.lo, wm1 = pred.wm1;
+    while (true) {
+        // Take the next tile only when this block can start it at once: a ticket
+        // held while its block is still busy would stall every later tile's look-back.
+        __syncthreads();  // the previous tile is done with s_tile / s_cnt / s_excl
+        if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const unsigned int tile = s_tile;
+        if (tile >= ntiles) break;
+        const uint64_t base = (uint64_t)tile * kLbTileRows;
+        // ---- predicate bits of all passes (kept in LDS); per-(pass, u, wave) counts.
+        // Software-pipelined: pass ps+1's loads are in flight while pass ps is counted.
+        int4 va[kLbUnroll], vb[kLbUnroll];
+        pass_load<VEC>(va, col, base, n, tid);
+#pragma unroll 1
+        for (int ps = 0; ps < kLbPasses; ps += 2) {
+            pass_load<VEC>(vb, col, base + (uint64_t)(ps + 1) * kLbPassRows, n, tid);
+            count_pass(pass_bits(va, base + (uint64_t)ps * kLbPassRows, n, lo, wm1, tid), ps, tid,
+                       lane, wave, s_bits, s_cnt);
+            if (ps + 2 < kLbPasses) pass_load<VEC>(va, col, base + (uint64_t)(ps + 2) * kLbPassRows, n, tid);
+            count_pass(pass_bits(vb, base + (uint64_t)(ps + 1) * kLbPassRows, n, lo, wm1, tid), ps + 1,
+                       tid, lane, wave, s_bits, s_cnt);
+        }
+        __syncthreads();
+        unsigned int tot = 0;
+#pragma unroll
+        for (int i = 0; i < kGroups * kWaves; i++) tot += s_cnt[i];
+        // ---- publish aggregate, look back, publish inclusive prefix
+        if (wave == 0) {
+            unsigned long long excl = 0;
+            if (tile == 0) {
+                if (lane == 0) st_status(&status[0], kStP | (unsigned long long)tot);
+            } else {
+                if (lane == 0) st_status(&status[tile], kStA | (unsigned long long)tot);
+                long long pos = (long long)tile - 1;
+                unsigned int spins = 0;
+                while (true) {
+                    const long long idx = pos - lane;
+                    const unsigned long long st = idx >= 0 ? ld_status(&status[idx]) : kStP;
+                    const unsigned long long flag = st & ~kStVal;
+                    const unsigned long long pmask = __ballot(flag == kStP);
+                    const unsigned long long zmask = __ballot(flag == 0ull);
+                    // lanes [0, nearest inclusive prefix] must all have published
+                    const unsigned long long upto = pmask ? ((pmask & (~pmask + 1)) << 1) - 1 : ~0ull;
+                    if (zmask & upto) {
+                        if (++spins > (1u << 24)) {  // never expected; fail loudly, never hang
+                            if (lane == 0) atomicOr(err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    const unsigned long long val = ((1ull << lane) & upto) ? (st & kStVal) : 0ull;
+                    excl += wave_sum_u64(val);
+                    if (pmask) break;
+                    pos -= 64;
+                }
+                if (lane == 0) st_status(&status[tile], kStP | (excl + tot));
+            }
+            if (lane == 0) {
+                s_excl = excl;
+                if (tile == ntiles - 1) *d_count = excl + tot;
+            }
+        }
+        __syncthreads();
+        // ---- write positions in row order: (pass, u, wave, lane, element)
+        unsigned long long off = s_excl;
+#pragma unroll 1
+        for (int ps = 0; ps < kLbPasses; ps++) {
+            const uint32_t pbits = s_bits[ps][tid];
+#pragma unroll
+            for (int u = 0; u < kLbUnroll; u++) {
+                const int g = ps * kLbUnroll + u;
+                unsigned long long o_uw = off;
+#pragma unroll
+                for (int w = 0; w < kWaves; w++) {
+                    const unsigned int c = s_cnt[g * kWaves + w];
+                    if (w < wave) o_uw += c;
+                    off += c;
+                }
+                if (s_cnt[g * kWaves + wave] != 0) {  // uniform in the wave
+                    const uint32_t b = (pbits >> (4 * u)) & 0xFu;
+                    const unsigned long long m0 = __ballot(b & 1u), m1 = __ballot(b & 2u),
+                                             m2 = __ballot(b & 4u), m3 = __ballot(b & 8u);
+                    const unsigned int pre =
+                        (unsigned int)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) +
+                                       __popcll(m2 & ltmask) + __popcll(m3 & ltmask));
+                    const uint64_t row = base + (uint64_t)ps * kLbPassRows +
+                                         (uint64_t)u * kTileRows + (uint64_t)tid * 4;
+                    int* o = out + o_uw + pre;
+                    unsigned int k = 0;
+                    if (b & 1u) o[k++] = PAYLOAD ? payload[row + 0] : (int)(row + 0);
+                    if (b & 2u) o[k++] = PAYLOAD ? payload[row + 1] : (int)(row + 1);
+                    if (b & 4u) o[k++] = PAYLOAD ? payload[row + 2] : (int)(row + 2);
+                    if (b & 8u) o[k++] = PAYLOAD ? payload[row + 3] : (int)(row + 3);
+                }
+            }
         }
     }
 }
@@ -537,11 +860,6 @@ int ensure_ready(DevState** out) {
             return set_err(MQ_ENODEV, "device %d is %s, libmq is built for gfx950 only", d,
                            prop.gcnArchName);
         s.cus = prop.multiProcessorCount;
-        int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void*>(&k_scan<false, false, true>), kTPB, 0));
-        if (occ < 1) occ = 1;
-        s.scan_blocks_per_cu = occ;
         s.ready = true;
     }
     *out = &s;
@@ -572,24 +890,74 @@ bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
     return true;
 }
 
-void geometry(const DevState* s, uint64_t n, uint32_t* blocks, uint64_t* rpb) {
-    uint64_t gmax = (uint64_t)s->cus * (uint64_t)s->scan_blocks_per_cu;
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Resident 256-thread blocks per CU for one kernel (cached per device and kernel).
+int blocks_per_cu(const void* fn) {
+    struct Entry {
+        int dev;
+        const void* fn;
+        int occ;
+    };
+    static Entry cache[64];
+    static int ncache = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    for (int i = 0; i < ncache; i++)
+        if (cache[i].dev == dev && cache[i].fn == fn) return cache[i].occ;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kTPB, 0) != hipSuccess || occ < 1)
+        occ = 1;
+    if (ncache < 64) cache[ncache++] = Entry{dev, fn, occ};
+    return occ;
+}
+
+// One wave of resident blocks, each owning a contiguous chunk of whole tiles.
+void geometry(const DevState* s, uint64_t n, const void* fn, uint32_t* blocks, uint64_t* rpb,
+              uint64_t granule = kTileRows) {
+    uint64_t gmax = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
     if (gmax > kMaxBlocks) gmax = kMaxBlocks;
-    const uint64_t tiles = (n + kTileRows - 1) / kTileRows;
+    const uint64_t tiles = (n + granule - 1) / granule;
     uint64_t g = tiles < gmax ? tiles : gmax;
     if (g == 0) g = 1;
     const uint64_t tiles_per_block = (tiles + g - 1) / g;
-    *rpb = (tiles_per_block == 0 ? 1 : tiles_per_block) * kTileRows;
+    *rpb = (tiles_per_block == 0 ? 1 : tiles_per_block) * granule;
     g = (n + *rpb - 1) / *rpb;
     *blocks = (uint32_t)(g == 0 ? 1 : g);
 }
 
-size_t partial_bytes() { return (size_t)kMaxBlocks * sizeof(Partial); }
-size_t mask_bytes(uint64_t n) {
-    return (size_t)((n + kTileRows - 1) / kTileRows) * kWaves * 4 * sizeof(unsigned long long);
+template <int MODE>
+const void* scan_fn(bool vec) {
+    return vec ? reinterpret_cast<const void*>(&k_scan<MODE, true>)
+               : reinterpret_cast<const void*>(&k_scan<MODE, false>);
 }
 
-inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+// Launch k_scan<MODE> over n rows; returns the number of blocks (partials) via *g_out.
+template <int MODE>
+int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
+                unsigned long long* masks, hipStream_t st, const DevState* s, uint32_t* g_out,
+                uint64_t* rpb_out = nullptr) {
+    const bool vec = aligned16(col);
+    uint32_t g;
+    uint64_t rpb;
+    geometry(s, n, scan_fn<MODE>(vec), &g, &rpb);
+    if (vec)
+        hipLaunchKernelGGL((k_scan<MODE, true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
+                           part, masks);
+    else
+        hipLaunchKernelGGL((k_scan<MODE, false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
+                           part, masks);
+    LAUNCHCHK("k_scan");
+    *g_out = g;
+    if (rpb_out) *rpb_out = rpb;
+    return MQ_OK;
+}
+
+size_t partial_bytes() { return (size_t)kMaxBlocks * sizeof(Partial); }
+size_t mask_bytes(uint64_t n) {  // 1 KiB (4 waves x 256 B) per 8192-row super-tile
+    return (size_t)((n + 8 * kTileRows - 1) / (8 * kTileRows)) * kWaves * 32 * sizeof(unsigned long long);
+}
+
 
 
 int empty_agg(mq_agg* d_out, hipStream_t st) {
@@ -608,29 +976,59 @@ int run_agg(const int32_t* col, const int32_t* aux, uint64_t n, Pred pred, mq_ag
             void* d_ws, size_t ws_bytes, hipStream_t st, const DevState* s) {
     if (ws_bytes < partial_bytes() || !d_ws)
         return set_err(MQ_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, partial_bytes());
-    uint32_t g;
-    uint64_t rpb;
-    geometry(s, n, &g, &rpb);
     Partial* part = static_cast<Partial*>(d_ws);
-    const bool vec = aligned16(col);
-    if (aux) {
-        if (vec)
-            hipLaunchKernelGGL((k_scan<false, true, true>), dim3(g), dim3(kTPB), 0, st, col, aux, n,
-                               rpb, pred, part, nullptr);
-        else
-            hipLaunchKernelGGL((k_scan<false, true, false>), dim3(g), dim3(kTPB), 0, st, col, aux,
-                               n, rpb, pred, part, nullptr);
-    } else {
-        if (vec)
-            hipLaunchKernelGGL((k_scan<false, false, true>), dim3(g), dim3(kTPB), 0, st, col,
-                               nullptr, n, rpb, pred, part, nullptr);
-        else
-            hipLaunchKernelGGL((k_scan<false, false, false>), dim3(g), dim3(kTPB), 0, st, col,
-                               nullptr, n, rpb, pred, part, nullptr);
-    }
-    LAUNCHCHK("k_scan");
+    uint32_t g;
+    int rc = aux ? launch_scan<kAux>(col, aux, n, pred, part, nullptr, st, s, &g)
+                 : launch_scan<kAgg>(col, nullptr, n, pred, part, nullptr, st, s, &g);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_final, dim3(1), dim3(kTPB), 0, st, part, g, d_out);
     LAUNCHCHK("k_final");
+    return MQ_OK;
+}
+
+// Ordered compaction: two streaming kernels (k_mask + k_compact, default) or the
+// single-pass decoupled look-back (MQ_POSITIONS_IMPL=lookback). Measured on 1e9 rows
+// (DESIGN.md §3.2): mask 0.84 / 1.57 ms vs look-back 1.05 / 1.66 ms at 1 % / 50 %.
+bool use_mask_compaction() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MQ_POSITIONS_IMPL");
+        v = (e && strcmp(e, "lookback") == 0) ? 0 : 1;
+    }
+    return v == 1;
+}
+
+size_t lb_status_bytes(uint64_t n) {
+    return ((n + kLbTileRows - 1) / kLbTileRows) * sizeof(unsigned long long) + 16;
+}
+
+int run_select_lb(const int32_t* col, const int32_t* payload, uint64_t n, Pred p, int32_t* out,
+                  uint64_t* d_count, void* d_ws, size_t ws_bytes, hipStream_t st,
+                  const DevState* s) {
+    const uint32_t ntiles = (uint32_t)((n + kLbTileRows - 1) / kLbTileRows);
+    // workspace: [ticket u32 | err u32 | pad 8][status u64 x ntiles] after the partials
+    char* w = static_cast<char*>(d_ws) + partial_bytes();
+    if (ws_bytes < partial_bytes() + lb_status_bytes(n))
+        return set_err(MQ_EINVAL, "mq_select_positions: workspace too small");
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(w);
+    unsigned int* err = ticket + 1;
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(w + 16);
+    HIPCHK(hipMemsetAsync(w, 0, lb_status_bytes(n), st));
+    const bool vec = aligned16(col);
+    const void* fn = payload ? (vec ? (const void*)&k_select_lb<true, true> : (const void*)&k_select_lb<true, false>)
+                             : (vec ? (const void*)&k_select_lb<false, true> : (const void*)&k_select_lb<false, false>);
+    uint64_t g = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
+    if (g > ntiles) g = ntiles;
+    if (g == 0) g = 1;
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
+    if (payload) {
+        if (vec) hipLaunchKernelGGL((k_select_lb<true, true>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_lb<true, false>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_select_lb<false, true>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_lb<false, false>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
+    }
+    LAUNCHCHK("k_select_lb");
     return MQ_OK;
 }
 
@@ -722,7 +1120,10 @@ int mq_stream_sync(void* stream) {
     return MQ_OK;
 }
 
-size_t mq_scan_workspace_bytes(uint64_t n) { return partial_bytes() + mask_bytes(n); }
+size_t mq_scan_workspace_bytes(uint64_t n) {
+    const size_t a = mask_bytes(n), b = lb_status_bytes(n);
+    return partial_bytes() + (a > b ? a : b);
+}
 
 void mq_scan_geometry(uint64_t n, uint32_t* blocks, uint64_t* rows_per_block) {
     DevState* s;
@@ -733,7 +1134,7 @@ void mq_scan_geometry(uint64_t n, uint32_t* blocks, uint64_t* rows_per_block) {
     }
     uint32_t g;
     uint64_t r;
-    geometry(s, n, &g, &r);
+    geometry(s, n, scan_fn<kSum>(true), &g, &r);
     if (blocks) *blocks = g;
     if (rows_per_block) *rows_per_block = r;
 }
@@ -803,7 +1204,8 @@ int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, 
 }
 
 int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
-                       int32_t high, void* d_ws, size_t ws_bytes, uint32_t* nblocks, void* stream) {
+                       int32_t high, int want_minmax, void* d_ws, size_t ws_bytes,
+                       uint32_t* nblocks, void* stream) {
     DevState* s;
     int rc = ensure_ready(&s);
     if (rc) return rc;
@@ -820,19 +1222,9 @@ int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t lo
         *nblocks = 1;
         return MQ_OK;
     }
-    uint32_t g;
-    uint64_t rpb;
-    geometry(s, n, &g, &rpb);
     Partial* part = static_cast<Partial*>(d_ws);
-    if (aligned16(d_col))
-        hipLaunchKernelGGL((k_scan<false, false, true>), dim3(g), dim3(kTPB), 0, st, d_col, nullptr,
-                           n, rpb, p, part, nullptr);
-    else
-        hipLaunchKernelGGL((k_scan<false, false, false>), dim3(g), dim3(kTPB), 0, st, d_col,
-                           nullptr, n, rpb, p, part, nullptr);
-    LAUNCHCHK("k_scan");
-    *nblocks = g;
-    return MQ_OK;
+    return want_minmax ? launch_scan<kAgg>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks)
+                       : launch_scan<kSum>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks);
 }
 
 int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream) {
@@ -874,19 +1266,23 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
     if (!d_ws || ws_bytes < mq_scan_workspace_bytes(n))
         return set_err(MQ_EINVAL, "mq_select_positions: workspace too small (%zu < %zu)", ws_bytes,
                        mq_scan_workspace_bytes(n));
+    if (!use_mask_compaction())
+        return run_select_lb(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, ws_bytes, st, s);
     uint32_t g;
     uint64_t rpb;
-    geometry(s, n, &g, &rpb);
     Partial* part = static_cast<Partial*>(d_ws);
     unsigned long long* masks =
         reinterpret_cast<unsigned long long*>(static_cast<char*>(d_ws) + partial_bytes());
-    if (aligned16(d_col))
-        hipLaunchKernelGGL((k_scan<true, false, true>), dim3(g), dim3(kTPB), 0, st, d_col, nullptr,
-                           n, rpb, p, part, masks);
-    else
-        hipLaunchKernelGGL((k_scan<true, false, false>), dim3(g), dim3(kTPB), 0, st, d_col,
-                           nullptr, n, rpb, p, part, masks);
-    LAUNCHCHK("k_scan<mask>");
+    {
+        const bool vec = aligned16(d_col);
+        const void* fn = vec ? (const void*)&k_mask<true> : (const void*)&k_mask<false>;
+        geometry(s, n, fn, &g, &rpb, 8 * kTileRows);
+        if (vec)
+            hipLaunchKernelGGL(k_mask<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, p, part, masks);
+        else
+            hipLaunchKernelGGL(k_mask<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, p, part, masks);
+        LAUNCHCHK("k_mask");
+    }
     if (d_payload)
         hipLaunchKernelGGL(k_compact<true>, dim3(g), dim3(kCompactTPB), 0, st, masks, part,
                            d_payload, n, rpb, d_pos_out,

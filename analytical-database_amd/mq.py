@@ -105,7 +105,7 @@ _SIGS = {
     "mq_gen_iota": (_int, [_vp, _u64, _vp]),
     # operators
     "mq_select_agg": (_int, [_vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
-    "mq_select_partials": (_int, [_vp, _u64, _int, _i32, _int, _i32, _vp, _sz,
+    "mq_select_partials": (_int, [_vp, _u64, _int, _i32, _int, _i32, _int, _vp, _sz,
                                   C.POINTER(C.c_uint32), _vp]),
     "mq_combine_partials": (_int, [_vp, C.c_uint32, _vp, _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),

@@ -130,7 +130,7 @@ def main() -> None:
         def step(ev0=None, ev1=None):
             if ev0 is not None:
                 ev0.record(stream)
-            mq.check(lib.mq_select_partials(col.data_ptr(), n, 1, lo, 1, hi, ws.data_ptr(),
+            mq.check(lib.mq_select_partials(col.data_ptr(), n, 1, lo, 1, hi, 0, ws.data_ptr(),
                                             ws_bytes, C.byref(nblk), sp), "scan")
             if ev1 is not None:
                 ev1.record(stream)
@@ -202,7 +202,7 @@ def main() -> None:
                        "rows_per_gpu": n, "selectivity": args.sel, "low": lo, "high": hi,
                        "parallelism": f"shard-by-query x{world}" if world > 1 else "single GPU"},
             "hbm_gbs_step": 4.0 * n * world / (elapsed / args.steps) / 1e9 / world,
-            "roofline": {"bound": "hbm", "kernel": "k_scan<false,false,true> (mq_select_partials)",
+            "roofline": {"bound": "hbm", "kernel": "k_scan<kSum,true> (mq_select_partials, count+sum)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
                          "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),

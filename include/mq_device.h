@@ -75,9 +75,12 @@ int mq_select_agg(const int32_t* d_col, uint64_t n, int has_low, int32_t low, in
 
 /* The two launches of mq_select_agg, for callers that time the scan kernel alone:
  * mq_select_partials writes one partial per block into d_ws (and *nblocks);
- * mq_combine_partials folds nblocks partials from d_ws into *d_out. */
+ * mq_combine_partials folds nblocks partials from d_ws into *d_out.
+ * want_minmax = 0 computes count + sum only (select + sum; min/max left at
+ * INT32_MAX / INT32_MIN), 1 also min/max. */
 int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
-                       int32_t high, void* d_ws, size_t ws_bytes, uint32_t* nblocks, void* stream);
+                       int32_t high, int want_minmax, void* d_ws, size_t ws_bytes,
+                       uint32_t* nblocks, void* stream);
 int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream);
 
 /* Config-3 fused: aggregate of d_val[i] over rows i where d_sel[i] is in range. */
