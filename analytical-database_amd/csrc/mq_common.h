@@ -24,6 +24,11 @@ int current_device(int* dev);
 int ensure_ready(DevState** out);
 // Grid for a grid-stride streaming kernel of 256-thread blocks.
 uint32_t stream_grid(const DevState* s, uint64_t work_items);
+// Device exclusive scan u32[n] -> u64[n] (mq_join.hip); scratch holds
+// scan_u32_scratch_elems(n) u64.
+uint64_t scan_u32_scratch_elems(uint64_t n);
+int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
+                       unsigned long long* scratch, hipStream_t st);
 
 }  // namespace mqi
 

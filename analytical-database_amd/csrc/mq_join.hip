@@ -356,6 +356,14 @@ __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict_
 
 }  // namespace
 
+namespace mqi {
+uint64_t scan_u32_scratch_elems(uint64_t n) { return scan_scratch_elems(n); }
+int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
+                       unsigned long long* scratch, hipStream_t st) {
+    return scan_exclusive<uint32_t>(in, out, n, scratch, st);
+}
+}  // namespace mqi
+
 // ===========================================================================
 // handle
 // ===========================================================================

@@ -34,62 +34,14 @@
 
 #include "mq_common.h"
 #include "mq_device.h"
+#include "mq_scan_common.h"
 
 namespace {
 
-constexpr int kTPB = 256;                 // scan block: 4 wave64
-constexpr int kWaves = kTPB / 64;
-constexpr int kTileRows = kTPB * 4;       // 1024 rows per tile (one dwordx4 per lane)
-constexpr int kUnroll = 8;                // tiles in flight per thread (128 B/lane)
+using namespace mqi;
+
 constexpr int kCompactTPB = 1024;         // compaction block: 16 wave64
 constexpr int kCompactWaves = kCompactTPB / 64;
-constexpr int kMaxBlocks = 8192;
-
-struct Partial {                          // 32 B, layout-identical to mq_agg
-    unsigned long long count;
-    long long sum;
-    int mn;
-    int mx;
-    unsigned long long pad;
-};
-static_assert(sizeof(Partial) == sizeof(mq_agg), "Partial must mirror mq_agg");
-
-// v matches when (uint32)(v - lo) <= wm1: one compare for low <= v < high
-// (the host folds NULL bounds and empty ranges; see make_pred).
-struct Pred {
-    uint32_t lo;
-    uint32_t wm1;
-};
-
-template <bool VEC>
-__device__ __forceinline__ int4 load4(const int* __restrict__ p) {  // cached (fetch / add / sub)
-    if constexpr (VEC) {
-        return *reinterpret_cast<const int4*>(p);
-    } else {
-        return make_int4(p[0], p[1], p[2], p[3]);
-    }
-}
-
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-__device__ __forceinline__ long long wave_sum_i64(long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-__device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-    return v;
-}
 
 // Block-wide combine of per-thread aggregates into part[blockIdx.x].
 __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long long sum, int mn,
@@ -141,21 +93,6 @@ __device__ __forceinline__ uint64_t mask_word(uint64_t T, int wave) {
     return ((T >> 3) * kWaves + (uint64_t)wave) * 32;
 }
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-template <bool VEC>
-__device__ __forceinline__ int4 load4_nt(const int* __restrict__ p) {
-    if constexpr (VEC) {
-        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
-        return make_int4(t.x, t.y, t.z, t.w);
-    } else {
-        return make_int4(__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1),
-                         __builtin_nontemporal_load(p + 2), __builtin_nontemporal_load(p + 3));
-    }
-}
-
-// Per-mode tiles in flight and occupancy target (waves per SIMD): 8 waves/SIMD
-// means <= 64 VGPRs, chosen where it fits without spills.
 template <int MODE>
 struct ScanTraits {
     static constexpr int kUnrollM = MODE == kAux ? 4 : (MODE == kAgg ? 6 : kUnroll);
@@ -873,11 +810,6 @@ uint32_t stream_grid(const DevState* s, uint64_t work_items) {
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
-}  // namespace mqi
-
-namespace {
-using namespace mqi;
-
 // Fold (has_low, low, has_high, high) into one unsigned range compare.
 // Returns false for an empty range.
 bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
@@ -889,8 +821,6 @@ bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
     p->wm1 = (uint32_t)(width - 1);
     return true;
 }
-
-inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Resident 256-thread blocks per CU for one kernel (cached per device and kernel).
 int blocks_per_cu(const void* fn) {
@@ -914,7 +844,7 @@ int blocks_per_cu(const void* fn) {
 
 // One wave of resident blocks, each owning a contiguous chunk of whole tiles.
 void geometry(const DevState* s, uint64_t n, const void* fn, uint32_t* blocks, uint64_t* rpb,
-              uint64_t granule = kTileRows) {
+              uint64_t granule) {
     uint64_t gmax = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
     if (gmax > kMaxBlocks) gmax = kMaxBlocks;
     const uint64_t tiles = (n + granule - 1) / granule;
@@ -925,6 +855,12 @@ void geometry(const DevState* s, uint64_t n, const void* fn, uint32_t* blocks, u
     g = (n + *rpb - 1) / *rpb;
     *blocks = (uint32_t)(g == 0 ? 1 : g);
 }
+
+size_t partial_bytes() { return (size_t)kMaxBlocks * sizeof(Partial); }
+}  // namespace mqi
+
+namespace {
+using namespace mqi;
 
 template <int MODE>
 const void* scan_fn(bool vec) {
@@ -953,7 +889,6 @@ int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Part
     return MQ_OK;
 }
 
-size_t partial_bytes() { return (size_t)kMaxBlocks * sizeof(Partial); }
 size_t mask_bytes(uint64_t n) {  // 1 KiB (4 waves x 256 B) per 8192-row super-tile
     return (size_t)((n + 8 * kTileRows - 1) / (8 * kTileRows)) * kWaves * 32 * sizeof(unsigned long long);
 }
@@ -1369,23 +1304,6 @@ int mq_sub(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, v
     return addsub(d_a, d_b, n, d_out, stream, true);
 }
 
-size_t mq_shared_select_workspace_bytes(uint64_t n, int q) {
-    (void)q;
-    return mq_scan_workspace_bytes(n);
-}
-
-int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
-                     const int32_t* h_highs, int q, int32_t* const* d_pos_out,
-                     uint64_t* d_counts, void* d_ws, size_t ws_bytes, void* stream) {
-    if (q < 0 || (q > 0 && (!h_lows || !h_highs || !d_pos_out || !d_counts)))
-        return set_err(MQ_EINVAL, "mq_shared_select: bad argument");
-    for (int j = 0; j < q; j++) {
-        int rc = mq_select_positions(d_col, nullptr, n, 1, h_lows[j], 1, h_highs[j], d_pos_out[j],
-                                     d_counts + j, d_ws, ws_bytes, stream);
-        if (rc) return rc;
-    }
-    return MQ_OK;
-}
 
 
 }  // extern "C"

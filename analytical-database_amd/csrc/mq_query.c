@@ -557,28 +557,64 @@ Result* max(Result* column, Status* ret_status) {
 /* query.c:496-583. As in the reference, every query reads `column` and uses its
  * low/high fields as given (has_low/has_high are not consulted, query.c:474).
  * Positions per query are ascending, which is what the reference's thread-order
- * concatenation (query.c:563-574) produces. */
+ * concatenation (query.c:563-574) produces. Two streaming passes over the column
+ * serve all queries of a chunk (up to 256): count -> exact allocation -> write; each
+ * query's device output becomes its result's HBM shadow. */
 Result** shared_select(SelectOperator* operators, int query_count, Column* column, Status* ret_status) {
     if (ready(ret_status)) return NULL;
     size_t n = column->row_count;
     const int32_t* dcol;
-    if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
-    Result** out = (Result**)malloc(sizeof(Result*) * (size_t)(query_count > 0 ? query_count : 1));
-    for (int q = 0; q < query_count; q++) {
-        int32_t lo = operators[q].low, hi = operators[q].high;
-        int32_t* dst = (int32_t*)g_scratch;
-        int rc = mq_shared_select(dcol, n, &lo, &hi, 1, &dst, (uint64_t*)g_small, g_ws, g_ws_bytes,
-                                  g_stream);
-        uint64_t k = 0;
-        if (rc || read_count(&k, ret_status) ||
-            !(out[q] = int_result_from_device(g_scratch, (size_t)k, ret_status))) {
-            if (rc) fail(ret_status, "shared_select", rc);
-            for (int j = 0; j < q; j++) {
+    if (column_device(column, &dcol, ret_status)) return NULL;
+    Result** out = (Result**)calloc((size_t)(query_count > 0 ? query_count : 1), sizeof(Result*));
+    if (query_count <= 3) {  /* a few queries: one ordered-compaction pass each is cheaper */
+        for (int j = 0; j < query_count; j++) {
+            int lo = operators[j].low, hi = operators[j].high;
+            if (!(out[j] = select_column_scan(column, &lo, &hi, ret_status))) {
+                for (int i = 0; i < j; i++) {
+                    free(out[i]->payload);
+                    free(out[i]);
+                }
+                free(out);
+                ret_status->code = ERROR;
+                return NULL;
+            }
+        }
+        ret_status->code = OK;
+        return out;
+    }
+    int done = 0;
+    for (int q0 = 0; q0 < query_count; q0 += 256) {
+        int q = query_count - q0 < 256 ? query_count - q0 : 256;
+        int32_t lows[256], highs[256];
+        uint64_t k[256];
+        void* dev[256] = {0};
+        for (int j = 0; j < q; j++) {
+            lows[j] = operators[q0 + j].low;
+            highs[j] = operators[q0 + j].high;
+        }
+        int rc = grow(&g_ws, &g_ws_bytes, mq_shared_select_workspace_bytes(n, q));
+        if (!rc) rc = mq_shared_select_count(dcol, n, lows, highs, q, k, g_ws, g_ws_bytes, g_stream);
+        for (int j = 0; !rc && j < q; j++) rc = mq_malloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
+        if (!rc) rc = mq_shared_select_write(g_ws, (int32_t* const*)dev, g_stream);
+        for (int j = 0; !rc && j < q; j++) {
+            int32_t* host = (int32_t*)malloc((k[j] ? k[j] : 1) * sizeof(int32_t));
+            if (k[j] && (rc = d2h(host, dev[j], (size_t)k[j] * sizeof(int32_t)))) {
+                free(host);
+                break;
+            }
+            shadow_put(host, (size_t)k[j], dev[j]);
+            dev[j] = NULL;  /* owned by the shadow now */
+            out[q0 + j] = new_result(INT, (size_t)k[j], host);
+            done = q0 + j + 1;
+        }
+        for (int j = 0; j < q; j++) mq_free(dev[j]);
+        if (rc) {
+            fail(ret_status, "shared_select", rc);
+            for (int j = 0; j < done; j++) {
                 free(out[j]->payload);
                 free(out[j]);
             }
             free(out);
-            ret_status->code = ERROR;
             return NULL;
         }
     }

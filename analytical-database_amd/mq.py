@@ -118,6 +118,8 @@ _SIGS = {
     "mq_sub": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "mq_shared_select_workspace_bytes": (_sz, [_u64, _int]),
     "mq_shared_select": (_int, [_vp, _u64, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
+    "mq_shared_select_count": (_int, [_vp, _u64, _vp, _vp, _int, _vp, _vp, _sz, _vp]),
+    "mq_shared_select_write": (_int, [_vp, _vp, _vp]),
     "mq_hash_join": (_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, C.POINTER(_u64),
                             _vp]),
     "mq_join_build": (_int, [_vp, _vp, _u64, C.POINTER(_vp), _vp]),

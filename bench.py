@@ -299,8 +299,50 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
             "algorithmic_bytes": 4 * n + 8 * k,
             "note": "select col0 + gather col1 at matches, one kernel"}
         del pos, col1, vals
+    out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold)
     return out
+
+
+def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:
+    """S11 shared_select on the 1e9-row column: Q range queries of 0.1 % each, two
+    passes (count + write) vs Q separate ordered selects."""
+    import numpy as np
+    sp = mq.stream_of(stream)
+    res = {}
+    rng = np.random.default_rng(5)
+    for q in (2, 16, 150):
+        lows = rng.integers(0, n - n // 1000, q).astype(np.int32)
+        highs = (lows + n // 1000).astype(np.int32)
+        lo_c = (C.c_int32 * q)(*lows.tolist())
+        hi_c = (C.c_int32 * q)(*highs.tolist())
+        wsb = lib.mq_shared_select_workspace_bytes(n, q)
+        with torch.cuda.stream(stream):
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            k = (C.c_uint64 * q)()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            mq.check(lib.mq_shared_select_count(col.data_ptr(), n, lo_c, hi_c, q, k, ws.data_ptr(), wsb, sp))
+            outs = [torch.empty(max(int(x), 1), dtype=torch.int32, device=dev) for x in k]
+            ptrs = (C.c_void_p * q)(*[o.data_ptr() for o in outs])
+            mq.check(lib.mq_shared_select_write(ws.data_ptr(), ptrs, sp))
+            torch.cuda.synchronize()
+            t1 = time.perf_counter() - t0
+            # the same with q separate ordered selects
+            sws = lib.mq_scan_workspace_bytes(n)
+            ws2 = torch.empty(sws, dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for j in range(q):
+                mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, int(lows[j]), 1, int(highs[j]),
+                                                 outs[j].data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
+            torch.cuda.synchronize()
+            t2 = time.perf_counter() - t0
+            del outs, ws, ws2
+        res[f"q{q}"] = {"ms_shared": 1e3 * t1, "ms_q_separate_selects": 1e3 * t2,
+                        "rows_x_queries_per_s": n * q / t1, "k_total": int(sum(k))}
+    return res
 
 
 def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28) -> dict:

@@ -114,14 +114,24 @@ int mq_reduce(const int32_t* d_vals, uint64_t n, mq_agg* d_out, void* d_ws, size
 int mq_add(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
 int mq_sub(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
 
-/* ---- S11 shared_select: q range predicates over one column ----
- * d_lows/d_highs: q int32 bounds (device), has_low/has_high ignored as in
- * query.c:472-479. d_pos_out[j] (host array of q device pointers, each capacity n)
- * receives query j's ascending positions; d_counts[j] (device) its K_j. */
+/* ---- S11 shared_select: q range predicates [lows[j], highs[j]) over one column ----
+ * h_lows/h_highs: q host int32 bounds, used as given (has_low/has_high are ignored
+ * there, query.c:472-479). d_pos_out[j] (host array of q device pointers, each of
+ * capacity n) receives query j's ascending positions; d_counts[j] (device) its K_j.
+ * q >= 2 reads the column twice in total (count pass + write pass), any q <= 256. */
 size_t mq_shared_select_workspace_bytes(uint64_t n, int q);
 int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
                      const int32_t* h_highs, int q, int32_t* const* d_pos_out,
                      uint64_t* d_counts, void* d_ws, size_t ws_bytes, void* stream);
+/* The same in two steps, so outputs can be sized exactly (q <= 256):
+ * count: one pass, *h_counts[j] = K_j (host, synchronous); the workspace keeps the
+ *        offsets for the next step;
+ * write: the second pass into d_pos_out[j] (capacity K_j each), on the workspace
+ *        of the immediately preceding count call of this thread. */
+int mq_shared_select_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
+                           const int32_t* h_highs, int q, uint64_t* h_counts, void* d_ws,
+                           size_t ws_bytes, void* stream);
+int mq_shared_select_write(void* d_ws, int32_t* const* d_pos_out, void* stream);
 
 /* ---- J1 hash_join as three steps on a handle (lets the caller size the output) ----
  * build: table over (c1, p1); p1 must stay valid until mq_join_free.

@@ -426,3 +426,43 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
     r = [x for x in goldens["join_survey"] if x["n"] == 1 << 28][0]
     m, h = _join_golden(lib, refcpu, r["n"])
     assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"])
+
+
+# ---------------------------------------------------------------------------
+# S11 shared_select (device API): Q predicates, two passes, exact-size outputs
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
+                                 (3_000_017, 20)])
+def test_shared_select_vs_oracle(lib, refcpu, n, q):
+    rng = np.random.default_rng(n + q)
+    d = rng.integers(-1000, 1000, n, dtype=np.int32)
+    if n > 8:
+        d[:3] = [I32MIN, I32MAX, 0]
+    lows = rng.integers(-1100, 1000, q).astype(np.int32)
+    highs = (lows + rng.integers(-50, 400, q)).astype(np.int32)  # some empty / inverted
+    if q > 3:
+        lows[0], highs[0] = I32MIN, I32MAX   # everything but INT_MAX
+        lows[1], highs[1] = 5, 5             # empty
+        lows[2], highs[2] = -3, 900          # wide, overlapping
+    want = [refcpu.select_scan(d, int(lows[j]), int(highs[j])) for j in range(q)]
+    dd = Dev.of(d)
+    ws = Dev(lib.mq_shared_select_workspace_bytes(n, q))
+    k = (C.c_uint64 * q)()
+    lo_c = (C.c_int32 * q)(*lows.tolist())
+    hi_c = (C.c_int32 * q)(*highs.tolist())
+    mq.check(lib.mq_shared_select_count(dd.ptr, n, lo_c, hi_c, q, k, ws.ptr, ws.nbytes, None))
+    assert [int(x) for x in k] == [len(w) for w in want]
+    outs = [Dev(max(int(x), 1) * 4) for x in k]
+    ptrs = (C.c_void_p * q)(*[o.ptr for o in outs])
+    mq.check(lib.mq_shared_select_write(ws.ptr, ptrs, None))
+    for j in range(q):
+        assert np.array_equal(outs[j].get(np.int32, int(k[j])), want[j]), (n, q, j)
+    # the one-call form (capacity-n outputs, device counts)
+    if n and q <= 20:
+        full = [Dev(n * 4) for _ in range(q)]
+        dk = Dev(8 * q)
+        fptrs = (C.c_void_p * q)(*[o.ptr for o in full])
+        mq.check(lib.mq_shared_select(dd.ptr, n, lo_c, hi_c, q, fptrs, dk.ptr, ws.ptr, ws.nbytes, None))
+        kk = dk.get(np.uint64, q)
+        for j in range(q):
+            assert np.array_equal(full[j].get(np.int32, int(kk[j])), want[j]), (n, q, j)
