@@ -199,6 +199,33 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
     block_store_partial(cnt, sum, mn, mx, part);
 }
 
+// k_stream_read: the achievable HBM read ceiling for this access pattern (SURVEY
+// §8(d) "achievable peak"): k_scan's chunking, nt dwordx4 loads and 8 tiles in
+// flight, with no predicate; each block stores the xor of its chunk so the loads
+// are live. Rows past the last full 8-tile group are not read (n is the bench's
+// 1e9 = a multiple of 8192 x blocks in practice; the byte count reported is the
+// number actually read, see mq_stream_read).
+template <bool VEC>
+__global__ __launch_bounds__(kTPB, 8) void k_stream_read(const int* __restrict__ col, uint64_t n,
+                                                         uint64_t rows_per_block,
+                                                         uint32_t* __restrict__ out) {
+    const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
+    uint64_t end = start + rows_per_block;
+    if (end > n) end = n;
+    const int tid = threadIdx.x;
+    uint32_t x = 0;
+    for (uint64_t t = start; t + 8ull * kTileRows <= end; t += 8ull * kTileRows) {
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
+#pragma unroll
+        for (int u = 0; u < 8; u++) x ^= (uint32_t)(v[u].x ^ v[u].y ^ v[u].z ^ v[u].w);
+    }
+    x = (uint32_t)wave_sum_u64(x);
+    if ((tid & 63) == 0) atomicXor(out + blockIdx.x, x);
+}
+
 // ---------------------------------------------------------------------------
 // k_mask: first half of the ordered compaction. Streams the chunk like k_scan
 // (nt dwordx4, 8 tiles in flight) and writes one predicate bit per row plus a
@@ -1160,6 +1187,31 @@ int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t lo
     Partial* part = static_cast<Partial*>(d_ws);
     return want_minmax ? launch_scan<kAgg>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks)
                        : launch_scan<kSum>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks);
+}
+
+int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes,
+                   uint64_t* bytes_read, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!d_ws || !bytes_read || (n && !d_col)) return set_err(MQ_EINVAL, "mq_stream_read: NULL pointer");
+    if ((uintptr_t)d_col & 15u) return set_err(MQ_EINVAL, "mq_stream_read: column not 16-byte aligned");
+    if (ws_bytes < (size_t)kMaxBlocks * sizeof(uint32_t))
+        return set_err(MQ_EINVAL, "mq_stream_read: workspace too small");
+    uint32_t g;
+    uint64_t rpb;
+    geometry(s, n, reinterpret_cast<const void*>(&k_stream_read<true>), &g, &rpb, 8 * kTileRows);
+    uint64_t read = 0;
+    for (uint32_t b = 0; b < g; b++) {
+        const uint64_t a = (uint64_t)b * rpb, e = a + rpb < n ? a + rpb : n;
+        read += e > a ? (e - a) / (8 * kTileRows) * (8 * kTileRows) : 0;
+    }
+    *bytes_read = read * 4;
+    if (n == 0) return MQ_OK;
+    hipLaunchKernelGGL((k_stream_read<true>), dim3(g), dim3(kTPB), 0, (hipStream_t)stream, d_col, n,
+                       rpb, static_cast<uint32_t*>(d_ws));
+    LAUNCHCHK("k_stream_read");
+    return MQ_OK;
 }
 
 int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream) {

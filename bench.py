@@ -77,12 +77,27 @@ def cpu_baseline(rows: int) -> dict:
         c, s2 = refcpu.count_sum(d, lo, hi, nthreads=16)
         mt.append(time.perf_counter() - t0)
     assert s2 == s
+    variants = {"host_cores_16": {"value": ns / statistics.median(mt), "cores": 16, "kind": "port",
+                                  "what": "refcpu rc_select_count_sum, 16 pthreads, row-balanced"}}
+    if kind == "reference":
+        # the reference as its Makefile builds it (-O0, src/Makefile:12), one run
+        api0 = Api(refcpu.reference(refcpu.REFLIB_O0))
+        t0 = time.perf_counter()
+        s0 = api0.sum_result(api0.fetch_column(col, api0.select_column(col, lo, hi)))
+        variants["reference_O0"] = {"value": ns / (time.perf_counter() - t0), "cores": 1,
+                                    "kind": "reference", "what": "same chain, libref_O0.so"}
+        assert s0 == s
+        # the reference's own 3-thread shared_select (query.c:496-583), one query
+        t0 = time.perf_counter()
+        api.shared_select(col, [lo], [hi])
+        variants["shared_select_3threads"] = {"value": ns / (time.perf_counter() - t0), "cores": 3,
+                                              "kind": "reference",
+                                              "what": "shared_select Q=1, value-range split"}
     return {"value": ns / t1, "unit": "rows/s", "cores": 1, "kind": kind,
             "sample": f"{ns} rows int32 uniform [0,{ns}) seed 42, select [{lo},{hi}) -> "
                       f"fetch -> sum, {'oracle/_ref/libref.so (reference query.c, gcc -O2)' if kind == 'reference' else 'oracle/refcpu.c -O2'}, "
                       f"median of 3 = {t1:.3f} s",
-            "host_cores_variant": {"value": ns / statistics.median(mt), "cores": 16,
-                                   "kind": "port", "what": "refcpu rc_select_count_sum, 16 pthreads"},
+            "variants": variants,
             "nproc": os.cpu_count()}
 
 
@@ -175,6 +190,8 @@ def main() -> None:
         want_s = sum(rows[s]["sum"] for s in range(42, 42 + world))
         parity = (res["count"], res["sum"]) == (want_k, want_s)
 
+    achievable = achievable_read_peak(lib, mq, torch, stream, col, ws) if world == 1 else None
+
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra:
         extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold)
@@ -206,6 +223,9 @@ def main() -> None:
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
                          "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),
+                         "kernel_ms_median": statistics.median(kernel_ms),
+                         "achievable_peak": achievable,
+                         "frac_of_achievable": (gbs / achievable["gbs"]) if achievable else None,
                          "algorithmic_bytes_per_launch": 4 * n},
             "parity": {"ok": parity, "count": res["count"], "sum": res["sum"]},
             "extra": extra,
@@ -215,6 +235,28 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def achievable_read_peak(lib, mq, torch, stream, col, ws, launches: int = 20) -> dict:
+    """SURVEY §8(d) 'achievable peak': k_stream_read (k_scan's loads, no predicate)
+    over the same resident column, HIP events on the launch stream, median of
+    `launches` after 3 warm-ups."""
+    sp = mq.stream_of(stream)
+    nbytes = C.c_uint64()
+    ms = []
+    with torch.cuda.stream(stream):
+        for i in range(3 + launches):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            mq.check(lib.mq_stream_read(col.data_ptr(), col.numel(), ws.data_ptr(), ws.numel(),
+                                        C.byref(nbytes), sp), "stream_read")
+            b.record(stream)
+            b.synchronize()
+            if i >= 3:
+                ms.append(a.elapsed_time(b))
+    med = statistics.median(ms)
+    return {"kernel": "k_stream_read", "gbs": nbytes.value / (med * 1e-3) / 1e9,
+            "bytes": nbytes.value, "ms_median": med}
 
 
 def traffic_per_launch(n: int):

@@ -83,6 +83,13 @@ int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t lo
                        uint32_t* nblocks, void* stream);
 int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream);
 
+/* Diagnostic (no reference counterpart): the achievable HBM read rate for the
+ * scan's access pattern (SURVEY.md §8(d) "achievable peak"). Streams d_col with
+ * k_scan's loads and no predicate; *bytes_read receives the bytes the launch reads
+ * (whole 8192-row groups of each block's chunk). d_ws: >= 8192 * 4 bytes. */
+int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes,
+                   uint64_t* bytes_read, void* stream);
+
 /* Config-3 fused: aggregate of d_val[i] over rows i where d_sel[i] is in range. */
 int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,
                         int32_t low, int has_high, int32_t high, mq_agg* d_out, void* d_ws,
