@@ -15,8 +15,9 @@
 //     wave covers 256 consecutive rows and one load instruction moves 1 KiB;
 //   * kUnroll tiles are loaded before any is consumed, so every lane keeps
 //     kUnroll x 16 B in flight;
-//   * per-block partial aggregates go to a workspace slab and a one-block kernel
-//     combines them (no atomics, bitwise deterministic).
+//   * per-block partial aggregates go to a workspace slab; the last block to
+//     arrive folds them in a fixed order (or k_final does, for callers of
+//     mq_select_partials), so results are bitwise deterministic.
 // Ordered compaction (select_column_scan's ascending position list,
 // query.c:92-137) is two kernels: k_scan<MASK> writes one predicate bit per row
 // (wave ballots, N/8 bytes) plus per-block counts; k_compact turns the bits into
@@ -25,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <climits>
 #include <cstdarg>
 #include <cstdint>
@@ -43,7 +45,18 @@ using namespace mqi;
 constexpr int kCompactTPB = 1024;         // compaction block: 16 wave64
 constexpr int kCompactWaves = kCompactTPB / 64;
 
-// Block-wide combine of per-thread aggregates into part[blockIdx.x].
+__device__ __forceinline__ void store_agent(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block-wide combine of per-thread aggregates into part[blockIdx.x]. WT = true
+// publishes it write-through (agent-scope relaxed atomic stores, global_store sc1)
+// for block_arrive_last's reader on another XCD.
+template <bool WT = false>
 __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long long sum, int mn,
                                                     int mx, Partial* __restrict__ part) {
     __shared__ Partial sp[kWaves];
@@ -63,7 +76,121 @@ __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long
             r.mn = min(r.mn, sp[w].mn);
             r.mx = max(r.mx, sp[w].mx);
         }
-        part[blockIdx.x] = r;
+        if constexpr (WT) {
+            unsigned long long* w = reinterpret_cast<unsigned long long*>(part + blockIdx.x);
+            store_agent(w + 0, r.count);
+            store_agent(w + 1, (unsigned long long)r.sum);
+            store_agent(w + 2, (unsigned long long)(uint32_t)r.mn | ((unsigned long long)(uint32_t)r.mx << 32));
+        } else {
+            part[blockIdx.x] = r;
+        }
+    }
+}
+
+// In-kernel combine (replaces the k_final launch on the fused paths). Arrival
+// counters: 8 shards (blockIdx % 8, one per XCD under round-robin placement, so no
+// word takes more than 1/8 of the arrivals) + a top counter. Zero at module load;
+// the last arriver resets them, so consecutive launches on a stream reuse a slot
+// without a memset. Slots rotate on the host so concurrent launches on different
+// streams do not share counters (up to kArriveSlots in flight).
+// Ordering without an L2 writeback: the partial is stored write-through (sc1),
+// `s_waitcnt vmcnt(0)` waits for those stores to be acknowledged before the
+// arrival add is issued, and the last block reads the partials with sc1 loads.
+// (A __threadfence() release here emits buffer_wbl2 per block: measured +70 us
+// per 1e9-row launch.) Measured at 1e9 rows: write-through partials alone save
+// the k_final launch (-4.5 us); arrivals cost ~6 us and the combine ~4 us, so the
+// fused launch ties k_scan + k_final on big scans (both end on a ~5 us latency
+// chain) and saves a launch on small ones.
+// Each counter sits on its own 4 KiB line: atomics on one line serialise at about
+// 12 ns each (2048 arrivals on one line measured +45 us per launch).
+constexpr int kArriveSlots = 16;
+constexpr int kArriveStride = 1024;  // uints = 4 KiB
+__device__ unsigned int g_arrive[kArriveSlots][9 * kArriveStride];
+
+// Called by every block after block_store_partial; true in the last block to
+// arrive, which then sees every block's partial.
+__device__ __forceinline__ bool block_arrive_last(uint32_t nblocks, uint32_t slot) {
+    __shared__ int s_last;
+    if (threadIdx.x == 0) {
+        unsigned int* ctr = g_arrive[slot];
+        const uint32_t shard = blockIdx.x & 7u;
+        const uint32_t shard_n = (nblocks - shard + 7u) / 8u;  // blocks b < nblocks, b % 8 == shard
+        __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): partial stores acked
+        int last = 0;
+        if (__hip_atomic_fetch_add(ctr + shard * kArriveStride, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == shard_n - 1u) {
+            const uint32_t nshards = nblocks < 8u ? nblocks : 8u;
+            last = __hip_atomic_fetch_add(ctr + 8 * kArriveStride, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == nshards - 1u;
+        }
+        if (last) {
+#pragma unroll
+            for (int i = 0; i < 9; i++)
+                __hip_atomic_store(ctr + i * kArriveStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
+// Block-wide fold of nparts partials into *out (the body of k_final).
+__device__ __forceinline__ void block_combine(const Partial* __restrict__ part, uint32_t nparts,
+                                              mq_agg* __restrict__ out) {
+    unsigned long long cnt = 0;
+    long long sum = 0;
+    int mn = INT_MAX, mx = INT_MIN;
+    // batches of 8 partials per thread with all 24 coherent (sc1) loads in flight
+    for (uint32_t base = 0; base < nparts; base += 8 * blockDim.x) {
+        unsigned long long c[8], sm[8], m[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t i = base + j * blockDim.x + threadIdx.x;
+            const unsigned long long* w =  // clamped: unconditional loads, no branches
+                reinterpret_cast<const unsigned long long*>(part + (i < nparts ? i : nparts - 1));
+            c[j] = load_agent(w + 0);
+            sm[j] = load_agent(w + 1);
+            m[j] = load_agent(w + 2);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (base + j * blockDim.x + threadIdx.x >= nparts) {
+                c[j] = 0ull;
+                sm[j] = 0ull;
+                m[j] = 0x800000007FFFFFFFull;  // {INT_MAX, INT_MIN}
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            cnt += c[j];
+            sum += (long long)sm[j];
+            mn = min(mn, (int)(uint32_t)m[j]);
+            mx = max(mx, (int)(uint32_t)(m[j] >> 32));
+        }
+    }
+    __shared__ Partial sc[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cnt = wave_sum_u64(cnt);
+    sum = wave_sum_i64(sum);
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) sc[wave] = Partial{cnt, sum, mn, mx, 0ull};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial r = sc[0];
+#pragma unroll
+        for (int w = 1; w < kWaves; w++) {
+            r.count += sc[w].count;
+            r.sum += sc[w].sum;
+            r.mn = min(r.mn, sc[w].mn);
+            r.mx = max(r.mx, sc[w].mx);
+        }
+        out->count = r.count;
+        out->sum = r.sum;
+        out->min = r.mn;
+        out->max = r.mx;
+        out->_pad = 0;
     }
 }
 
@@ -104,11 +231,11 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
                                                const int* __restrict__ aux, uint64_t n,
                                                uint64_t rows_per_block, Pred pred,
                                                Partial* __restrict__ part,
-                                               unsigned long long* __restrict__ masks) {
+                                               mq_agg* __restrict__ out, uint32_t slot) {
     const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
     uint64_t end = start + rows_per_block;
     if (end > n) end = n;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const uint32_t lo = pred.lo, wm1 = pred.wm1;
 
     unsigned int cnt = 0;
@@ -131,9 +258,7 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
             p3 = p3 && (row + 3 < end);
         }
         cnt += (unsigned)p0 + (unsigned)p1 + (unsigned)p2 + (unsigned)p3;
-        if constexpr (MODE == kMask) {
-            (void)lane;  // the mask pass is k_mask; k_scan<kMask> is not instantiated
-                } else if constexpr (MODE == kAux) {
+        if constexpr (MODE == kAux) {
             const int a0 = p0 ? aux[row + 0] : 0, a1 = p1 ? aux[row + 1] : 0,
                       a2 = p2 ? aux[row + 2] : 0, a3 = p3 ? aux[row + 3] : 0;
             sumv += (long long)a0 + (long long)a1 + (long long)a2 + (long long)a3;
@@ -196,7 +321,13 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
             mx = (int)(lo + (wm1 - maxr));
         }
     }
-    block_store_partial(cnt, sum, mn, mx, part);
+    // out != nullptr: the last block to finish folds all partials (no k_final launch)
+    if (out) {
+        block_store_partial<true>(cnt, sum, mn, mx, part);
+        if (block_arrive_last(gridDim.x, slot)) block_combine(part, gridDim.x, out);
+    } else {
+        block_store_partial(cnt, sum, mn, mx, part);
+    }
 }
 
 // k_stream_read: the achievable HBM read ceiling for this access pattern (SURVEY
@@ -896,20 +1027,23 @@ const void* scan_fn(bool vec) {
 }
 
 // Launch k_scan<MODE> over n rows; returns the number of blocks (partials) via *g_out.
+// out != nullptr folds the partials inside the launch (block_arrive_last).
 template <int MODE>
 int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
-                unsigned long long* masks, hipStream_t st, const DevState* s, uint32_t* g_out,
+                mq_agg* out, hipStream_t st, const DevState* s, uint32_t* g_out,
                 uint64_t* rpb_out = nullptr) {
+    static std::atomic<uint32_t> next_slot{0};
+    const uint32_t slot = out ? next_slot.fetch_add(1, std::memory_order_relaxed) % kArriveSlots : 0;
     const bool vec = aligned16(col);
     uint32_t g;
     uint64_t rpb;
     geometry(s, n, scan_fn<MODE>(vec), &g, &rpb);
     if (vec)
         hipLaunchKernelGGL((k_scan<MODE, true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
-                           part, masks);
+                           part, out, slot);
     else
         hipLaunchKernelGGL((k_scan<MODE, false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
-                           part, masks);
+                           part, out, slot);
     LAUNCHCHK("k_scan");
     *g_out = g;
     if (rpb_out) *rpb_out = rpb;
@@ -940,12 +1074,8 @@ int run_agg(const int32_t* col, const int32_t* aux, uint64_t n, Pred pred, mq_ag
         return set_err(MQ_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, partial_bytes());
     Partial* part = static_cast<Partial*>(d_ws);
     uint32_t g;
-    int rc = aux ? launch_scan<kAux>(col, aux, n, pred, part, nullptr, st, s, &g)
-                 : launch_scan<kAgg>(col, nullptr, n, pred, part, nullptr, st, s, &g);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_final, dim3(1), dim3(kTPB), 0, st, part, g, d_out);
-    LAUNCHCHK("k_final");
-    return MQ_OK;
+    return aux ? launch_scan<kAux>(col, aux, n, pred, part, d_out, st, s, &g)
+               : launch_scan<kAgg>(col, nullptr, n, pred, part, d_out, st, s, &g);
 }
 
 // Ordered compaction: two streaming kernels (k_mask + k_compact, default) or the
@@ -1147,6 +1277,22 @@ int mq_select_agg(const int32_t* d_col, uint64_t n, int has_low, int32_t low, in
     hipStream_t st = (hipStream_t)stream;
     if (n == 0 || !make_pred(has_low, low, has_high, high, &p)) return empty_agg(d_out, st);
     return run_agg(d_col, nullptr, n, p, d_out, d_ws, ws_bytes, st, s);
+}
+
+int mq_select_sum(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                  int32_t high, mq_agg* d_out, void* d_ws, size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!d_out || !d_ws || (n && !d_col)) return set_err(MQ_EINVAL, "mq_select_sum: NULL pointer");
+    if ((uintptr_t)d_col & 3u) return set_err(MQ_EINVAL, "mq_select_sum: column not 4-byte aligned");
+    if (ws_bytes < partial_bytes())
+        return set_err(MQ_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, partial_bytes());
+    Pred p;
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0 || !make_pred(has_low, low, has_high, high, &p)) return empty_agg(d_out, st);
+    uint32_t g;
+    return launch_scan<kSum>(d_col, nullptr, n, p, static_cast<Partial*>(d_ws), d_out, st, s, &g);
 }
 
 int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,

@@ -140,17 +140,15 @@ def main() -> None:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         agg = mqd.agg_tensor(dev)
         mq.check(lib.mq_gen_uniform(col.data_ptr(), n, seed, n, sp), "gen")
-        nblk = C.c_uint32()
 
         def step(ev0=None, ev1=None):
+            # one launch: k_scan<kSum> with the partials folded by the last block
             if ev0 is not None:
                 ev0.record(stream)
-            mq.check(lib.mq_select_partials(col.data_ptr(), n, 1, lo, 1, hi, 0, ws.data_ptr(),
-                                            ws_bytes, C.byref(nblk), sp), "scan")
+            mq.check(lib.mq_select_sum(col.data_ptr(), n, 1, lo, 1, hi, agg.data_ptr(),
+                                       ws.data_ptr(), ws_bytes, sp), "select_sum")
             if ev1 is not None:
                 ev1.record(stream)
-            mq.check(lib.mq_combine_partials(ws.data_ptr(), nblk.value, agg.data_ptr(), sp),
-                     "combine")
             mqd.combine_count_sum(agg)
 
         for _ in range(args.warmup):
@@ -219,7 +217,7 @@ def main() -> None:
                        "rows_per_gpu": n, "selectivity": args.sel, "low": lo, "high": hi,
                        "parallelism": f"shard-by-query x{world}" if world > 1 else "single GPU"},
             "hbm_gbs_step": 4.0 * n * world / (elapsed / args.steps) / 1e9 / world,
-            "roofline": {"bound": "hbm", "kernel": "k_scan<kSum,true> (mq_select_partials, count+sum)",
+            "roofline": {"bound": "hbm", "kernel": "k_scan<kSum,true> (mq_select_sum: count+sum, partials folded in-kernel)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
                          "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),
@@ -305,6 +303,21 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
             mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, lo, 1, hi, pos.data_ptr(),
                                              cnt.data_ptr(), ws.data_ptr(), ws_bytes, sp))
 
+        nblk = C.c_uint32()
+
+        def two_launch():  # the headline step before the in-kernel combine (A/B)
+            mq.check(lib.mq_select_partials(col.data_ptr(), n, 1, lo, 1, hi, 0, ws.data_ptr(),
+                                            ws_bytes, C.byref(nblk), sp))
+            mq.check(lib.mq_combine_partials(ws.data_ptr(), nblk.value, agg.data_ptr(), sp))
+
+        def one_launch():
+            mq.check(lib.mq_select_sum(col.data_ptr(), n, 1, lo, 1, hi, agg.data_ptr(),
+                                       ws.data_ptr(), ws_bytes, sp))
+
+        out["headline_ab"] = {"ms_two_launch": timed(two_launch, 20),
+                              "ms_one_launch": timed(one_launch, 20),
+                              "note": "k_scan + k_final vs k_scan with in-kernel combine, "
+                                      "back-to-back on one stream"}
         t_pos = timed(positions)
         k = int(cnt.item())
         vals = torch.empty(max(k, 1), dtype=torch.int32, device=dev)

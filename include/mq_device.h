@@ -68,6 +68,13 @@ int mq_gen_uniform(int32_t* d_out, uint64_t n, uint64_t seed, uint64_t modulus, 
 int mq_gen_join_keys(int32_t* d_out, uint64_t n, int kind, void* stream);
 int mq_gen_iota(int32_t* d_out, uint64_t n, void* stream);
 
+/* ---- S1/S7 fused, one launch: count + int64 sum of rows of d_col in range ----
+ * (select_column -> fetch_column -> sum, query.c:92-137 + 223-243 + 325-354, with
+ * the positions never materialised). min/max are left INT32_MAX / INT32_MIN.
+ * This is the bench's headline step. d_ws: >= mq_scan_workspace_bytes(0). */
+int mq_select_sum(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                  int32_t high, mq_agg* d_out, void* d_ws, size_t ws_bytes, void* stream);
+
 /* ---- S1/S7 fused: count + int64 sum (+min/max) of rows of d_col in range ----
  * One HBM pass over d_col (4n bytes). *d_out receives the aggregate. */
 int mq_select_agg(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,

@@ -88,6 +88,46 @@ def test_select_agg_and_positions_vs_oracle(lib, refcpu, n):
                 assert (a.min, a.max) == (int(vals.min()), int(vals.max()))
             else:
                 assert (a.min, a.max) == (I32MAX, I32MIN)
+            c, sm = _select_sum(lib, dd.ptr, n, lo, hi)
+            assert (c, sm) == (a.count, a.sum), (n, off, lo, hi)
+
+
+def _select_sum(L, dcol_ptr, n, lo, hi, ws=None, out=None):
+    """mq_select_sum: one launch, partials folded by the last block to arrive."""
+    ws = ws or Dev(L.mq_scan_workspace_bytes(n))
+    out = out or Dev(32)
+    hl, l, hh, h = mq.bounds(lo, hi)
+    mq.check(L.mq_select_sum(dcol_ptr, n, hl, l, hh, h, out.ptr, ws.ptr, ws.nbytes, None))
+    a = mq.MqAgg.from_buffer_copy(out.get(np.uint8, 32).tobytes())
+    return a.count, a.sum
+
+
+def test_select_sum_in_kernel_combine_repeated(lib, refcpu):
+    """The arrival counters reset themselves: many back-to-back launches (every
+    slot is reused several times), grids from 1 block to a full wave, and
+    launches queued without a host sync in between, each matching the oracle."""
+    sizes = [1, 1024 * 3, 1024 * 7 + 5, 1024 * 9, 1 << 16, 1 << 20, 3_000_001, 12_345_678]
+    data = {n: _data(n, 1000 + n) for n in sizes}
+    devs = {n: Dev.of(d) for n, d in data.items()}
+    want = {}
+    for n, d in data.items():
+        v = d[refcpu.select_scan(d, -5, 5)]
+        want[n] = (len(v), int(v.astype(np.int64).sum()))
+    for rep in range(20):
+        for n in sizes:
+            assert _select_sum(lib, devs[n].ptr, n, -5, 5) == want[n], (rep, n)
+    # queued: 80 launches into separate outputs, one sync at the end
+    ws = [Dev(lib.mq_scan_workspace_bytes(n)) for n in sizes]
+    outs = [[Dev(32) for _ in sizes] for _ in range(10)]
+    hl, l, hh, h = mq.bounds(-5, 5)
+    for r in range(10):
+        for i, n in enumerate(sizes):
+            mq.check(lib.mq_select_sum(devs[n].ptr, n, hl, l, hh, h, outs[r][i].ptr, ws[i].ptr,
+                                       ws[i].nbytes, None))
+    for r in range(10):
+        for i, n in enumerate(sizes):
+            a = mq.MqAgg.from_buffer_copy(outs[r][i].get(np.uint8, 32).tobytes())
+            assert (a.count, a.sum) == want[n], (r, n)
 
 
 @pytest.mark.parametrize("n", [0, 7, 4097, 200_003])
