@@ -265,20 +265,53 @@ __device__ __forceinline__ uint64_t ht_find(const u64* words, uint64_t mask, int
     return ~0ull;
 }
 
+// Unique-key table: one 64-bit word per slot, {key (low 32), build row + 1 (high 32)};
+// 0 = empty. One CAS per build row and one random read per probe row (the general
+// layout needs three scattered accesses for each).
+__device__ __forceinline__ u64 pack_row(int key, uint64_t row) {
+    return (u64)(uint32_t)key | ((row + 1) << 32);
+}
+
 __global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict__ keys, uint64_t n,
-                                                           u64* words, uint32_t* __restrict__ start,
-                                                           uint32_t* __restrict__ len, uint64_t mask,
+                                                           u64* words, uint64_t mask,
                                                            uint32_t* __restrict__ dup) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        bool fresh;
-        const uint64_t h = ht_claim(words, mask, keys[i], &fresh);
-        if (fresh) {
-            start[h] = (uint32_t)i;
-            len[h] = 1;
-        } else {
-            *dup = 1;
+        const int key = keys[i];
+        const u64 w = pack_row(key, i);
+        uint64_t h = hash32((uint32_t)key) & mask;
+        for (uint64_t step = 0; step <= mask; step++) {
+            const u64 old = atomicCAS(&words[h], 0ull, w);
+            if (old == 0ull) break;
+            if ((uint32_t)old == (uint32_t)key) {  // second sighting: general path
+                *dup = 1;
+                break;
+            }
+            h = (h + 1) & mask;
         }
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
+                                                          const u64* __restrict__ words, uint64_t mask,
+                                                          uint32_t* __restrict__ pstart,
+                                                          uint32_t* __restrict__ plen) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
+        const uint32_t key = (uint32_t)pkeys[j];
+        uint64_t h = hash32(key) & mask;
+        uint32_t row1 = 0;  // build row + 1, 0 = no match
+        for (uint64_t step = 0; step <= mask; step++) {
+            const u64 cur = words[h];
+            if (cur == 0ull) break;
+            if ((uint32_t)cur == key) {
+                row1 = (uint32_t)(cur >> 32);
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+        pstart[j] = row1 ? row1 - 1 : 0u;
+        plen[j] = row1 ? 1u : 0u;
     }
 }
 
@@ -369,6 +402,7 @@ int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
 // ===========================================================================
 struct mq_join {
     int device;
+    int unique;            // 1: packed {key, row+1} table (words only); 0: words/start/len
     uint64_t n1, mask;
     u64* words;
     uint32_t* start;
@@ -469,24 +503,30 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     while (slots < 2 * n1) slots <<= 1;
     j->mask = slots - 1;
     uint32_t* dflag = nullptr;
-    if ((rc = jalloc(j, (void**)&j->words, slots * 8)) ||
-        (rc = jalloc(j, (void**)&j->start, slots * 4)) ||
-        (rc = jalloc(j, (void**)&j->len, slots * 4)) || (rc = jalloc(j, (void**)&dflag, 16))) {
+    if ((rc = jalloc(j, (void**)&j->words, slots * 8)) || (rc = jalloc(j, (void**)&dflag, 16))) {
         jfree_all(j);
         delete j;
         return rc;
     }
     j->bpos = d_p1;
+    j->unique = 1;
     if (n1) {
         HIPCHK(hipMemsetAsync(j->words, 0, slots * 8, st));
         HIPCHK(hipMemsetAsync(dflag, 0, 4, st));
         hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, d_c1,
-                           n1, j->words, j->start, j->len, j->mask, dflag);
+                           n1, j->words, j->mask, dflag);
         LAUNCHCHK("k_ht_insert_unique");
         uint32_t dup = 0;
         HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (dup) {  // general path: stable sort by key, runs in insertion order
+            j->unique = 0;
+            if ((rc = jalloc(j, (void**)&j->start, slots * 4)) ||
+                (rc = jalloc(j, (void**)&j->len, slots * 4))) {
+                jfree_all(j);
+                delete j;
+                return rc;
+            }
             uint32_t *skeys, *svals;
             if ((rc = sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) {
                 jfree_all(j);
@@ -528,8 +568,12 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (hipMalloc(&j->pstart, n2 * 4) || hipMalloc(&j->plen, n2 * 4) ||
         hipMalloc(&j->offs, n2 * 8) || hipMalloc(&j->scan_scratch, scan_scratch_elems(n2) * 8))
         return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
-    hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2, j->words,
-                       j->start, j->len, j->mask, j->pstart, j->plen);
+    if (j->unique)
+        hipLaunchKernelGGL(k_ht_probe_unique, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
+                           j->words, j->mask, j->pstart, j->plen);
+    else
+        hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
+                           j->words, j->start, j->len, j->mask, j->pstart, j->plen);
     LAUNCHCHK("k_ht_probe");
     if ((rc = scan_exclusive<uint32_t>(j->plen, j->offs, n2, j->scan_scratch, st))) return rc;
     u64 last_off = 0;
