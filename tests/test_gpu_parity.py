@@ -404,7 +404,8 @@ def _dev_join(lib, c1, p1, c2, p2):
     return o1.get(np.int32, m), o2.get(np.int32, m)
 
 
-@pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty"])
+@pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
+                                  "unique_partitioned", "dups_partitioned"])
 def test_hash_join_vs_oracle(lib, refcpu, case):
     rng = np.random.default_rng(hash(case) % 1000)
     if case == "unique":
@@ -423,18 +424,35 @@ def test_hash_join_vs_oracle(lib, refcpu, case):
     elif case == "tiny":  # the reference's full-table hang shapes (multimap.c:65-71)
         c1 = np.array([5, 9], dtype=np.int32)
         c2 = np.array([1, 9, 5, 5, 2], dtype=np.int32)
+    elif case == "marker":  # unique keys, one build row {key -1, position -1} = the
+        c1 = (rng.permutation(3000) - 1500).astype(np.int32)  # packed table's empty word
+        c2 = rng.integers(-1600, 1600, 5000, dtype=np.int32)
+    elif case in ("unique_partitioned", "dups_partitioned"):
+        # > 2^22 build rows: the window-partitioned insert. Keys from the spread
+        # config-5 generator: the oracle restates the reference's `key % size`
+        # multimap, which goes quadratic on dense or arithmetic key runs.
+        c1 = rng.permutation(refcpu.gen_join(5_000_000, "build"))
+        c2 = refcpu.gen_join(3_000_000, "probe")
+        if case == "dups_partitioned":  # one duplicate, seen only after partitioning
+            c1[4_999_999] = c1[17]
     else:
         c1 = np.array([], dtype=np.int32)
         c2 = np.array([1, 2], dtype=np.int32)
     p1 = rng.integers(0, 10 ** 7, len(c1), dtype=np.int32)
     p2 = rng.integers(0, 10 ** 7, len(c2), dtype=np.int32)
+    if case == "marker":
+        p1[np.nonzero(c1 == -1)[0][0]] = -1
     g1, g2 = _dev_join(lib, c1, p1, c2, p2)
     w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
     assert np.array_equal(g1, w1) and np.array_equal(g2, w2), case
     if len(c2) and len(c1):  # swapped roles (nested_loop_join's build side)
         h1, h2 = _dev_join(lib, c2, p2, c1, p1)
-        v1, v2 = refcpu.hash_join(c1, p1, c2, p2, nested=True)
-        assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
+        if len(c1) * len(c2) <= 10 ** 10:  # the oracle's nested loop is O(n1 * n2)
+            v1, v2 = refcpu.hash_join(c1, p1, c2, p2, nested=True)
+            assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
+        else:  # nested == swapped hash join, pinned by the smaller cases above
+            v2, v1 = refcpu.hash_join(c2, p2, c1, p1)
+            assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
 
 
 def _join_golden(lib, refcpu, n):
