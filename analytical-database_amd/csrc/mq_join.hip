@@ -276,46 +276,231 @@ __device__ __forceinline__ u64 pack_pair(int key, int payload) {
     return (u64)(uint32_t)key | ((u64)(uint32_t)payload << 32);
 }
 
-// Insert one (key, payload) word; sets *general on a duplicate key or the marker.
-__device__ __forceinline__ void ht_insert_pair(u64* words, uint64_t mask, u64 w,
-                                               uint32_t* general) {
-    if (w == kEmpty) {
-        *general = 1;
-        return;
-    }
-    const uint32_t key = (uint32_t)w;
-    uint64_t h = hash32(key) & mask;
-    for (uint64_t step = 0; step <= mask; step++) {
-        const u64 old = atomicCAS(&words[h], kEmpty, w);
-        if (old == kEmpty) return;
-        if ((uint32_t)old == key) {  // second sighting of the key
+// Windowed open addressing: the table is cut into windows of W = min(8192, slots)
+// slots and linear probing wraps inside the key's home window, so a window can be
+// built in LDS (64 KB) and written out with one coalesced sweep.
+constexpr int kWinLog = 13;
+
+struct Win {
+    uint64_t mask;   // slots - 1
+    uint64_t wmask;  // W - 1
+    int wlog;        // log2 W
+};
+
+__device__ __forceinline__ uint64_t win_next(uint64_t h, const Win& t) {
+    return (h & ~t.wmask) | ((h + 1) & t.wmask);
+}
+__device__ __forceinline__ uint32_t win_id(uint32_t key, const Win& t) {
+    return (uint32_t)((hash32(key) & t.mask) >> t.wlog);
+}
+
+// Global-CAS insert (builds below kWindowBuildRows): sets *general on a duplicate
+// key, the empty marker, or a full window.
+__global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict__ keys,
+                                                           const int* __restrict__ pay, uint64_t n,
+                                                           u64* words, Win t,
+                                                           uint32_t* __restrict__ general) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const u64 w = pack_pair(keys[i], pay[i]);
+        if (w == kEmpty) {
             *general = 1;
-            return;
+            continue;
         }
-        h = (h + 1) & mask;
+        const uint32_t key = (uint32_t)w;
+        uint64_t h = hash32(key) & t.mask;
+        bool placed = false;
+        for (uint64_t step = 0; step <= t.wmask; step++) {
+            const u64 old = atomicCAS(&words[h], kEmpty, w);
+            if (old == kEmpty) {
+                placed = true;
+                break;
+            }
+            if ((uint32_t)old == key) break;  // second sighting of the key
+            h = win_next(h, t);
+        }
+        if (!placed) *general = 1;
     }
 }
 
-__global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict__ keys,
-                                                           const int* __restrict__ pay, uint64_t n,
-                                                           u64* words, uint64_t mask,
-                                                           uint32_t* __restrict__ general) {
+// ---- window build: stable LSD radix partition of the (key, payload) words by
+// window id (8 bits per pass), then one block per window builds it in LDS ----
+template <bool FROM_COLS>
+__device__ __forceinline__ u64 win_elem(const int* c1, const int* p1, const u64* in, uint64_t i) {
+    if constexpr (FROM_COLS) return pack_pair(c1[i], p1[i]);
+    else return in[i];
+}
+
+template <bool FROM_COLS>
+__global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
+                                                   const u64* __restrict__ in, uint64_t n, Win t,
+                                                   int shift, uint32_t* __restrict__ hist,
+                                                   uint32_t ntiles) {
+    __shared__ uint32_t h[kRadix];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
+        if (i < n) {
+            const uint32_t key = FROM_COLS ? (uint32_t)c1[i] : (uint32_t)in[i];
+            atomicAdd(&h[(win_id(key, t) >> shift) & 0xFF], 1u);
+        }
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter (k_sort_scatter's ballot ranking), staged through LDS so that each
+// digit's run leaves the block as contiguous, coalesced stores.
+template <bool FROM_COLS>
+__global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1,
+                                                      const int* __restrict__ p1,
+                                                      const u64* __restrict__ in, uint64_t n, Win t,
+                                                      int shift, const u64* __restrict__ goff,
+                                                      uint32_t ntiles, u64* __restrict__ out) {
+    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    __shared__ uint32_t loff[kRadix];
+    __shared__ u64 gofs[kRadix];
+    __shared__ u64 stage[kSortTile];
+    __shared__ uint32_t wsum[kTPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    gofs[tid] = goff[(uint64_t)tid * ntiles + blockIdx.x];
+    __syncthreads();
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    u64 el[kSortItems];
+    uint32_t dr[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const bool valid = i < n;
+        el[k] = valid ? win_elem<FROM_COLS>(c1, p1, in, i) : 0ull;
+        const uint32_t d = (win_id((uint32_t)el[k], t) >> shift) & 0xFF;
+        u64 peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const bool bit = (d >> b) & 1u;
+            const u64 m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t cur = wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // per digit (thread tid = digit): prefix over waves, tile total
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = tot;
+        tot += c;
+    }
+    // tile-local exclusive scan of the digit totals (256 digits = 4 waves)
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t excl = incl - tot;
+    for (int w = 0; w < wave; w++) excl += wsum[w];
+    loff[tid] = excl;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        if (dr[k] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
+            stage[loff[d] + wcnt[wave][d] + r] = el[k];
+        }
+    }
+    __syncthreads();
+    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t e = (uint32_t)(k * kTPB + tid);
+        if (e < tn) {
+            const u64 v = stage[e];
+            const uint32_t d = (win_id((uint32_t)v, t) >> shift) & 0xFF;
+            out[gofs[d] + (e - loff[d])] = v;
+        }
+    }
+}
+
+// wstart[w] = first index of window w in the partitioned words (wstart[nw] = n).
+__global__ __launch_bounds__(kTPB) void k_win_bounds(const u64* __restrict__ in, uint64_t n, Win t,
+                                                     uint32_t nw, uint32_t* __restrict__ wstart) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
-        ht_insert_pair(words, mask, pack_pair(keys[i], pay[i]), general);
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const uint32_t w = win_id((uint32_t)in[i], t);
+        const uint32_t wp = i ? win_id((uint32_t)in[i - 1], t) + 1 : 0u;
+        for (uint32_t x = wp; x <= w; x++) wstart[x] = (uint32_t)i;
+        if (i == n - 1)
+            for (uint32_t x = w + 1; x <= nw; x++) wstart[x] = (uint32_t)n;
+    }
+}
+
+// One block per window: insert the window's words into an LDS table with LDS CAS,
+// then store the whole window (coalesced). Duplicates, the empty marker and an
+// overfull window set *general.
+__global__ __launch_bounds__(kTPB) void k_win_build(const u64* __restrict__ in,
+                                                    const uint32_t* __restrict__ wstart,
+                                                    u64* __restrict__ words, Win t,
+                                                    uint32_t* __restrict__ general) {
+    __shared__ u64 tab[1 << kWinLog];
+    const uint32_t W = (uint32_t)t.wmask + 1;
+    const uint32_t w = blockIdx.x;
+    for (uint32_t x = threadIdx.x; x < W; x += kTPB) tab[x] = kEmpty;
+    __syncthreads();
+    const uint32_t b = wstart[w], e = wstart[w + 1];
+    if (e - b > W - W / 4) {  // over 3/4 full: probes would run long (adversarial keys)
+        if (threadIdx.x == 0) *general = 1;
+    } else {
+        for (uint32_t i = b + threadIdx.x; i < e; i += kTPB) {
+            const u64 v = in[i];
+            if (v == kEmpty) {
+                *general = 1;
+                continue;
+            }
+            const uint32_t key = (uint32_t)v;
+            uint32_t h = (uint32_t)(hash32(key) & t.wmask);
+            for (uint32_t step = 0; step < W; step++) {
+                const u64 old = atomicCAS(&tab[h], kEmpty, v);
+                if (old == kEmpty) break;
+                if ((uint32_t)old == key) {
+                    *general = 1;
+                    break;
+                }
+                h = (h + 1) & (W - 1);
+            }
+        }
+    }
+    __syncthreads();
+    u64* dst = words + (uint64_t)w * W;
+    for (uint32_t x = threadIdx.x; x < W; x += kTPB) dst[x] = tab[x];
 }
 
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
-                                                          const u64* __restrict__ words, uint64_t mask,
+                                                          const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
                                                           uint32_t* __restrict__ plen) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
         const uint32_t key = (uint32_t)pkeys[j];
-        uint64_t h = hash32(key) & mask;
+        uint64_t h = hash32(key) & t.mask;
         bool hit = false;
         uint32_t payload = 0;
-        for (uint64_t step = 0; step <= mask; step++) {
+        for (uint64_t step = 0; step <= t.wmask; step++) {
             const u64 cur = words[h];
             if (cur == kEmpty) break;
             if ((uint32_t)cur == key) {
@@ -323,7 +508,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                 payload = (uint32_t)(cur >> 32);
                 break;
             }
-            h = (h + 1) & mask;
+            h = win_next(h, t);
         }
         pstart[j] = payload;  // unique path: the build position itself
         plen[j] = hit ? 1u : 0u;
@@ -422,8 +607,9 @@ int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
 // ===========================================================================
 struct mq_join {
     int device;
-    int unique;            // 1: packed {key, row+1} table (words only); 0: words/start/len
+    int unique;            // 1: windowed {key, payload} table (words only); 0: words/start/len
     uint64_t n1, mask;
+    Win win;               // unique table geometry
     u64* words;
     uint32_t* start;
     uint32_t* len;
@@ -453,16 +639,79 @@ void jfree_all(mq_join* j) {
     j->nowned = 0;
 }
 
-// Unique-path build: one CAS per build row in input order. (Grouping the rows by
-// table window first, so the CAS traffic stays in a ~16 MB cache-resident window,
-// measured 20.3 vs 21.0 ms at 2^28 rows plus a 5.8 ms partition pass: the
-// device-scope CAS cost does not depend on where the line lives.)
-int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint32_t* general,
-                  hipStream_t st, const DevState* s) {
-    hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, p1, n,
-                       j->words, j->mask, general);
-    LAUNCHCHK("k_ht_insert_unique");
-    return MQ_OK;
+// Unique-path build.
+//  * below kWindowBuildRows: one global CAS per build row (the table is small);
+//  * above: stable LSD radix partition of the (key, payload) words by window id,
+//    then one block per window builds it in LDS and stores it whole (no global
+//    atomics; every window is written, so the table needs no memset).
+// (A partition by table window feeding the global-CAS insert measured 20.3 vs
+// 21.0 ms at 2^28 rows plus the partition pass: device-scope CAS costs the same
+// wherever the line lives, so the atomics themselves have to go.)
+constexpr uint64_t kWindowBuildRows = 1ull << 16;
+
+int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
+                  uint32_t* general, hipStream_t st, const DevState* s) {
+    const Win t = j->win;
+    if (n < kWindowBuildRows) {
+        HIPCHK(hipMemsetAsync(j->words, 0xFF, slots * 8, st));
+        hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, p1,
+                           n, j->words, t, general);
+        LAUNCHCHK("k_ht_insert_unique");
+        return MQ_OK;
+    }
+    int lg = 0;
+    while ((1ull << lg) < slots) lg++;
+    const int wid_bits = lg - t.wlog;
+    const int passes = (wid_bits + 7) / 8;
+    const uint32_t nw = (uint32_t)(slots >> t.wlog);
+    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t nh = ntiles * kRadix;
+    u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
+    uint32_t *hist = nullptr, *wstart = nullptr;
+    auto done = [&](int rc) {
+        (void)hipFree(a);
+        (void)hipFree(b);
+        (void)hipFree(hist);
+        (void)hipFree(hscan);
+        (void)hipFree(scratch);
+        (void)hipFree(wstart);
+        return rc;
+    };
+    if (hipMalloc(&a, n * 8) || (passes > 1 && hipMalloc(&b, n * 8)) || hipMalloc(&hist, nh * 4) ||
+        hipMalloc(&hscan, nh * 8) || hipMalloc(&scratch, scan_scratch_elems(nh) * 8) ||
+        hipMalloc(&wstart, ((uint64_t)nw + 1) * 4))
+        return done(set_err(MQ_ENOMEM, "join: window build buffers (%llu rows)", (unsigned long long)n));
+    u64* src = nullptr;
+    u64* dst = a;
+    for (int pass = 0; pass < passes; pass++) {
+        const int shift = 8 * pass;
+        if (pass == 0) {
+            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1,
+                               (const u64*)nullptr, n, t, shift, hist, (uint32_t)ntiles);
+        } else {
+            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st,
+                               (const int*)nullptr, src, n, t, shift, hist, (uint32_t)ntiles);
+        }
+        int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
+        if (rc) return done(rc);
+        if (pass == 0) {
+            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
+                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst);
+        } else {
+            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st,
+                               (const int*)nullptr, (const int*)nullptr, src, n, t, shift, hscan,
+                               (uint32_t)ntiles, dst);
+        }
+        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window partition"));
+        src = dst;
+        dst = (dst == a) ? b : a;
+    }
+    hipLaunchKernelGGL(k_win_bounds, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, src, n, t, nw, wstart);
+    hipLaunchKernelGGL(k_win_build, dim3(nw), dim3(kTPB), 0, st, src, wstart, j->words, t, general);
+    if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window build"));
+    // the temporaries are released only after the build has run
+    if (hipStreamSynchronize(st) != hipSuccess) return done(set_err(MQ_EHIP, "join: build sync"));
+    return done(MQ_OK);
 }
 
 int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, uint32_t** vals_out,
@@ -534,6 +783,10 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     uint64_t slots = 64;
     while (slots < 2 * n1) slots <<= 1;
     j->mask = slots - 1;
+    j->win.mask = j->mask;
+    j->win.wlog = 0;
+    while (j->win.wlog < kWinLog && (1ull << (j->win.wlog + 1)) <= slots) j->win.wlog++;
+    j->win.wmask = (1ull << j->win.wlog) - 1;
     uint32_t* dflag = nullptr;
     if ((rc = jalloc(j, (void**)&j->words, slots * 8)) || (rc = jalloc(j, (void**)&dflag, 16))) {
         jfree_all(j);
@@ -543,9 +796,8 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     j->bpos = nullptr;  // unique table carries the build positions itself
     j->unique = 1;
     if (n1) {
-        HIPCHK(hipMemsetAsync(j->words, 0xFF, slots * 8, st));
         HIPCHK(hipMemsetAsync(dflag, 0, 4, st));
-        if ((rc = insert_unique(j, d_c1, d_p1, n1, dflag, st, s))) {
+        if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s))) {
             jfree_all(j);
             delete j;
             return rc;
@@ -605,7 +857,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
         return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
     if (j->unique)
         hipLaunchKernelGGL(k_ht_probe_unique, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->mask, j->pstart, j->plen);
+                           j->words, j->win, j->pstart, j->plen);
     else
         hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->start, j->len, j->mask, j->pstart, j->plen);
