@@ -38,6 +38,10 @@
 #include "mq_device.h"
 #include "mq_scan_common.h"
 
+// v_writelane through the LLVM intrinsic (this clang has no builtin for it); the
+// backend inserts the hazard waits that an inline-asm v_writelane does not.
+__device__ int mq_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 namespace {
 
 using namespace mqi;
@@ -360,21 +364,12 @@ __global__ __launch_bounds__(kTPB, 8) void k_stream_read(const int* __restrict__
 // ---------------------------------------------------------------------------
 // k_mask: first half of the ordered compaction. Streams the chunk like k_scan
 // (nt dwordx4, 8 tiles in flight) and writes one predicate bit per row plus a
-// count per block. Per 8-tile super-tile each lane holds 32 predicate bits
-// (bit 4u+e = its row u*1024 + 4*tid + e); 32 ballots transpose them so that
-// lane k of the wave holds record word k, written back with v_writelane, and the
-// wave stores its 256-byte record with one instruction.
+// count per block. Per 8-tile super-tile the wave's 32 row compares (tile u, row
+// e of each lane's dwordx4) are 32 ballots; ballot 4u+e is placed in lane 4u+e
+// with v_writelane, and the wave stores its 256-byte record with one instruction.
+// (Packing bits per lane and transposing them with 32 more ballots cost 48 us per
+// 1e9 rows; writelane removes the pack and the transpose.)
 // ---------------------------------------------------------------------------
-// Transpose: returns, in lane k < 32, the 64-bit ballot of bit k of every lane's pbits.
-__device__ __forceinline__ unsigned long long transpose_bits(uint32_t pbits, int lane) {
-    unsigned long long w = 0;
-#pragma unroll
-    for (int k = 0; k < 32; k++) {
-        const unsigned long long m = __ballot((pbits >> k) & 1u);
-        w = lane == k ? m : w;
-    }
-    return w;
-}
 
 template <bool VEC>
 __global__ __launch_bounds__(kTPB, 8) void k_mask(const int* __restrict__ col, uint64_t n,
@@ -399,17 +394,27 @@ __global__ __launch_bounds__(kTPB, 8) void k_mask(const int* __restrict__ col, u
         for (int u = 0; u < 8; u++)
             v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
         if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;
-        uint32_t pbits = 0;
+        // the row compares are the record words: ballot (u, e) goes to lane 4u + e
+        int wlo = 0, whi = 0;
+        unsigned int c = 0;
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const uint32_t b = (((uint32_t)v[u].x - lo) <= wm1 ? 1u : 0u) |
-                               (((uint32_t)v[u].y - lo) <= wm1 ? 2u : 0u) |
-                               (((uint32_t)v[u].z - lo) <= wm1 ? 4u : 0u) |
-                               (((uint32_t)v[u].w - lo) <= wm1 ? 8u : 0u);
-            pbits |= b << (4 * u);
+            const unsigned long long m0 = __ballot(((uint32_t)v[u].x - lo) <= wm1),
+                                     m1 = __ballot(((uint32_t)v[u].y - lo) <= wm1),
+                                     m2 = __ballot(((uint32_t)v[u].z - lo) <= wm1),
+                                     m3 = __ballot(((uint32_t)v[u].w - lo) <= wm1);
+            c += (unsigned)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
+            wlo = mq_writelane((int)m0, 4 * u + 0, wlo);
+            whi = mq_writelane((int)(m0 >> 32), 4 * u + 0, whi);
+            wlo = mq_writelane((int)m1, 4 * u + 1, wlo);
+            whi = mq_writelane((int)(m1 >> 32), 4 * u + 1, whi);
+            wlo = mq_writelane((int)m2, 4 * u + 2, wlo);
+            whi = mq_writelane((int)(m2 >> 32), 4 * u + 2, whi);
+            wlo = mq_writelane((int)m3, 4 * u + 3, wlo);
+            whi = mq_writelane((int)(m3 >> 32), 4 * u + 3, whi);
         }
-        cnt += (unsigned int)__popc(pbits);
-        pending = transpose_bits(pbits, lane);
+        if (lane == 0) cnt += c;  // c is wave-uniform: count it once per wave
+        pending = (unsigned long long)(uint32_t)wlo | ((unsigned long long)(uint32_t)whi << 32);
         pending_at = mask_word(t / kTileRows, wave);
     }
     if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;

@@ -189,6 +189,9 @@ __global__ __launch_bounds__(256, 8) void k_maskv(const int* __restrict__ col, u
     unsigned cnt = 0;
     unsigned long long acc = 0;
     unsigned long long pending = 0, pat = ~0ull;
+    __shared__ unsigned long long sbuf[(STORE == 7 || STORE == 8) ? 16 * 128 : 1];
+    int nbuf = 0;
+    unsigned long long fbase = 0;
     for (unsigned long long t = start; t + 8192 <= end; t += 8192) {
         int4 v[8];
 #pragma unroll
@@ -229,13 +232,105 @@ __global__ __launch_bounds__(256, 8) void k_maskv(const int* __restrict__ col, u
             } else if (STORE == 3) {
                 pending = w;
                 pat = ((t >> 13) * 4 + wave) * 32;
+            } else if (STORE == 7 || STORE == 8) {
+                // LDS-buffered: 16 super-tiles (16 KB contiguous) per flush, 16 B per lane
+                if (nbuf == 0) fbase = (t >> 13) * 128;
+                if (lane < 32) sbuf[nbuf * 128 + wave * 32 + lane] = w;
+                if (++nbuf == 16) {
+                    __syncthreads();
+                    for (int k = tid; k < 16 * 64; k += 256) {
+                        ulonglong2 q;
+                        q.x = sbuf[2 * k];
+                        q.y = sbuf[2 * k + 1];
+                        ulonglong2* d = reinterpret_cast<ulonglong2*>(masks + fbase) + k;
+                        if (STORE == 8) {
+                            typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
+                            v2u qq = {q.x, q.y};
+                            __builtin_nontemporal_store(qq, reinterpret_cast<v2u*>(d));
+                        } else {
+                            *d = q;
+                        }
+                    }
+                    __syncthreads();
+                    nbuf = 0;
+                }
             } else {
                 acc ^= w;
             }
         }
     }
     if (STORE == 3 && pat != ~0ull && lane < 32) masks[pat + lane] = pending;
+    if ((STORE == 7 || STORE == 8) && nbuf) {
+        __syncthreads();
+        for (int k = tid; k < nbuf * 64; k += 256)
+            reinterpret_cast<ulonglong2*>(masks + fbase)[k] = make_ulonglong2(sbuf[2 * k], sbuf[2 * k + 1]);
+    }
     if (threadIdx.x == 0) part[blockIdx.x].count = cnt + (unsigned)acc;
+}
+
+// v_writelane via the LLVM intrinsic (no clang builtin in this toolchain); the backend
+// inserts the hazard waits an inline-asm writelane would not.
+__device__ int mq_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// direct-ballot mask pass: the row compares ARE the ballots; each goes straight into
+// its record lane with v_writelane (no bit packing, no 32-ballot transpose).
+// GRID 0: contiguous chunk per block; GRID 1: grid-stride super-tiles.
+template <int GRID>
+__global__ __launch_bounds__(256, 8) void k_maskw(const int* __restrict__ col, unsigned long long n,
+                                                  unsigned long long rpb, unsigned lo, unsigned wm1,
+                                                  Partial* __restrict__ part,
+                                                  unsigned long long* __restrict__ masks) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long cnt = 0;
+    unsigned long long s0, s1, step;
+    if (GRID) {
+        s0 = blockIdx.x;
+        s1 = n / 8192;
+        step = gridDim.x;
+    } else {
+        const unsigned long long start = (unsigned long long)blockIdx.x * rpb;
+        s0 = start / 8192;
+        s1 = min(start + rpb, n) / 8192;
+        step = 1;
+    }
+    for (unsigned long long st = s0; st < s1; st += step) {
+        const unsigned long long t = st * 8192;
+        int4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = ld_nt4(reinterpret_cast<const int4*>(col + t + u * 1024 + tid * 4));
+        int wlo = 0, whi = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const unsigned long long m0 = __ballot(((unsigned)v[u].x - lo) <= wm1);
+            const unsigned long long m1 = __ballot(((unsigned)v[u].y - lo) <= wm1);
+            const unsigned long long m2 = __ballot(((unsigned)v[u].z - lo) <= wm1);
+            const unsigned long long m3 = __ballot(((unsigned)v[u].w - lo) <= wm1);
+            cnt += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+            wlo = mq_writelane((int)m0, 4 * u + 0, wlo);
+            whi = mq_writelane((int)(m0 >> 32), 4 * u + 0, whi);
+            wlo = mq_writelane((int)m1, 4 * u + 1, wlo);
+            whi = mq_writelane((int)(m1 >> 32), 4 * u + 1, whi);
+            wlo = mq_writelane((int)m2, 4 * u + 2, wlo);
+            whi = mq_writelane((int)(m2 >> 32), 4 * u + 2, whi);
+            wlo = mq_writelane((int)m3, 4 * u + 3, wlo);
+            whi = mq_writelane((int)(m3 >> 32), 4 * u + 3, whi);
+        }
+        const unsigned long long w = (unsigned long long)(unsigned)wlo | ((unsigned long long)(unsigned)whi << 32);
+        if (lane < 32) masks[(st * 4 + wave) * 32 + lane] = w;
+    }
+    if (threadIdx.x == 0) part[blockIdx.x].count = cnt;
+}
+
+template <int GRID>
+void launch_maskw(const int* col, unsigned long long n, unsigned lo, unsigned wm1, Partial* part,
+                  hipStream_t st, int blocks) {
+    static unsigned long long* masks = nullptr;
+    if (!masks) hipMalloc(&masks, n / 8 + 65536);
+    unsigned long long tiles = (n + 8191) / 8192;
+    unsigned long long tpb = (tiles + blocks - 1) / blocks;
+    unsigned long long rpb = tpb * 8192;
+    unsigned g = GRID ? (unsigned)blocks : (unsigned)((n + rpb - 1) / rpb);
+    hipLaunchKernelGGL((k_maskw<GRID>), dim3(g), dim3(256), 0, st, col, n, rpb, lo, wm1, part, masks);
 }
 
 // grid-stride mask pass: super-tile s handled by block s % G; records indexed by s (contiguous over the grid)
@@ -339,6 +434,12 @@ int main(int argc, char** argv) {
         {"mask: + transpose", launch_mask<1>, 8},
         {"mask: + transpose + store", launch_mask<2>, 8},
         {"mask: + transpose + deferred store", launch_mask<3>, 8},
+        {"mask: writelane chunk + store", launch_maskw<0>, 8},
+        {"mask: writelane grid-stride + store", launch_maskw<1>, 8},
+        {"mask: LDS-buffered 16KB flush", launch_mask<7>, 8},
+        {"mask: LDS-buffered 16KB flush nt", launch_mask<8>, 8},
+        {"mask: + transpose + store (again)", launch_mask<2>, 8},
+        {"ref t256 u8 chunk nt 8/CU (again)", launch<256, 8, true, 0, false>, 8},
         {"mask grid-stride + store", launch_maskg<0>, 8},
         {"mask grid-stride + store + counts", launch_maskg<1>, 8},
     };
