@@ -682,6 +682,52 @@ Result** nested_loop_join(Result* column_one, Result* position_one, Result* colu
 /* query.c:245-304: host string formatting (stays on the CPU).
  * Same formats and separators; an all-empty input yields "" (the reference
  * returns an unterminated malloc(0) buffer there, query.c:253). */
+/* Large INT results are formatted on the GPU from their HBM copy (mq_format_int32:
+ * per-value lengths, a scan, a digit-writing pass) and copied back as text; the
+ * bytes equal the reference's sprintf loop. Other results stay on the host. */
+#define PRINT_GPU_MIN_TUPLES 32768 /* MQ_PRINT_GPU_MIN overrides */
+
+static size_t print_gpu_min(void) {
+    static size_t v = 0;
+    if (!v) {
+        const char* e = getenv("MQ_PRINT_GPU_MIN");
+        v = (e && atoll(e) > 0) ? (size_t)atoll(e) : PRINT_GPU_MIN_TUPLES;
+    }
+    return v;
+}
+
+static void* g_print_out;
+static void* g_print_ws;
+static size_t g_print_out_cap, g_print_ws_cap;
+
+static int print_gpu(const Result* r, char* dst, size_t* len, Status* st) {
+    const uint64_t n = r->num_tuples;
+    const int32_t* d;
+    if (ready(st) || result_device(r, &d, st)) return -1;
+    const size_t need_out = (size_t)n * 12, need_ws = mq_format_workspace_bytes(n);
+    int rc;
+    if (g_print_out_cap < need_out) {
+        mq_free(g_print_out);
+        g_print_out = NULL;
+        g_print_out_cap = 0;
+        if ((rc = mq_malloc(&g_print_out, need_out))) return fail(st, "print: device buffer", rc);
+        g_print_out_cap = need_out;
+    }
+    if (g_print_ws_cap < need_ws) {
+        mq_free(g_print_ws);
+        g_print_ws = NULL;
+        g_print_ws_cap = 0;
+        if ((rc = mq_malloc(&g_print_ws, need_ws))) return fail(st, "print: workspace", rc);
+        g_print_ws_cap = need_ws;
+    }
+    uint64_t h_len = 0;
+    if ((rc = mq_format_int32(d, n, (char*)g_print_out, &h_len, g_print_ws, g_print_ws_cap, g_stream)) ||
+        (rc = mq_memcpy_d2h(dst, g_print_out, h_len, g_stream)) || (rc = mq_stream_sync(g_stream)))
+        return fail(st, "print: mq_format_int32", rc);
+    *len = (size_t)h_len;
+    return 0;
+}
+
 char* print(Result** results, int result_num, Status* ret_status) {
     size_t total = 0;
     for (int i = 0; i < result_num; i++) total += results[i]->num_tuples;
@@ -692,6 +738,16 @@ char* print(Result** results, int result_num, Status* ret_status) {
     for (int i = 0; i < result_num; i++) {
         Result* r = results[i];
         if (i > 0) at += (size_t)snprintf(s + at, cap - at, ",");
+        if (r->data_type == INT && r->num_tuples >= print_gpu_min()) {
+            size_t len = 0;
+            if (print_gpu(r, s + at, &len, ret_status)) {
+                free(s);
+                return NULL;
+            }
+            at += len;
+            s[at] = '\0';
+            continue;
+        }
         for (size_t j = 0; j < r->num_tuples; j++) {
             switch (r->data_type) {
                 case INT: at += (size_t)snprintf(s + at, cap - at, "%d", ((int*)r->payload)[j]); break;
@@ -738,6 +794,10 @@ const void* mq_result_device_ptr(const Result* result) {
 }
 
 void mq_release_all(void) {
+    mq_free(g_print_out);
+    mq_free(g_print_ws);
+    g_print_out = g_print_ws = NULL;
+    g_print_out_cap = g_print_ws_cap = 0;
     while (g_ncols) col_drop(&g_cols[g_ncols - 1]);
     while (g_nshadows) shadow_drop(g_nshadows - 1);
     while (g_nidx) {

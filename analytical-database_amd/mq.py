@@ -109,6 +109,8 @@ _SIGS = {
                                   C.POINTER(C.c_uint32), _vp]),
     "mq_combine_partials": (_int, [_vp, C.c_uint32, _vp, _vp]),
     "mq_select_sum": (_int, [_vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
+    "mq_format_workspace_bytes": (_sz, [_u64]),
+    "mq_format_int32": (_int, [_vp, _u64, _vp, C.POINTER(C.c_uint64), _vp, _sz, _vp]),
     "mq_stream_read": (_int, [_vp, _u64, _vp, _sz, C.POINTER(C.c_uint64), _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,

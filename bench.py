@@ -257,6 +257,41 @@ def achievable_read_peak(lib, mq, torch, stream, col, ws, launches: int = 20) ->
             "bytes": nbytes.value, "ms_median": med}
 
 
+def print_leg(lib, mq, torch, dev, stream, pos, k) -> dict:
+    """print (query.c:245-304) of config 2's K positions: GPU formatting
+    (mq_format_int32 + D2H of the text) vs the reference's sprintf loop on the
+    same values (oracle/_ref/libref.so, host)."""
+    import numpy as np
+    sp = mq.stream_of(stream)
+    out_d = torch.empty(12 * k, dtype=torch.uint8, device=dev)
+    ws = torch.empty(lib.mq_format_workspace_bytes(k), dtype=torch.uint8, device=dev)
+    host = torch.empty(12 * k, dtype=torch.uint8).pin_memory()
+    ln = C.c_uint64()
+    ms = []
+    with torch.cuda.stream(stream):
+        for i in range(4):
+            t0 = time.perf_counter()
+            mq.check(lib.mq_format_int32(pos.data_ptr(), k, out_d.data_ptr(), C.byref(ln),
+                                         ws.data_ptr(), ws.numel(), sp))
+            mq.check(lib.mq_memcpy_d2h(host.data_ptr(), out_d.data_ptr(), ln.value, sp))
+            mq.check(lib.mq_stream_sync(sp))
+            if i:
+                ms.append(1e3 * (time.perf_counter() - t0))
+    res = {"k": k, "bytes": ln.value, "ms_gpu_incl_d2h": statistics.median(ms)}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refcpu  # baseline only
+    if refcpu.have_reference():
+        from refapi import Api
+        vals = pos[:k].cpu().numpy()
+        api = Api(refcpu.reference())
+        t0 = time.perf_counter()
+        s_ref = api.print([(vals, mq.INT)])
+        res["ms_cpu_reference"] = 1e3 * (time.perf_counter() - t0)
+        res["identical"] = s_ref.encode() == host[:ln.value].numpy().tobytes()
+    return res
+
+
 def traffic_per_launch(n: int):
     """HBM bytes per k_scan launch from the committed rocprofv3 PMC summary (if one
     exists for this N): FETCH_SIZE x 2 (gfx950 halving, MI355X_MICROARCH.md §HBM) +
@@ -339,6 +374,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
         t_fused = timed(fused)
         a2 = agg.cpu()
         fused_ok = bool(c3) and (int(a2[0]), int(a2[1])) == (c3[0]["k"], c3[0]["sum"])
+        out["print_positions"] = print_leg(lib, mq, torch, dev, stream, pos, k)
         out["config2_positions"] = {
             "ms": t_pos, "rows_per_s": n / (t_pos * 1e-3), "k": k,
             "algorithmic_bytes": 4 * n + 4 * k,

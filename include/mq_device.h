@@ -124,6 +124,14 @@ int mq_fetch(const int32_t* d_col, const int32_t* d_pos, uint64_t k, int32_t* d_
 int mq_reduce(const int32_t* d_vals, uint64_t n, mq_agg* d_out, void* d_ws, size_t ws_bytes,
               void* stream);
 
+/* ---- P1 print (query.c:245-304): int32 values as decimal text ----
+ * Writes "%d" of every value, joined by "\n" (no trailing separator, no NUL),
+ * into d_out (capacity >= 12 * n bytes); *h_len receives the byte count. The
+ * call synchronises the stream. d_ws: >= mq_format_workspace_bytes(n). */
+size_t mq_format_workspace_bytes(uint64_t n);
+int mq_format_int32(const int32_t* d_vals, uint64_t n, char* d_out, uint64_t* h_len, void* d_ws,
+                    size_t ws_bytes, void* stream);
+
 /* ---- S10 add / sub (int32, two's-complement wrap) ---- */
 int mq_add(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
 int mq_sub(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);

@@ -163,3 +163,11 @@ def test_libmq_dropin_server_passes_suite_and_matches_reference(tmp_path):
     assert set(failed) <= {25}, f"server_mq failed {failed}"
     differ = [t for t in TESTS if t not in REF_FAILS and _ws(mine[t][0]) != _ws(ref[t][0])]
     assert not differ, f"server_mq output differs from the reference server on tests {differ}"
+    # every INT print through the GPU formatter (mq_format_int32), not just >= 32768 tuples
+    os.environ["MQ_PRINT_GPU_MIN"] = "1"
+    try:
+        gpu_print = run_suite(os.path.join(REFBIN, "server_mq"), str(tmp_path / "mq_gpu_print"))
+    finally:
+        del os.environ["MQ_PRINT_GPU_MIN"]
+    differ = [t for t in TESTS if _ws(gpu_print[t][0]) != _ws(mine[t][0])]
+    assert not differ, f"GPU-formatted print differs on tests {differ}"

@@ -387,6 +387,41 @@ def test_query_api_print_and_empty(lib):
     assert len(mine.select_column(col, 500, 600)) == 0
 
 
+def _int_edge_values(n, seed):
+    rng = np.random.default_rng(seed)
+    v = rng.integers(I32MIN, I32MAX, n, dtype=np.int64, endpoint=True).astype(np.int32)
+    edge = [I32MIN, I32MAX, 0, -1, 1, 9, 10, -9, -10, 99, 100, 999999999, 1000000000, -1000000000]
+    v[:min(n, len(edge))] = edge[:min(n, len(edge))]
+    v[len(edge):len(edge) + n // 4] = rng.integers(-1000, 1000, max(0, min(n // 4, n - len(edge))))
+    return v
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 15, 100_003, 1 << 20])
+def test_format_int32_vs_printf(lib, n):
+    v = _int_edge_values(n, n)
+    d = Dev.of(v)
+    out = Dev(max(12 * n, 1))
+    ws = Dev(max(lib.mq_format_workspace_bytes(n), 1))
+    ln = C.c_uint64()
+    mq.check(lib.mq_format_int32(d.ptr, n, out.ptr, C.byref(ln), ws.ptr, ws.nbytes, None))
+    want = "\n".join("%d" % x for x in v.tolist()).encode()
+    assert ln.value == len(want)
+    assert out.get(np.uint8, ln.value).tobytes() == want if n else ln.value == 0
+
+
+@needs_ref
+def test_query_api_print_large_vs_reference(lib, refcpu):
+    """GPU formatting of big INT results (>= 32768 tuples) next to host-formatted
+    LONG / DOUBLE / small INT results: the same bytes as the reference's print."""
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    parts = [(_int_edge_values(100_003, 1), mq.INT),
+             (np.array([1234567890123, -5], np.int64), mq.LONG),
+             (np.array([2.0 / 3.0, -1.005], np.float64), mq.DOUBLE),
+             (np.array([7, -8], np.int32), mq.INT),
+             (_int_edge_values(40_000, 2), mq.INT)]
+    assert mine.print(parts) == ref.print(parts)
+
+
 # ---------------------------------------------------------------------------
 # J1 hash join (device API) vs the oracle and the reference goldens
 # ---------------------------------------------------------------------------
