@@ -30,6 +30,13 @@ uint64_t scan_u32_scratch_elems(uint64_t n);
 int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st);
 
+// Caching device allocator for per-call scratch (join tables and partitions,
+// probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
+// idle blocks are released by mq_trim(). A freed block may be handed out again at
+// once, so callers free only what no queued kernel still uses (sync first).
+void* pool_alloc(size_t bytes);
+void pool_free(void* p);
+
 }  // namespace mqi
 
 #define HIPCHK(expr)                                                                         \

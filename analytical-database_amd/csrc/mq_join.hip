@@ -630,15 +630,14 @@ struct mq_join {
 namespace {
 
 int jalloc(mq_join* j, void** p, size_t bytes) {
-    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
-    if (e != hipSuccess)
-        return set_err(MQ_ENOMEM, "join: hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    *p = pool_alloc(bytes);
+    if (!*p) return set_err(MQ_ENOMEM, "join: device allocation of %zu bytes failed", bytes);
     j->owned[j->nowned++] = *p;
     return MQ_OK;
 }
 
 void jfree_all(mq_join* j) {
-    for (int i = 0; i < j->nowned; i++) (void)hipFree(j->owned[i]);
+    for (int i = 0; i < j->nowned; i++) pool_free(j->owned[i]);
     j->nowned = 0;
 }
 
@@ -672,17 +671,21 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t *hist = nullptr, *wstart = nullptr;
     auto done = [&](int rc) {
-        (void)hipFree(a);
-        (void)hipFree(b);
-        (void)hipFree(hist);
-        (void)hipFree(hscan);
-        (void)hipFree(scratch);
-        (void)hipFree(wstart);
+        pool_free(a);
+        pool_free(b);
+        pool_free(hist);
+        pool_free(hscan);
+        pool_free(scratch);
+        pool_free(wstart);
         return rc;
     };
-    if (hipMalloc(&a, n * 8) || (passes > 1 && hipMalloc(&b, n * 8)) || hipMalloc(&hist, nh * 4) ||
-        hipMalloc(&hscan, nh * 8) || hipMalloc(&scratch, scan_scratch_elems(nh) * 8) ||
-        hipMalloc(&wstart, ((uint64_t)nw + 1) * 4))
+    a = (u64*)pool_alloc(n * 8);
+    b = passes > 1 ? (u64*)pool_alloc(n * 8) : nullptr;
+    hist = (uint32_t*)pool_alloc(nh * 4);
+    hscan = (u64*)pool_alloc(nh * 8);
+    scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
+    wstart = (uint32_t*)pool_alloc(((uint64_t)nw + 1) * 4);
+    if (!a || (passes > 1 && !b) || !hist || !hscan || !scratch || !wstart)
         return done(set_err(MQ_ENOMEM, "join: window build buffers (%llu rows)", (unsigned long long)n));
     u64* src = nullptr;
     u64* dst = a;
@@ -725,18 +728,23 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
     const uint64_t ntiles = ceil_div(n, kSortTile);
     const uint64_t nh = ntiles * kRadix;
     auto fail = [&](int rc) {
-        (void)hipFree(k1);
-        (void)hipFree(v1);
-        (void)hipFree(hist);
-        (void)hipFree(hscan);
-        (void)hipFree(scratch);
-        (void)hipFree(k0);
-        (void)hipFree(v0);
+        pool_free(k1);
+        pool_free(v1);
+        pool_free(hist);
+        pool_free(hscan);
+        pool_free(scratch);
+        pool_free(k0);
+        pool_free(v0);
         return rc;
     };
-    if (hipMalloc(&k0, n * 4) || hipMalloc(&v0, n * 4) || hipMalloc(&k1, n * 4) ||
-        hipMalloc(&v1, n * 4) || hipMalloc(&hist, nh * 4) || hipMalloc(&hscan, nh * 8) ||
-        hipMalloc(&scratch, scan_scratch_elems(nh) * 8))
+    k0 = (uint32_t*)pool_alloc(n * 4);
+    v0 = (uint32_t*)pool_alloc(n * 4);
+    k1 = (uint32_t*)pool_alloc(n * 4);
+    v1 = (uint32_t*)pool_alloc(n * 4);
+    hist = (uint32_t*)pool_alloc(nh * 4);
+    hscan = (u64*)pool_alloc(nh * 8);
+    scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
+    if (!k0 || !v0 || !k1 || !v1 || !hist || !hscan || !scratch)
         return fail(set_err(MQ_ENOMEM, "join: sort buffers (%llu rows)", (unsigned long long)n));
     hipLaunchKernelGGL(k_flip_keys, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, n, k0);
     if (hipMemcpyAsync(v0, p1, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -757,11 +765,12 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
         v0 = v1;
         v1 = t;
     }
-    (void)hipFree(k1);
-    (void)hipFree(v1);
-    (void)hipFree(hist);
-    (void)hipFree(hscan);
-    (void)hipFree(scratch);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_err(MQ_EHIP, "join: sort sync"));
+    pool_free(k1);
+    pool_free(v1);
+    pool_free(hist);
+    pool_free(hscan);
+    pool_free(scratch);
     *keys_out = k0;
     *vals_out = v0;
     return MQ_OK;
@@ -845,18 +854,22 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (rc) return rc;
     if (!j || !h_m || (n2 && !d_c2)) return set_err(MQ_EINVAL, "mq_join_probe: bad argument");
     hipStream_t st = (hipStream_t)stream;
-    (void)hipFree(j->pstart);
-    (void)hipFree(j->plen);
-    (void)hipFree(j->offs);
-    (void)hipFree(j->scan_scratch);
+    if (j->pstart) HIPCHK(hipDeviceSynchronize());  // a queued write may still read them
+    pool_free(j->pstart);
+    pool_free(j->plen);
+    pool_free(j->offs);
+    pool_free(j->scan_scratch);
     j->pstart = j->plen = nullptr;
     j->offs = j->scan_scratch = nullptr;
     j->n2 = n2;
     j->m = 0;
     *h_m = 0;
     if (n2 == 0 || j->n1 == 0) return MQ_OK;
-    if (hipMalloc(&j->pstart, n2 * 4) || hipMalloc(&j->plen, n2 * 4) ||
-        hipMalloc(&j->offs, n2 * 8) || hipMalloc(&j->scan_scratch, scan_scratch_elems(n2) * 8))
+    j->pstart = (uint32_t*)pool_alloc(n2 * 4);
+    j->plen = (uint32_t*)pool_alloc(n2 * 4);
+    j->offs = (u64*)pool_alloc(n2 * 8);
+    j->scan_scratch = (u64*)pool_alloc(scan_scratch_elems(n2) * 8);
+    if (!j->pstart || !j->plen || !j->offs || !j->scan_scratch)
         return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
     if (j->unique)
         hipLaunchKernelGGL(k_ht_probe_unique, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
@@ -891,10 +904,11 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
 
 int mq_join_free(mq_join* j) {
     if (!j) return MQ_OK;
-    (void)hipFree(j->pstart);
-    (void)hipFree(j->plen);
-    (void)hipFree(j->offs);
-    (void)hipFree(j->scan_scratch);
+    (void)hipDeviceSynchronize();  // queued probe/write kernels may still use the buffers
+    pool_free(j->pstart);
+    pool_free(j->plen);
+    pool_free(j->offs);
+    pool_free(j->scan_scratch);
     jfree_all(j);
     delete j;
     return MQ_OK;

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
+#include <vector>
 #include <climits>
 #include <cstdarg>
 #include <cstdint>
@@ -966,6 +968,67 @@ int ensure_ready(DevState** out) {
     return MQ_OK;
 }
 
+namespace {
+struct PoolBlock {
+    void* p;
+    size_t bytes;
+    int dev;
+    bool busy;
+};
+std::mutex g_pool_mu;
+std::vector<PoolBlock> g_pool;
+
+void pool_release_idle_locked() {
+    for (size_t i = 0; i < g_pool.size();) {
+        if (!g_pool[i].busy) {
+            (void)hipFree(g_pool[i].p);
+            g_pool[i] = g_pool.back();
+            g_pool.pop_back();
+        } else {
+            i++;
+        }
+    }
+}
+}  // namespace
+
+void* pool_alloc(size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    PoolBlock* best = nullptr;
+    for (auto& b : g_pool)
+        if (!b.busy && b.dev == dev && b.bytes >= bytes && b.bytes / 2 <= bytes &&
+            (!best || b.bytes < best->bytes))
+            best = &b;
+    if (best) {
+        best->busy = true;
+        return best->p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        pool_release_idle_locked();  // give the cache back and retry once
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    }
+    g_pool.push_back(PoolBlock{p, bytes, dev, true});
+    return p;
+}
+
+void pool_free(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto& b : g_pool)
+        if (b.p == p) {
+            b.busy = false;
+            return;
+        }
+    (void)hipFree(p);  // not from the pool
+}
+
 uint32_t stream_grid(const DevState* s, uint64_t work_items) {
     uint64_t g = (work_items + kTPB - 1) / kTPB;
     const uint64_t cap = (uint64_t)s->cus * 8;
@@ -1215,6 +1278,12 @@ int mq_memset(void* dptr, int value, size_t bytes, void* stream) {
 int mq_stream_sync(void* stream) {
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
     return MQ_OK;
+}
+
+void mq_trim(void) {
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    pool_release_idle_locked();
 }
 
 size_t mq_scan_workspace_bytes(uint64_t n) {

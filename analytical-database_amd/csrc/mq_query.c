@@ -794,6 +794,7 @@ const void* mq_result_device_ptr(const Result* result) {
 }
 
 void mq_release_all(void) {
+    mq_trim();
     mq_free(g_print_out);
     mq_free(g_print_ws);
     g_print_out = g_print_ws = NULL;

@@ -111,6 +111,7 @@ _SIGS = {
     "mq_select_sum": (_int, [_vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
     "mq_format_workspace_bytes": (_sz, [_u64]),
     "mq_format_int32": (_int, [_vp, _u64, _vp, C.POINTER(C.c_uint64), _vp, _sz, _vp]),
+    "mq_trim": (None, []),
     "mq_stream_read": (_int, [_vp, _u64, _vp, _sz, C.POINTER(C.c_uint64), _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,

@@ -55,6 +55,9 @@ int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memset(void* dptr, int value, size_t bytes, void* stream);
 int mq_stream_sync(void* stream);
 void* mq_default_stream(void);
+/* Release the device scratch libmq keeps cached between calls (join tables and
+ * partition buffers, probe arrays); the next call allocates afresh. */
+void mq_trim(void);
 
 /* Workspace (device bytes) needed by the scan entry points for n rows. */
 size_t mq_scan_workspace_bytes(uint64_t n);

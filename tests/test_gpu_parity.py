@@ -490,6 +490,24 @@ def test_hash_join_vs_oracle(lib, refcpu, case):
             assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
 
 
+def test_hash_join_scratch_reuse_and_trim(lib, refcpu):
+    """Join scratch comes from libmq's caching pool: back-to-back joins of
+    different sizes reuse (and outgrow) blocks, mq_trim() releases them, and every
+    result still matches the oracle."""
+    rng = np.random.default_rng(77)
+    for rep, (n1, n2) in enumerate([(300_000, 200_000), (100_000, 400_000), (300_000, 200_000),
+                                    (70_000, 5_000), (500_000, 100_000)]):
+        c1 = rng.permutation(refcpu.gen_join(n1, "build"))
+        c2 = refcpu.gen_join(n2, "probe")
+        p1 = rng.integers(0, 10 ** 7, n1, dtype=np.int32)
+        p2 = rng.integers(0, 10 ** 7, n2, dtype=np.int32)
+        g1, g2 = _dev_join(lib, c1, p1, c2, p2)
+        w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
+        assert np.array_equal(g1, w1) and np.array_equal(g2, w2), rep
+        if rep == 2:
+            lib.mq_trim()
+
+
 def _join_golden(lib, refcpu, n):
     D = {k: Dev(n * 4) for k in ("a", "b", "p")}
     mq.check(lib.mq_gen_join_keys(D["a"].ptr, n, 0, None))
