@@ -120,10 +120,19 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for the N > 1 path on a one-GPU box (never set by the driver):
+    # MQ_BENCH_BACKEND=gloo and MQ_BENCH_ONE_DEVICE=1 put every rank on GPU 0
+    # (RCCL refuses two ranks per GPU; gloo combines through host memory).
+    if os.environ.get("MQ_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     lib = mq.load()
     mq.check(lib.mq_init(local), "mq_init")
