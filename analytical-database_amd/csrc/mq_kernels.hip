@@ -778,6 +778,252 @@ __global__ __launch_bounds__(kTPB, 7) void k_select_lb(
 }
 
 // ---------------------------------------------------------------------------
+// k_select_stage: ordered compaction in ONE launch (select_column_scan /
+// select_result, query.c:38-137). Default positions path.
+//   * block b's 4 waves each own a contiguous run of rw rows (wave unit
+//     u = 4b + w, rows [u*rw, (u+1)*rw)) and stream it like k_scan (nt dwordx4,
+//     8 x 256-row wave tiles in flight);
+//   * positions mode: a tile's matches are ranked by 4 ballots (mbcnt) and
+//     appended in row order to the wave's 1024-entry LDS buffer; nothing is
+//     written to HBM while the wave's matches fit there (at 1 % selectivity a wave
+//     sees ~1200 matches);
+//   * bitmap mode: from the first tile that would overflow the buffer on, the wave
+//     stores each tile's 4 ballot words (32 B per 256 rows) to the workspace
+//     instead, like k_mask, and counts;
+//   * end: each block publishes its count ({done, count} in one 64-bit word) and
+//     sums ALL lower blocks' words in one parallel sweep (blocks finish together,
+//     so a look-back chain would serialise); each wave then writes its buffer to
+//     out[D ...] and expands its bitmap tiles after it, like k_compact.
+// Every output word is written once, at its final place (no staging in the output,
+// so no write-after-read between blocks). HBM traffic: 4N + 4K + 2 x (N_b/8) where
+// N_b is the rows scanned in bitmap mode (0 for sparse waves, ~N at high
+// selectivity). Blocks wait only for blocks with lower blockIdx, at the very end:
+// workgroups are dispatched in grid order, so those are running or done (spins are
+// bounded; a timeout sets the error word and poisons the count).
+// ---------------------------------------------------------------------------
+constexpr int kStTiles = 8;                        // wave tiles (256 rows) in flight per lane
+constexpr int kStGranule = 256 * kStTiles;         // rows per wave iteration
+constexpr int kStBuf = 1024;                       // LDS positions per wave
+constexpr unsigned long long kStDone = 1ull << 63;
+
+__device__ __forceinline__ uint32_t rank_lt(unsigned long long m, uint32_t acc) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, acc));
+}
+
+struct StageState {
+    uint32_t fill;  // matches in the wave's LDS buffer (positions mode)
+    uint32_t nbm;   // matches recorded in the bitmap (bitmap mode)
+    uint64_t sw;    // first row in bitmap mode (a tile boundary); E = never
+    bool bmode;     // wave-uniform
+};
+
+// One 256-row wave tile starting at row t0: lane l holds rows t0+4l .. t0+4l+3.
+// Bitmap mode inside the unrolled loop (J >= 0): tile J's ballot e goes to lane 4J+e
+// of the iteration's 256-byte record (rlo/rhi), stored by the caller after the next
+// iteration's loads are issued. J < 0 (the tail): stored at once.
+template <bool PAYLOAD, int BUF, bool FULL, int J>
+__device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint64_t t0, uint64_t E, uint32_t lo,
+                                           uint32_t wm1, int lane, int* buf,
+                                           const int* __restrict__ payload,
+                                           unsigned long long* __restrict__ bm, int& rlo, int& rhi) {
+    const uint64_t row0 = t0 + (uint64_t)lane * 4;
+    bool p0 = ((uint32_t)v.x - lo) <= wm1, p1 = ((uint32_t)v.y - lo) <= wm1,
+         p2 = ((uint32_t)v.z - lo) <= wm1, p3 = ((uint32_t)v.w - lo) <= wm1;
+    if (!FULL) {
+        p0 = p0 && row0 + 0 < E;
+        p1 = p1 && row0 + 1 < E;
+        p2 = p2 && row0 + 2 < E;
+        p3 = p3 && row0 + 3 < E;
+    }
+    const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
+                             m3 = __ballot(p3);
+    const uint32_t c = (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
+    if (!st.bmode) {
+        if (c == 0) return;
+        if (st.fill + c <= (uint32_t)BUF) {
+            uint32_t k = rank_lt(m3, rank_lt(m2, rank_lt(m1, rank_lt(m0, st.fill))));
+            if (p0) buf[k++] = PAYLOAD ? payload[row0 + 0] : (int)(row0 + 0);
+            if (p1) buf[k++] = PAYLOAD ? payload[row0 + 1] : (int)(row0 + 1);
+            if (p2) buf[k++] = PAYLOAD ? payload[row0 + 2] : (int)(row0 + 2);
+            if (p3) buf[k++] = PAYLOAD ? payload[row0 + 3] : (int)(row0 + 3);
+            st.fill += c;
+            return;
+        }
+        st.bmode = true;
+        st.sw = t0;
+    }
+    if (J >= 0) {
+        rlo = mq_writelane((int)m0, 4 * J + 0, rlo);
+        rhi = mq_writelane((int)(m0 >> 32), 4 * J + 0, rhi);
+        rlo = mq_writelane((int)m1, 4 * J + 1, rlo);
+        rhi = mq_writelane((int)(m1 >> 32), 4 * J + 1, rhi);
+        rlo = mq_writelane((int)m2, 4 * J + 2, rlo);
+        rhi = mq_writelane((int)(m2 >> 32), 4 * J + 2, rhi);
+        rlo = mq_writelane((int)m3, 4 * J + 3, rlo);
+        rhi = mq_writelane((int)(m3 >> 32), 4 * J + 3, rhi);
+    } else if (lane < 4) {
+        bm[(t0 >> 8) * 4 + (uint64_t)lane] = lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
+    }
+    st.nbm += c;
+}
+
+template <bool PAYLOAD, bool VEC, int BUF = kStBuf>
+__global__ __launch_bounds__(kTPB, 8) void k_select_stage(
+    const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, uint64_t rw, Pred pred,
+    unsigned long long* status, unsigned long long* __restrict__ bm, int* __restrict__ out,
+    unsigned long long* __restrict__ d_count, unsigned int* err) {
+    __shared__ int s_buf[kWaves][BUF > 0 ? BUF : 1];
+    __shared__ unsigned int s_cnt[kWaves];
+    __shared__ unsigned long long s_red[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lo = pred.lo, wm1 = pred.wm1;
+    const uint32_t b = blockIdx.x;
+    uint64_t S = ((uint64_t)b * kWaves + (uint64_t)wave) * rw;
+    if (S > n) S = n;
+    uint64_t E = S + rw;
+    if (E > n) E = n;
+    StageState st{0u, 0u, E, false};
+    int rlo = 0, rhi = 0;           // bitmap record of the current iteration
+    unsigned long long rec = 0;     // ... and of the previous one, pending store
+    uint64_t rec_at = ~0ull;
+    uint64_t t = S;
+    for (; t + kStGranule <= E; t += kStGranule) {
+        int4 v[kStTiles];
+#pragma unroll
+        for (int j = 0; j < kStTiles; j++)
+            v[j] = load4_nt<VEC>(col + t + (uint64_t)j * 256 + (uint64_t)lane * 4);
+        // vmcnt retires loads and stores in order: storing the previous record only
+        // now keeps its write round trip off this iteration's first wait (k_mask)
+        if (rec_at != ~0ull && lane < 32) bm[rec_at + (uint64_t)lane] = rec;
+        rec_at = ~0ull;
+        stage_tile<PAYLOAD, BUF, true, 0>(st, v[0], t + 0 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 1>(st, v[1], t + 1 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 2>(st, v[2], t + 2 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 3>(st, v[3], t + 3 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 4>(st, v[4], t + 4 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 5>(st, v[5], t + 5 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 6>(st, v[6], t + 6 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        stage_tile<PAYLOAD, BUF, true, 7>(st, v[7], t + 7 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        if (st.bmode) {  // words of tiles before the switch are garbage and never read
+            rec = (unsigned long long)(uint32_t)rlo | ((unsigned long long)(uint32_t)rhi << 32);
+            rec_at = (t >> 8) * 4;
+        }
+    }
+    if (rec_at != ~0ull && lane < 32) bm[rec_at + (uint64_t)lane] = rec;
+    for (; t < E; t += 256) {  // the last unit's tail, one wave tile at a time
+        const uint64_t row = t + (uint64_t)lane * 4;
+        int4 v;
+        v.x = row + 0 < E ? col[row + 0] : 0;
+        v.y = row + 1 < E ? col[row + 1] : 0;
+        v.z = row + 2 < E ? col[row + 2] : 0;
+        v.w = row + 3 < E ? col[row + 3] : 0;
+        stage_tile<PAYLOAD, BUF, false, -1>(st, v, t, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+    }
+    int* buf = s_buf[wave];
+    const uint32_t fill = st.fill, nbm = st.nbm;
+    const uint64_t sw = st.sw;
+
+    // ---- block count, then the exclusive prefix over every lower block
+    const uint32_t mine = fill + nbm;
+    if (lane == 0) s_cnt[wave] = mine;
+    __syncthreads();
+    unsigned long long blk = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) blk += s_cnt[w];
+    if (tid == 0) store_agent(&status[b], kStDone | blk);
+    unsigned long long acc = 0;
+    for (uint32_t i = tid; i < b; i += kTPB) {
+        unsigned long long x;
+        unsigned int spins = 0;
+        while (!((x = load_agent(&status[i])) & kStDone)) {
+            if (++spins > (1u << 26)) {  // never expected; fail loudly, never hang
+                atomicOr(err, 1u);
+                x = kStDone;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        acc += x & ~kStDone;
+    }
+    acc = wave_sum_u64(acc);
+    if (lane == 0) s_red[wave] = acc;
+    __syncthreads();
+    unsigned long long D = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) D += s_red[w];
+    if (b == gridDim.x - 1 && tid == 0)
+        *d_count = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? ~0ull : D + blk;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++)
+        if (w < wave) D += s_cnt[w];
+
+    // ---- positions mode part: the LDS buffer, in order
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i];
+    if (sw >= E) return;
+    // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's bitmap stores are done
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    unsigned long long o = D + fill;
+    const uint64_t T1 = (E + 255) >> 8;
+    for (uint64_t tb = sw >> 8; tb < T1; tb += 64) {
+        const uint64_t T = tb + (uint64_t)lane;
+        unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        if (T < T1) {
+            const ulonglong2 a = reinterpret_cast<const ulonglong2*>(bm + T * 4)[0];
+            const ulonglong2 c2 = reinterpret_cast<const ulonglong2*>(bm + T * 4)[1];
+            w0 = a.x;
+            w1 = a.y;
+            w2 = c2.x;
+            w3 = c2.y;
+        }
+        const unsigned int c = (unsigned int)(__popcll(w0) + __popcll(w1) + __popcll(w2) + __popcll(w3));
+        unsigned int incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned int y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const unsigned int tot = __shfl(incl, 63, 64);
+        const unsigned long long ol = o + (incl - c);
+        const uint64_t row0 = T * 256;
+        if (tot > 1024) {
+            // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e)
+            for (int j = 0; j < 64; j++) {
+                if (__shfl(c, j, 64) == 0) continue;
+                const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
+                                         x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
+                const unsigned long long oj = __shfl(ol, j, 64);
+                const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
+                const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
+                                                        __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
+                int* q = out + oj + pre;
+                unsigned int k = 0;
+                if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 0] : (int)(rj + 0);
+                if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 1] : (int)(rj + 1);
+                if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 2] : (int)(rj + 2);
+                if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 3] : (int)(rj + 3);
+            }
+        } else if (c) {
+            // sparse: each lane emits its own tile's rows in order
+            unsigned long long oo = ol;
+            unsigned long long m = w0 | w1 | w2 | w3;
+            while (m) {
+                const int l = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const uint64_t r = row0 + 4 * (uint64_t)l;
+                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0);
+                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1);
+                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2);
+                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3);
+            }
+        }
+        o += tot;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // fetch (query.c:223-243): out[i] = col[pos[i]], 4 positions per lane.
 // ---------------------------------------------------------------------------
 template <bool VEC>
@@ -1146,16 +1392,51 @@ int run_agg(const int32_t* col, const int32_t* aux, uint64_t n, Pred pred, mq_ag
                : launch_scan<kAgg>(col, nullptr, n, pred, part, d_out, st, s, &g);
 }
 
-// Ordered compaction: two streaming kernels (k_mask + k_compact, default) or the
-// single-pass decoupled look-back (MQ_POSITIONS_IMPL=lookback). Measured on 1e9 rows
-// (DESIGN.md §3.2): mask 0.84 / 1.57 ms vs look-back 1.05 / 1.66 ms at 1 % / 50 %.
-bool use_mask_compaction() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("MQ_POSITIONS_IMPL");
-        v = (e && strcmp(e, "lookback") == 0) ? 0 : 1;
+// Ordered compaction implementations (MQ_POSITIONS_IMPL, read per call):
+//   stage    (default) k_select_stage, one pass, 4N + 4K (+ staging) bytes;
+//   mask     k_mask + k_compact, 4N + N/8 + N/8 + 4K bytes;
+//   lookback k_select_lb, per-tile decoupled look-back.
+// Measured on 1e9 rows in DESIGN.md §3.2.
+enum PosImpl { kPosStage = 0, kPosMask = 1, kPosLookback = 2 };
+PosImpl positions_impl() {
+    const char* e = getenv("MQ_POSITIONS_IMPL");
+    if (e && strcmp(e, "mask") == 0) return kPosMask;
+    if (e && strcmp(e, "lookback") == 0) return kPosLookback;
+    return kPosStage;
+}
+
+// k_select_stage state: [err u32 | pad][status u64 x G] in the partial slab; the
+// bitmap (bitmap-mode tiles only) in the mask area after it.
+size_t stage_state_bytes(uint32_t g) { return 64 + (size_t)g * 8; }
+static_assert(64 + (size_t)kMaxBlocks * 8 <= (size_t)kMaxBlocks * sizeof(Partial),
+              "stage state must fit the partial slab");
+
+int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pred p, int32_t* out,
+                     uint64_t* d_count, void* d_ws, hipStream_t st, const DevState* s) {
+    const bool vec = aligned16(col);
+    const void* fn = payload ? (vec ? (const void*)&k_select_stage<true, true> : (const void*)&k_select_stage<true, false>)
+                             : (vec ? (const void*)&k_select_stage<false, true> : (const void*)&k_select_stage<false, false>);
+    uint64_t gmax = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
+    if (gmax > kMaxBlocks) gmax = kMaxBlocks;
+    const uint64_t granules = (n + kStGranule - 1) / kStGranule;
+    const uint64_t units = gmax * kWaves;
+    const uint64_t rw = ((granules + units - 1) / units) * kStGranule;
+    const uint32_t g = (uint32_t)((n + rw * kWaves - 1) / (rw * kWaves));
+    char* w = static_cast<char*>(d_ws);
+    unsigned int* err = reinterpret_cast<unsigned int*>(w);
+    unsigned long long* status = reinterpret_cast<unsigned long long*>(w + 64);
+    unsigned long long* bm = reinterpret_cast<unsigned long long*>(w + partial_bytes());
+    HIPCHK(hipMemsetAsync(w, 0, stage_state_bytes(g), st));
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
+    if (payload) {
+        if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_select_stage<false, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_stage<false, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
     }
-    return v == 1;
+    LAUNCHCHK("k_select_stage");
+    return MQ_OK;
 }
 
 size_t lb_status_bytes(uint64_t n) {
@@ -1473,7 +1754,10 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
     if (!d_ws || ws_bytes < mq_scan_workspace_bytes(n))
         return set_err(MQ_EINVAL, "mq_select_positions: workspace too small (%zu < %zu)", ws_bytes,
                        mq_scan_workspace_bytes(n));
-    if (!use_mask_compaction())
+    const PosImpl impl = positions_impl();
+    if (impl == kPosStage)
+        return run_select_stage(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, st, s);
+    if (impl == kPosLookback)
         return run_select_lb(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, ws_bytes, st, s);
     uint32_t g;
     uint64_t rpb;

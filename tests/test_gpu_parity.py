@@ -71,8 +71,17 @@ def _data(n, seed):
     return d
 
 
+POS_IMPLS = ["stage", "mask", "lookback"]  # MQ_POSITIONS_IMPL (read by libmq per call)
+
+
+@pytest.fixture(params=POS_IMPLS)
+def pos_impl(request, monkeypatch):
+    monkeypatch.setenv("MQ_POSITIONS_IMPL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n", SIZES)
-def test_select_agg_and_positions_vs_oracle(lib, refcpu, n):
+def test_select_agg_and_positions_vs_oracle(lib, refcpu, n, pos_impl):
     d = _data(n, n)
     for off in (0, 1):  # 16-B aligned column and an unaligned (+4 B) one
         dd = Dev.of(d, offset_elems=off)
@@ -130,8 +139,8 @@ def test_select_sum_in_kernel_combine_repeated(lib, refcpu):
             assert (a.count, a.sum) == want[n], (r, n)
 
 
-@pytest.mark.parametrize("n", [0, 7, 4097, 200_003])
-def test_select_result_payload_vs_oracle(lib, refcpu, n):
+@pytest.mark.parametrize("n", [0, 7, 4097, 200_003, 3_000_017])
+def test_select_result_payload_vs_oracle(lib, refcpu, n, pos_impl):
     rng = np.random.default_rng(n + 1)
     vals = rng.integers(-100, 100, n, dtype=np.int32)
     prev = np.sort(rng.choice(10 ** 7, n, replace=False)).astype(np.int32)
@@ -139,6 +148,36 @@ def test_select_result_payload_vs_oracle(lib, refcpu, n):
     for lo, hi in BOUNDS:
         assert np.array_equal(_positions(lib, dv.ptr, n, lo, hi, dp.ptr),
                               refcpu.select_result(vals, prev, lo, hi)), (n, lo, hi)
+
+
+def test_positions_stage_repeated_queued(lib, refcpu):
+    """k_select_stage: waves switch from the LDS buffer to bitmap mode at different
+    points (selectivities from 0.1 % to 100 %); blocks combine counts across the
+    grid at the end. Every launch (three queued back to back, one sync) must
+    equal the oracle's list word for word, with the mask path as a second opinion."""
+    n = 20_000_003
+    rng = np.random.default_rng(77)
+    d = rng.integers(0, 1000, n, dtype=np.int32)
+    dd = Dev.of(d)
+    cases = [(0, 1), (0, 10), (0, 250), (100, 600), (0, 999), (0, 1000), (500, 501)]
+    want = {c: refcpu.select_scan(d, *c) for c in cases}
+    ws = Dev(lib.mq_scan_workspace_bytes(n))
+    outs = [Dev(n * 4) for _ in range(3)]
+    cnts = [Dev(8) for _ in range(3)]
+    os.environ["MQ_POSITIONS_IMPL"] = "stage"
+    try:
+        for rep in range(3):
+            for lo, hi in cases:
+                hl, l, hh, h = mq.bounds(lo, hi)
+                for i in range(3):  # three launches queued, one sync
+                    mq.check(lib.mq_select_positions(dd.ptr, None, n, hl, l, hh, h, outs[i].ptr,
+                                                     cnts[i].ptr, ws.ptr, ws.nbytes, None))
+                for i in range(3):
+                    k = int(cnts[i].get(np.uint64, 1)[0])
+                    assert k == len(want[(lo, hi)]), (rep, lo, hi, i)
+                    assert np.array_equal(outs[i].get(np.int32, k), want[(lo, hi)]), (rep, lo, hi, i)
+    finally:
+        os.environ.pop("MQ_POSITIONS_IMPL", None)
 
 
 @pytest.mark.parametrize("k", [0, 1, 5, 4096, 100_003])
