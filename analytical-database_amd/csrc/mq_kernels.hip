@@ -784,12 +784,12 @@ __global__ __launch_bounds__(kTPB, 7) void k_select_lb(
 //     u = 4b + w, rows [u*rw, (u+1)*rw)) and stream it like k_scan (nt dwordx4,
 //     8 x 256-row wave tiles in flight);
 //   * positions mode: a tile's matches are ranked by 4 ballots (mbcnt) and
-//     appended in row order to the wave's 1024-entry LDS buffer; nothing is
-//     written to HBM while the wave's matches fit there (at 1 % selectivity a wave
-//     sees ~1200 matches);
-//   * bitmap mode: from the first tile that would overflow the buffer on, the wave
-//     stores each tile's 4 ballot words (32 B per 256 rows) to the workspace
-//     instead, like k_mask, and counts;
+//     appended in row order to the wave's 1024-entry LDS ring; when the ring is
+//     full its oldest entries spill to the wave's own workspace slice, as long as
+//     the spilled positions take no more bytes than the bitmap of the rows already
+//     scanned would (match density below 1/32);
+//   * bitmap mode: past that, the wave stores each tile's 4 ballot words (32 B per
+//     256 rows) to the workspace instead, like k_mask, and counts;
 //   * end: each block publishes its count ({done, count} in one 64-bit word) and
 //     sums ALL lower blocks' words in one parallel sweep (blocks finish together,
 //     so a look-back chain would serialise); each wave then writes its buffer to
@@ -811,22 +811,31 @@ __device__ __forceinline__ uint32_t rank_lt(unsigned long long m, uint32_t acc) 
 }
 
 struct StageState {
-    uint32_t fill;  // matches in the wave's LDS buffer (positions mode)
-    uint32_t nbm;   // matches recorded in the bitmap (bitmap mode)
-    uint64_t sw;    // first row in bitmap mode (a tile boundary); E = never
-    bool bmode;     // wave-uniform
+    uint32_t fill;     // matches appended in positions mode (monotonic)
+    uint32_t flushed;  // ... of which the oldest `flushed` spilled to the workspace
+    uint32_t nbm;      // matches recorded in the bitmap (bitmap mode)
+    uint64_t sw;       // first row in bitmap mode (a tile boundary); E = never
+    bool bmode;        // wave-uniform
 };
 
 // One 256-row wave tile starting at row t0: lane l holds rows t0+4l .. t0+4l+3.
+// Positions mode: matches go to the wave's LDS ring (BUF entries, entry i at
+// ring[i % BUF]); when a tile does not fit, the oldest entries spill, 64 at a time,
+// to the start of the wave's own workspace slice (`spill`, the bytes its bitmap
+// would use) while the spilled positions take no more room than the bitmap of the
+// rows already finished (<= 8 per tile before the current iteration, tile r0):
+// density < 1/32, where positions are the smaller form. Past that: bitmap mode.
 // Bitmap mode inside the unrolled loop (J >= 0): tile J's ballot e goes to lane 4J+e
 // of the iteration's 256-byte record (rlo/rhi), stored by the caller after the next
 // iteration's loads are issued. J < 0 (the tail): stored at once.
+// Rows are 32-bit here: positions are int32, so n < 2^31 (mq_select_positions).
 template <bool PAYLOAD, int BUF, bool FULL, int J>
-__device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint64_t t0, uint64_t E, uint32_t lo,
+__device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint32_t t0, uint32_t E, uint32_t lo,
                                            uint32_t wm1, int lane, int* buf,
                                            const int* __restrict__ payload,
-                                           unsigned long long* __restrict__ bm, int& rlo, int& rhi) {
-    const uint64_t row0 = t0 + (uint64_t)lane * 4;
+                                           unsigned long long* __restrict__ bm, int* __restrict__ spill,
+                                           uint32_t r0, int& rlo, int& rhi) {
+    const uint32_t row0 = t0 + (uint32_t)lane * 4;
     bool p0 = ((uint32_t)v.x - lo) <= wm1, p1 = ((uint32_t)v.y - lo) <= wm1,
          p2 = ((uint32_t)v.z - lo) <= wm1, p3 = ((uint32_t)v.w - lo) <= wm1;
     if (!FULL) {
@@ -837,16 +846,29 @@ __device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint64_t t0, 
     }
     const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
                              m3 = __ballot(p3);
-    const uint32_t c = (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
+    // all state is wave-uniform; readfirstlane keeps it in SGPRs
+    const uint32_t c = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3)));
     if (!st.bmode) {
         if (c == 0) return;
-        if (st.fill + c <= (uint32_t)BUF) {
+        const uint32_t over = st.fill + c - st.flushed;
+        const uint32_t need = __builtin_amdgcn_readfirstlane(
+            over > (uint32_t)BUF ? ((over - (uint32_t)BUF + 63u) & ~63u) : 0u);
+        if (st.flushed + need <= 8u * r0) {
+            if (need) {
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t f = 0; f < need; f += 64u) {  // spill the oldest entries, 64 at a time
+                    const uint32_t i = st.flushed + f + (uint32_t)lane;
+                    spill[i] = buf[i % (uint32_t)BUF];
+                }
+                st.flushed = __builtin_amdgcn_readfirstlane(st.flushed + need);
+            }
             uint32_t k = rank_lt(m3, rank_lt(m2, rank_lt(m1, rank_lt(m0, st.fill))));
-            if (p0) buf[k++] = PAYLOAD ? payload[row0 + 0] : (int)(row0 + 0);
-            if (p1) buf[k++] = PAYLOAD ? payload[row0 + 1] : (int)(row0 + 1);
-            if (p2) buf[k++] = PAYLOAD ? payload[row0 + 2] : (int)(row0 + 2);
-            if (p3) buf[k++] = PAYLOAD ? payload[row0 + 3] : (int)(row0 + 3);
-            st.fill += c;
+            if (p0) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 0] : (int)(row0 + 0);
+            if (p1) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 1] : (int)(row0 + 1);
+            if (p2) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 2] : (int)(row0 + 2);
+            if (p3) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 3] : (int)(row0 + 3);
+            st.fill = __builtin_amdgcn_readfirstlane(st.fill + c);
             return;
         }
         st.bmode = true;
@@ -862,9 +884,9 @@ __device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint64_t t0, 
         rlo = mq_writelane((int)m3, 4 * J + 3, rlo);
         rhi = mq_writelane((int)(m3 >> 32), 4 * J + 3, rhi);
     } else if (lane < 4) {
-        bm[(t0 >> 8) * 4 + (uint64_t)lane] = lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
+        bm[(uint64_t)(t0 >> 8) * 4 + (uint64_t)lane] = lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
     }
-    st.nbm += c;
+    st.nbm = __builtin_amdgcn_readfirstlane(st.nbm + c);
 }
 
 template <bool PAYLOAD, bool VEC, int BUF = kStBuf>
@@ -883,45 +905,49 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     if (S > n) S = n;
     uint64_t E = S + rw;
     if (E > n) E = n;
-    StageState st{0u, 0u, E, false};
+    StageState st{0u, 0u, 0u, E, false};
+    int* spill = reinterpret_cast<int*>(bm + (S >> 8) * 4);  // this wave's workspace slice
     int rlo = 0, rhi = 0;           // bitmap record of the current iteration
     unsigned long long rec = 0;     // ... and of the previous one, pending store
-    uint64_t rec_at = ~0ull;
-    uint64_t t = S;
-    for (; t + kStGranule <= E; t += kStGranule) {
+    uint32_t rec_at = ~0u;          // its first tile (global index), ~0 = none
+    const uint32_t S32 = (uint32_t)S, E32 = (uint32_t)E;
+    uint32_t t = S32;
+    for (; t + kStGranule <= E32; t += kStGranule) {
+        const int* base = col + t;  // wave-uniform
         int4 v[kStTiles];
 #pragma unroll
-        for (int j = 0; j < kStTiles; j++)
-            v[j] = load4_nt<VEC>(col + t + (uint64_t)j * 256 + (uint64_t)lane * 4);
+        for (int j = 0; j < kStTiles; j++) v[j] = load4_nt<VEC>(base + (uint32_t)(j * 256 + lane * 4));
         // vmcnt retires loads and stores in order: storing the previous record only
         // now keeps its write round trip off this iteration's first wait (k_mask)
-        if (rec_at != ~0ull && lane < 32) bm[rec_at + (uint64_t)lane] = rec;
-        rec_at = ~0ull;
-        stage_tile<PAYLOAD, BUF, true, 0>(st, v[0], t + 0 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 1>(st, v[1], t + 1 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 2>(st, v[2], t + 2 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 3>(st, v[3], t + 3 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 4>(st, v[4], t + 4 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 5>(st, v[5], t + 5 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 6>(st, v[6], t + 6 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
-        stage_tile<PAYLOAD, BUF, true, 7>(st, v[7], t + 7 * 256, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        if (rec_at != ~0u && lane < 32) bm[(uint64_t)rec_at * 4 + (uint64_t)lane] = rec;
+        rec_at = ~0u;
+        const uint32_t r0 = (t - S32) >> 8;  // this iteration's first tile in the wave's slice
+#pragma unroll
+        for (int j = 0; j < kStTiles; j++) {
+            switch (j) {  // J must be a constant for the writelane lane index
+#define MQ_ST(JJ) case JJ: stage_tile<PAYLOAD, BUF, true, JJ>(st, v[JJ], t + JJ * 256, E32, lo, wm1, lane, s_buf[wave], payload, bm, spill, r0, rlo, rhi); break;
+                MQ_ST(0) MQ_ST(1) MQ_ST(2) MQ_ST(3) MQ_ST(4) MQ_ST(5) MQ_ST(6) MQ_ST(7)
+#undef MQ_ST
+            }
+        }
         if (st.bmode) {  // words of tiles before the switch are garbage and never read
             rec = (unsigned long long)(uint32_t)rlo | ((unsigned long long)(uint32_t)rhi << 32);
-            rec_at = (t >> 8) * 4;
+            rec_at = t >> 8;
         }
     }
-    if (rec_at != ~0ull && lane < 32) bm[rec_at + (uint64_t)lane] = rec;
-    for (; t < E; t += 256) {  // the last unit's tail, one wave tile at a time
-        const uint64_t row = t + (uint64_t)lane * 4;
+    if (rec_at != ~0u && lane < 32) bm[(uint64_t)rec_at * 4 + (uint64_t)lane] = rec;
+    for (; t < E32; t += 256) {  // the last unit's tail, one wave tile at a time
+        const uint32_t row = t + (uint32_t)lane * 4;
         int4 v;
-        v.x = row + 0 < E ? col[row + 0] : 0;
-        v.y = row + 1 < E ? col[row + 1] : 0;
-        v.z = row + 2 < E ? col[row + 2] : 0;
-        v.w = row + 3 < E ? col[row + 3] : 0;
-        stage_tile<PAYLOAD, BUF, false, -1>(st, v, t, E, lo, wm1, lane, s_buf[wave], payload, bm, rlo, rhi);
+        v.x = row + 0 < E32 ? col[row + 0] : 0;
+        v.y = row + 1 < E32 ? col[row + 1] : 0;
+        v.z = row + 2 < E32 ? col[row + 2] : 0;
+        v.w = row + 3 < E32 ? col[row + 3] : 0;
+        stage_tile<PAYLOAD, BUF, false, -1>(st, v, t, E32, lo, wm1, lane, s_buf[wave], payload, bm, spill,
+                                            (t - S32) >> 8, rlo, rhi);
     }
     int* buf = s_buf[wave];
-    const uint32_t fill = st.fill, nbm = st.nbm;
+    const uint32_t fill = st.fill, nbm = st.nbm, flushed = st.flushed;
     const uint64_t sw = st.sw;
 
     // ---- block count, then the exclusive prefix over every lower block
@@ -958,12 +984,25 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     for (int w = 0; w < kWaves; w++)
         if (w < wave) D += s_cnt[w];
 
-    // ---- positions mode part: the LDS buffer, in order
+    // ---- positions mode part: the spilled entries, then the LDS ring, in order
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's spill/bitmap stores are done
+    for (uint32_t i0 = 0; i0 < flushed; i0 += 64u * 8u) {  // 8 loads in flight per lane
+        int x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t i = i0 + (uint32_t)j * 64u + (uint32_t)lane;
+            x[j] = i < flushed ? spill[i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t i = i0 + (uint32_t)j * 64u + (uint32_t)lane;
+            if (i < flushed) out[D + i] = x[j];
+        }
+    }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i];
+    for (uint32_t i = flushed + (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i % (uint32_t)BUF];
     if (sw >= E) return;
     // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's bitmap stores are done
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     unsigned long long o = D + fill;
     const uint64_t T1 = (E + 255) >> 8;

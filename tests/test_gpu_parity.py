@@ -337,6 +337,40 @@ def test_full_size_properties_1e9(lib):
     assert v.min() >= lo and v.max() < hi
 
 
+def _check_positions_exact(lib, col, n, lo, hi, pos):
+    """count == the fused count, strictly ascending, every row's value in range:
+    together these say pos is exactly the reference's list (query.c:100-104)."""
+    assert len(pos) == _agg(lib, col.ptr, n, lo, hi).count, (lo, hi)
+    if len(pos) == 0:
+        return
+    assert np.all(np.diff(pos.astype(np.int64)) > 0), (lo, hi)
+    assert pos[0] >= 0 and pos[-1] < n
+    dp, vals = Dev.of(pos), Dev(len(pos) * 4)
+    mq.check(lib.mq_fetch(col.ptr, dp.ptr, len(pos), vals.ptr, None))
+    v = vals.get(np.int32, len(pos))
+    assert v.min() >= lo and v.max() < hi, (lo, hi)
+
+
+@pytest.mark.big
+def test_positions_spill_boundary_1e9(lib, pos_impl):
+    """k_select_stage's three regimes at full size: LDS ring only, ring + spill to
+    the workspace (density below 1/32 with more than 1024 matches per wave), and
+    the switch to bitmap mode (past 1/32), on a uniform column and on a bursty one
+    (4096 equal rows per value, so a wave's matches arrive in dense runs)."""
+    n = 1_000_000_000
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, 42, n, None))
+    for sel in (0.005, 0.02, 0.03, 0.0325, 0.04):
+        lo = n // 3
+        hi = lo + int(sel * n)
+        _check_positions_exact(lib, col, n, lo, hi, _positions(lib, col.ptr, n, lo, hi))
+    bursty = (np.arange(n, dtype=np.int32) // 4096) % 1000
+    col = Dev.of(bursty)
+    del bursty
+    for lo, hi in ((0, 3), (0, 30), (500, 532), (0, 40)):
+        _check_positions_exact(lib, col, n, lo, hi, _positions(lib, col.ptr, n, lo, hi))
+
+
 # ---------------------------------------------------------------------------
 # the drop-in query API (mq_query.c) against the reference's own query.c
 # ---------------------------------------------------------------------------

@@ -69,14 +69,12 @@ int main(int argc, char** argv) {
                 unsigned long long* status = (unsigned long long*)(w + 64);
                 unsigned long long* bm = (unsigned long long*)(w + partial_bytes());
 #define L_(B) hipLaunchKernelGGL((k_select_stage<false, true, B>), dim3(g), dim3(kTPB), 0, q, col, nullptr, n, rw, p, status, bm, out, cnt, err)
-                if (buf == 0) L_(0);
-                else if (buf == 256) L_(256);
+                if (buf == 256) L_(256);
                 else if (buf == 512) L_(512);
                 else L_(1024);
 #undef L_
             };
         };
-        vars.push_back({"stage buf 0 (bitmap only)", stv(0)});
         vars.push_back({"stage buf 256", stv(256)});
         vars.push_back({"stage buf 512", stv(512)});
         vars.push_back({"k_mask + k_compact", [&](hipStream_t q) {
