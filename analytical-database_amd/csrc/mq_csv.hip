@@ -1,0 +1,732 @@
+// mq_csv.hip — the load path on gfx950: CSV text in HBM -> int32 columns.
+//
+// Restates the data loop of load_db (src/db_manager.c:304-318) with insert_row
+// (:164-199), the step that feeds every column the select/fetch/aggregate path reads:
+//   * a row is one fgets(line, MAX_LINE_SIZE = 1024) piece (db_manager.c:23,306):
+//     the bytes through the next '\n', at most 1023 of them, or up to EOF;
+//   * the piece is split by strsep(",") and the first ncols tokens go through atoi
+//     (= (int)strtol(tok, NULL, 10): leading isspace, sign, digits, saturation at
+//     LONG_MIN/LONG_MAX, then the low 32 bits);
+//   * tokens past ncols are ignored; a token missing from a piece keeps the
+//     previous row's value (row[] is reused across lines; before the first line the
+//     reference reads an uninitialised VLA, here 0); a NUL byte ends the string
+//     strsep sees;
+//   * min/max per column fold over the rows as insert_row does (:193-194).
+//
+// Layout: the text is cut into 16 KB chunks, one block each.
+//   k_csv_count : every thread owns 64 bytes; a row starts at p when p == 0 or
+//                 text[p-1] == '\n' (plus, inside lines longer than 1023 bytes,
+//                 every 1023 bytes: "long mode"). Counts per chunk; in the first
+//                 pass also the first/last start per chunk and a long-line flag.
+//   scan        : chunk counts -> first row of each chunk (the shared u32 scan).
+//   k_csv_parse : the chunk plus a 1 KB halo (a piece is <= 1023 bytes) is staged
+//                 in LDS; the starts are enumerated again into an LDS list and each
+//                 thread parses whole pieces from LDS, writing column j of row r to
+//                 cols[j][r] (consecutive lanes -> consecutive rows, coalesced).
+//                 min/max per column: lane registers (first 8 columns) or LDS
+//                 atomics, one partial per block, folded by k_csv_minmax.
+//   missing-token fix-up (only when a piece had fewer than ncols tokens): tokens
+//                 per row, then per column a max-scan of "last row that had the
+//                 token" over 1024-row tiles, and the copy.
+// HBM traffic: 2 reads of the text (count + parse, +6 % halo) + 4 B per cell.
+
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "mq_common.h"
+#include "mq_device.h"
+
+namespace {
+
+using namespace mqi;
+
+constexpr int kTPB = 256;
+constexpr int kWaves = kTPB / 64;
+constexpr int kChunk = 16384;            // text bytes per block
+constexpr int kSeg = kChunk / kTPB;      // 64 bytes per thread
+constexpr int kPre = 16;                 // LDS bytes before the chunk (byte cs-1 at kPre-1)
+constexpr int kHalo = 1024;              // after the chunk: a piece has <= 1023 bytes
+constexpr int kLds = kPre + kChunk + kHalo;
+constexpr int kPiece = 1023;             // fgets(line, 1024)
+constexpr int kRegCols = 8;              // columns whose min/max live in lane registers
+constexpr int kMaxCols = 1024;
+constexpr int kFillTile = 1024;          // rows per tile in the missing-token fix-up
+
+enum { F_LONG = 0, F_MISSING = 1 };
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+struct CsvWs {  // carved from the caller's workspace (mq_csv_workspace_bytes)
+    unsigned* flags;
+    uint32_t* cnt;
+    long long* first;
+    long long* last;
+    long long* prev;
+    unsigned long long* row_base;
+    unsigned long long* scratch;
+    int32_t** colptr;
+    int2* partial;
+};
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+uint64_t nchunks_of(uint64_t n) { return (n + kChunk - 1) / kChunk; }
+
+size_t carve(void* ws, uint64_t n, int ncols, CsvWs* w) {
+    const uint64_t c = nchunks_of(n) + 1;
+    size_t o = 0;
+    char* b = static_cast<char*>(ws);
+    auto take = [&](size_t bytes) {
+        char* p = b ? b + o : nullptr;
+        o += align16(bytes);
+        return p;
+    };
+    CsvWs t;
+    t.flags = reinterpret_cast<unsigned*>(take(64));
+    t.cnt = reinterpret_cast<uint32_t*>(take(c * 4));
+    t.first = reinterpret_cast<long long*>(take(c * 8));
+    t.last = reinterpret_cast<long long*>(take(c * 8));
+    t.prev = reinterpret_cast<long long*>(take(c * 8));
+    t.row_base = reinterpret_cast<unsigned long long*>(take(c * 8));
+    t.scratch = reinterpret_cast<unsigned long long*>(take(scan_u32_scratch_elems(c) * 8));
+    t.colptr = reinterpret_cast<int32_t**>(take((size_t)kMaxCols * 8));
+    t.partial = reinterpret_cast<int2*>(take(c * (size_t)(ncols > 0 ? ncols : 1) * 8));
+    if (w) *w = t;
+    return o;
+}
+
+// ---- staging: text[cs - kPre, cs + kChunk + kHalo) -> s (0 outside [0, n), except
+// that the byte before position 0 reads as '\n': position 0 starts a row).
+template <bool VEC>
+__device__ __forceinline__ void stage_chunk(const char* __restrict__ text, uint64_t n, uint64_t cs,
+                                            uint8_t* s) {
+    const long long base = (long long)cs - kPre;
+    for (int i = threadIdx.x; i < kLds / 16; i += kTPB) {
+        const long long g = base + (long long)i * 16;
+        uint4 v;
+        if (VEC && g >= 0 && (uint64_t)g + 16 <= n) {
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + g));
+            v = make_uint4(t.x, t.y, t.z, t.w);
+        } else {
+            uint8_t t[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const long long q = g + k;
+                t[k] = q == -1 ? (uint8_t)'\n' : (q >= 0 && (uint64_t)q < n) ? (uint8_t)text[q] : 0;
+            }
+            memcpy(&v, t, 16);
+        }
+        *reinterpret_cast<uint4*>(s + i * 16) = v;
+    }
+}
+
+// bit k set <=> byte k of the 4 is '\n' (exact SWAR zero-byte test)
+__device__ __forceinline__ uint32_t nl4(uint32_t w) {
+    const uint32_t x = w ^ 0x0A0A0A0Au;
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
+}
+
+// Real starts of this thread's 64-byte segment [a, a+64): bit k <=> a+k starts a
+// line (byte a+k-1 is '\n'); bytes at or past ce are masked off.
+__device__ __forceinline__ unsigned long long real_starts(const uint8_t* s, uint64_t cs, uint64_t ce,
+                                                          int tid) {
+    const int off = kPre + tid * kSeg;  // LDS index of byte a
+    unsigned long long nl = 0;
+#pragma unroll
+    for (int q = 0; q < kSeg / 16; q++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s + off + q * 16);
+        nl |= (unsigned long long)(nl4(v.x) | (nl4(v.y) << 4) | (nl4(v.z) << 8) | (nl4(v.w) << 12))
+              << (q * 16);
+    }
+    unsigned long long st = (nl << 1) | (s[off - 1] == '\n' ? 1ull : 0ull);
+    const uint64_t a = cs + (uint64_t)tid * kSeg;
+    if (a >= ce) return 0;
+    if (ce - a < 64) st &= (1ull << (ce - a)) - 1;
+    return st;
+}
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_max(T v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T u = __shfl_up(v, o, 64);
+        if (lane >= o) v = v > u ? v : u;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// Exclusive max over the block's threads (in order), seeded with `seed`.
+__device__ __forceinline__ long long block_excl_max(long long x, long long seed, long long* s_w) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long inc = wave_incl_max(x, lane);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    long long carry = seed;
+    for (int w = 0; w < wave; w++) carry = carry > s_w[w] ? carry : s_w[w];
+    long long ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = LLONG_MIN;
+    __syncthreads();
+    return carry > ex ? carry : ex;
+}
+
+// Exclusive sum over the block's threads; *total receives the block sum.
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t x, uint32_t* s_w, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t inc = wave_incl_sum(x, lane);
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t carry = 0, tot = 0;
+    for (int w = 0; w < kWaves; w++) {
+        if (w < wave) carry += s_w[w];
+        tot += s_w[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return carry + inc - x;
+}
+
+// Row starts of the segment, in long mode: the real starts plus, inside a line that
+// is longer than 1023 bytes, every 1023rd byte after its start (fgets pieces).
+// ls_in = last real start before the segment (global). Between two real starts of
+// one 64-byte segment there is no room for 1023 bytes, so only the part before
+// the first real start can hold a piece start.
+__device__ __forceinline__ unsigned long long piece_starts(unsigned long long real, uint64_t a,
+                                                           long long ls_in, uint64_t ce) {
+    if (ls_in < 0 || a >= ce) return real;
+    const uint64_t q = (a - (uint64_t)ls_in) % kPiece;
+    const uint64_t p = q == 0 ? 0 : kPiece - q;  // first piece boundary at or after a
+    const int rf = real ? __builtin_ctzll(real) : 64;
+    if (p < (uint64_t)rf && a + p < ce) real |= 1ull << p;
+    return real;
+}
+
+// ---- pass 1: row starts per chunk ----
+//   LONG = false: real starts; also first/last start (global) per chunk and the
+//                 long-line flag for gaps inside the chunk.
+//   LONG = true : piece starts, given prev[c] = last real start before the chunk.
+template <bool VEC, bool LONG>
+__global__ __launch_bounds__(kTPB) void k_csv_count(const char* __restrict__ text, uint64_t n,
+                                                     uint32_t* __restrict__ cnt, long long* __restrict__ first,
+                                                     long long* __restrict__ last,
+                                                     const long long* __restrict__ prev, unsigned* flags) {
+    __shared__ __attribute__((aligned(16))) uint8_t s[kLds];
+    __shared__ long long s_w[kWaves];
+    __shared__ uint32_t s_u[kWaves];
+    const uint64_t c = blockIdx.x, cs = c * kChunk;
+    const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
+    const int tid = threadIdx.x;
+    stage_chunk<VEC>(text, n, cs, s);
+    __syncthreads();
+    unsigned long long st = real_starts(s, cs, ce, tid);
+    const uint64_t a = cs + (uint64_t)tid * kSeg;
+    const long long mylast = st ? (long long)(a + 63 - __builtin_clzll(st)) : -1;
+    if (LONG) {
+        const long long ls = block_excl_max(mylast, prev[c], s_w);
+        st = piece_starts(st, a, ls, ce);
+    } else {
+        const long long ls = block_excl_max(mylast, -1, s_w);
+        if (st && ls >= 0) {
+            const long long f = (long long)(a + __builtin_ctzll(st));
+            if (f - ls > kPiece) atomicOr(&flags[F_LONG], 1u);
+        }
+    }
+    uint32_t tot;
+    block_excl_sum((uint32_t)__popcll(st), s_u, &tot);
+    if (!LONG) {  // first / last start of the chunk
+        const long long myfirst = st ? (long long)(a + __builtin_ctzll(st)) : LLONG_MAX;
+        long long f = myfirst;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long u = __shfl_xor(f, o, 64);
+            f = f < u ? f : u;
+        }
+        long long l = mylast;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long u = __shfl_xor(l, o, 64);
+            l = l > u ? l : u;
+        }
+        __syncthreads();
+        if ((tid & 63) == 0) s_w[tid >> 6] = f;
+        __syncthreads();
+        if (tid == 0) {
+            long long m = s_w[0];
+            for (int w = 1; w < kWaves; w++) m = m < s_w[w] ? m : s_w[w];
+            first[c] = m == LLONG_MAX ? -1 : m;
+        }
+        __syncthreads();
+        if ((tid & 63) == 0) s_w[tid >> 6] = l;
+        __syncthreads();
+        if (tid == 0) {
+            long long m = s_w[0];
+            for (int w = 1; w < kWaves; w++) m = m > s_w[w] ? m : s_w[w];
+            last[c] = m;
+        }
+    }
+    if (tid == 0) cnt[c] = tot;
+}
+
+// Long lines across chunks: a full chunk without a start lies inside a line of
+// more than 16 KB; otherwise compare each chunk's first start with the previous
+// chunk's last, and the text end with the final start.
+__global__ __launch_bounds__(kTPB) void k_csv_long_check(const uint32_t* __restrict__ cnt,
+                                                          const long long* __restrict__ first,
+                                                          const long long* __restrict__ last,
+                                                          uint64_t nch, uint64_t n, unsigned* flags) {
+    const uint64_t c = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+    if (c >= nch) return;
+    bool lng = false;
+    if (cnt[c] == 0) {
+        lng = c + 1 < nch;  // a full 16 KB chunk inside one line
+    } else {
+        if (c > 0 && cnt[c - 1] > 0 && first[c] - last[c - 1] > kPiece) lng = true;
+        const bool final_start = c + 1 == nch || (c + 2 == nch && cnt[c + 1] == 0);
+        if (final_start && (long long)n - last[c] > kPiece) lng = true;
+    }
+    if (lng) atomicOr(&flags[F_LONG], 1u);
+}
+
+// prev[c] = last real start before chunk c (-1 for none): one block, exclusive max
+// over the chunks (long mode only).
+__global__ __launch_bounds__(1024) void k_csv_prev_start(const long long* __restrict__ last,
+                                                          uint64_t nch, long long* __restrict__ prev) {
+    __shared__ long long s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    long long carry = -1;
+    for (uint64_t b = 0; b < nch; b += 1024) {
+        const uint64_t c = b + tid;
+        const long long x = c < nch ? last[c] : -1;
+        const long long inc = wave_incl_max(x, lane);
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        long long pre = carry, all = carry;
+        for (int w = 0; w < 16; w++) {
+            if (w < wave) pre = pre > s_w[w] ? pre : s_w[w];
+            all = all > s_w[w] ? all : s_w[w];
+        }
+        long long ex = __shfl_up(inc, 1, 64);
+        if (lane == 0) ex = LLONG_MIN;
+        if (c < nch) prev[c] = pre > ex ? pre : ex;
+        carry = all;
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ bool is_space(uint32_t b) {  // isspace() in the C locale
+    return b == ' ' || (b >= '\t' && b <= '\r');
+}
+
+// atoi of the token starting at LDS index k (its piece ends at index kend, the
+// first '\n' included). Returns the value; *k is left on the byte that ended the
+// token; *more is false when the piece ended (a '\n', a NUL, or kend), true when
+// a ',' ended it.
+__device__ __forceinline__ int32_t parse_token(const uint8_t* __restrict__ s, int& k, int kend,
+                                               bool& more) {
+    // leading isspace ('\n' included: it is the piece's last byte)
+    uint32_t b = 0;
+    while (k < kend) {
+        b = s[k];
+        if (!is_space(b) || b == '\n') break;
+        k++;
+    }
+    bool neg = false;
+    if (k < kend && (b == '+' || b == '-')) {
+        neg = b == '-';
+        k++;
+    }
+    unsigned long long acc = 0;
+    int nd = 0;  // significant digits
+    bool sat = false;
+    while (k < kend) {
+        b = s[k];
+        const uint32_t d = b - '0';
+        if (d > 9) break;
+        if (acc != 0 || d != 0) {
+            if (nd >= 19) sat = true;
+            else acc = acc * 10 + d, nd++;
+        }
+        k++;
+    }
+    // rest of the token: up to ',', '\n', NUL or the piece end
+    while (k < kend) {
+        b = s[k];
+        if (b == ',' || b == '\n' || b == 0) break;
+        k++;
+    }
+    more = k < kend && b == ',';
+    if (more) k++;
+    if (!sat && nd == 19 && acc > (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull)) sat = true;
+    if (sat) return neg ? 0 : -1;  // (int)LONG_MIN, (int)LONG_MAX
+    return (int32_t)(uint32_t)(neg ? 0ull - acc : acc);
+}
+
+// ---- pass 2: parse. One block per chunk. The chunk's row starts stay as one
+// 64-bit mask per thread segment plus the exclusive prefix of their counts; lane i
+// takes pieces i, i+256, ... and finds piece i's byte by a binary search over the
+// prefix and a select in the mask (2 KB of LDS instead of a 32 KB start list).
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ text, uint64_t n,
+                                                     const unsigned long long* __restrict__ row_base,
+                                                     const long long* __restrict__ prev, int ncols,
+                                                     int32_t* const* __restrict__ cols,
+                                                     int2* __restrict__ partial, uint16_t* __restrict__ nf,
+                                                     unsigned* flags) {
+    __shared__ __attribute__((aligned(16))) uint8_t s[kLds];
+    __shared__ unsigned long long s_mask[kTPB];
+    __shared__ uint32_t s_off[kTPB];
+    __shared__ long long s_w[kWaves];
+    __shared__ uint32_t s_u[kWaves];
+    extern __shared__ int s_mm[];  // 2 * ncols: min, max
+    const uint64_t c = blockIdx.x, cs = c * kChunk;
+    const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool lmode = __builtin_amdgcn_readfirstlane(flags[F_LONG]) != 0;
+    stage_chunk<VEC>(text, n, cs, s);
+    for (int j = tid; j < ncols; j += kTPB) {
+        s_mm[2 * j] = INT_MAX;
+        s_mm[2 * j + 1] = INT_MIN;
+    }
+    __syncthreads();
+    unsigned long long st = real_starts(s, cs, ce, tid);
+    const uint64_t a = cs + (uint64_t)tid * kSeg;
+    if (lmode) {
+        const long long mylast = st ? (long long)(a + 63 - __builtin_clzll(st)) : -1;
+        st = piece_starts(st, a, block_excl_max(mylast, prev[c], s_w), ce);
+    }
+    uint32_t nst;
+    s_off[tid] = block_excl_sum((uint32_t)__popcll(st), s_u, &nst);
+    s_mask[tid] = st;
+    __syncthreads();
+
+    const uint64_t r0 = row_base[c];
+    int mn[kRegCols], mx[kRegCols];
+#pragma unroll
+    for (int j = 0; j < kRegCols; j++) mn[j] = INT_MAX, mx[j] = INT_MIN;
+    bool missing = false;
+    for (uint32_t i = tid; i < nst; i += kTPB) {
+        int t = 0;  // last segment whose prefix is <= i
+#pragma unroll
+        for (int step = kTPB / 2; step > 0; step >>= 1)
+            if (s_off[t + step] <= i) t += step;
+        unsigned long long m = s_mask[t];
+        for (uint32_t r = s_off[t]; r < i; r++) m &= m - 1;
+        const int off = t * kSeg + __builtin_ctzll(m);  // piece start within the chunk
+        const uint64_t p = cs + (uint64_t)off;
+        const uint64_t pe = p + kPiece < n ? p + kPiece : n;  // fgets cap / EOF
+        int k = kPre + off;
+        const int kend = k + (int)(pe - p);
+        const uint64_t row = r0 + i;
+        bool more = true;
+        int got = 0;
+#pragma unroll
+        for (int j = 0; j < kRegCols; j++) {
+            if (j < ncols && more) {
+                const int32_t v = parse_token(s, k, kend, more);
+                cols[j][row] = v;
+                mn[j] = min(mn[j], v);
+                mx[j] = max(mx[j], v);
+                got = j + 1;
+            }
+        }
+        for (int j = kRegCols; j < ncols && more; j++) {
+            const int32_t v = parse_token(s, k, kend, more);
+            cols[j][row] = v;
+            atomicMin(&s_mm[2 * j], v);
+            atomicMax(&s_mm[2 * j + 1], v);
+            got = j + 1;
+        }
+        if (got < ncols) missing = true;
+        if (nf) nf[row] = (uint16_t)got;
+    }
+    if (__ballot(missing) && lane == 0) atomicOr(&flags[F_MISSING], 1u);
+#pragma unroll
+    for (int j = 0; j < kRegCols; j++) {
+        if (j < ncols) {
+            const int a0 = wave_min_i(mn[j]), a1 = wave_max_i(mx[j]);
+            if (lane == 0) {
+                atomicMin(&s_mm[2 * j], a0);
+                atomicMax(&s_mm[2 * j + 1], a1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < ncols; j += kTPB)
+        partial[c * (uint64_t)ncols + j] = make_int2(s_mm[2 * j], s_mm[2 * j + 1]);
+}
+
+// min/max per column over the chunk partials (one block per column); zfill[j]
+// set = the fix-up wrote 0s into column j (rows before its first token), which
+// count as values like every other row.
+__global__ __launch_bounds__(kTPB) void k_csv_minmax(const int2* __restrict__ partial, uint64_t nch,
+                                                      int ncols, const unsigned* __restrict__ zfill,
+                                                      int32_t* __restrict__ out) {
+    __shared__ int s_a[kWaves], s_b[kWaves];
+    const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    int mn = INT_MAX, mx = INT_MIN;
+    for (uint64_t c = tid; c < nch; c += kTPB) {
+        const int2 v = partial[c * (uint64_t)ncols + j];
+        mn = min(mn, v.x);
+        mx = max(mx, v.y);
+    }
+    if (zfill && zfill[j]) mn = min(mn, 0), mx = max(mx, 0);
+    mn = wave_min_i(mn);
+    mx = wave_max_i(mx);
+    if (lane == 0) s_a[tid >> 6] = mn, s_b[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kWaves; w++) mn = min(mn, s_a[w]), mx = max(mx, s_b[w]);
+        out[2 * j] = mn;
+        out[2 * j + 1] = mx;
+    }
+}
+
+// ---- missing-token fix-up: a row whose piece had got = nf[r] tokens keeps, for
+// every column j >= got, the value of the last earlier row that had token j
+// (0 when there is none). Tiles of kFillTile rows, 4 per thread.
+__global__ __launch_bounds__(kTPB) void k_fill_tile_last(const uint16_t* __restrict__ nf, uint64_t rows,
+                                                          int ncols, long long* __restrict__ tile_last) {
+    __shared__ long long s_w[kWaves];
+    const uint64_t t = blockIdx.x, r0 = t * kFillTile + (uint64_t)threadIdx.x * 4;
+    const int lane = threadIdx.x & 63;
+    uint16_t g[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) g[e] = r0 + e < rows ? nf[r0 + e] : 0;
+    for (int j = 0; j < ncols; j++) {
+        long long l = -1;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if (r0 + e < rows && g[e] > j) l = (long long)(r0 + e);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long u = __shfl_xor(l, o, 64);
+            l = l > u ? l : u;
+        }
+        if (lane == 0) s_w[threadIdx.x >> 6] = l;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long m = s_w[0];
+            for (int w = 1; w < kWaves; w++) m = m > s_w[w] ? m : s_w[w];
+            tile_last[t * (uint64_t)ncols + j] = m;
+        }
+        __syncthreads();
+    }
+}
+
+// carry[t][j] = last row with token j in tiles < t (exclusive max; one block per column)
+__global__ __launch_bounds__(1024) void k_fill_carry(const long long* __restrict__ tile_last,
+                                                      uint64_t ntiles, int ncols,
+                                                      long long* __restrict__ carry) {
+    __shared__ long long s_w[16];
+    const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    long long run = -1;
+    for (uint64_t b = 0; b < ntiles; b += 1024) {
+        const uint64_t t = b + tid;
+        const long long x = t < ntiles ? tile_last[t * (uint64_t)ncols + j] : -1;
+        const long long inc = wave_incl_max(x, lane);
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        long long pre = run, all = run;
+        for (int w = 0; w < 16; w++) {
+            if (w < wave) pre = pre > s_w[w] ? pre : s_w[w];
+            all = all > s_w[w] ? all : s_w[w];
+        }
+        long long ex = __shfl_up(inc, 1, 64);
+        if (lane == 0) ex = LLONG_MIN;
+        if (t < ntiles) carry[t * (uint64_t)ncols + j] = pre > ex ? pre : ex;
+        run = all;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_fill_apply(const uint16_t* __restrict__ nf, uint64_t rows,
+                                                      int ncols, int32_t* const* __restrict__ cols,
+                                                      const long long* __restrict__ carry,
+                                                      unsigned* __restrict__ zfill) {
+    __shared__ long long s_w[kWaves];
+    const uint64_t t = blockIdx.x, r0 = t * kFillTile + (uint64_t)threadIdx.x * 4;
+    uint16_t g[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) g[e] = r0 + e < rows ? nf[r0 + e] : 0xFFFF;
+    for (int j = 0; j < ncols; j++) {
+        long long l = -1;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if (r0 + e < rows && g[e] > j) l = (long long)(r0 + e);
+        long long src = block_excl_max(l, carry[t * (uint64_t)ncols + j], s_w);
+        int32_t* col = cols[j];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            if (r0 + e >= rows) break;
+            if (g[e] > j) {
+                src = (long long)(r0 + e);
+            } else {
+                col[r0 + e] = src >= 0 ? col[src] : 0;
+                if (src < 0) atomicOr(&zfill[j], 1u);
+            }
+        }
+    }
+}
+
+int launch_count(const char* text, uint64_t n, const CsvWs& w, bool lng, hipStream_t st) {
+    const uint64_t nch = nchunks_of(n);
+    const bool vec = aligned16(text);
+    const dim3 g((unsigned)nch);
+    if (lng) {
+        if (vec) hipLaunchKernelGGL((k_csv_count<true, true>), g, dim3(kTPB), 0, st, text, n, w.cnt, w.first, w.last, w.prev, w.flags);
+        else hipLaunchKernelGGL((k_csv_count<false, true>), g, dim3(kTPB), 0, st, text, n, w.cnt, w.first, w.last, w.prev, w.flags);
+    } else {
+        if (vec) hipLaunchKernelGGL((k_csv_count<true, false>), g, dim3(kTPB), 0, st, text, n, w.cnt, w.first, w.last, w.prev, w.flags);
+        else hipLaunchKernelGGL((k_csv_count<false, false>), g, dim3(kTPB), 0, st, text, n, w.cnt, w.first, w.last, w.prev, w.flags);
+    }
+    LAUNCHCHK("k_csv_count");
+    return MQ_OK;
+}
+
+int launch_parse(const char* text, uint64_t n, int ncols, const CsvWs& w, uint16_t* nf, hipStream_t st) {
+    const uint64_t nch = nchunks_of(n);
+    const size_t dyn = (size_t)ncols * 8;
+    if (aligned16(text))
+        hipLaunchKernelGGL((k_csv_parse<true>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags);
+    else
+        hipLaunchKernelGGL((k_csv_parse<false>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags);
+    LAUNCHCHK("k_csv_parse");
+    return MQ_OK;
+}
+
+int check_args(const char* text, uint64_t n, void* ws, size_t ws_bytes, int ncols) {
+    if (n && !text) return set_err(MQ_EINVAL, "mq_csv: NULL text");
+    if (!ws) return set_err(MQ_EINVAL, "mq_csv: NULL workspace");
+    if (ncols < 0 || ncols > kMaxCols) return set_err(MQ_EINVAL, "mq_csv: ncols %d outside [0, %d]", ncols, kMaxCols);
+    if (nchunks_of(n) >= (1ull << 31)) return set_err(MQ_EINVAL, "mq_csv: text too large");
+    if (ws_bytes < carve(nullptr, n, ncols, nullptr)) return set_err(MQ_EINVAL, "mq_csv: workspace too small");
+    return MQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mq_csv_workspace_bytes(uint64_t n, int ncols) {
+    return carve(nullptr, n, ncols < 0 ? 0 : (ncols > kMaxCols ? kMaxCols : ncols), nullptr);
+}
+
+int mq_csv_count_rows(const char* d_text, uint64_t n, int ncols, uint64_t* h_rows, void* d_ws,
+                      size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!h_rows) return set_err(MQ_EINVAL, "mq_csv_count_rows: NULL h_rows");
+    *h_rows = 0;
+    if ((rc = check_args(d_text, n, d_ws, ws_bytes, ncols))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    CsvWs w;
+    carve(d_ws, n, ncols, &w);
+    HIPCHK(hipMemsetAsync(w.flags, 0, 64, st));
+    if (n == 0) return MQ_OK;
+    const uint64_t nch = nchunks_of(n);
+    if ((rc = launch_count(d_text, n, w, false, st))) return rc;
+    hipLaunchKernelGGL(k_csv_long_check, dim3((unsigned)((nch + kTPB - 1) / kTPB)), dim3(kTPB), 0, st,
+                       w.cnt, w.first, w.last, nch, n, w.flags);
+    LAUNCHCHK("k_csv_long_check");
+    unsigned flags[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(flags, w.flags, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flags[F_LONG]) {  // lines over 1023 bytes: rows are fgets pieces
+        hipLaunchKernelGGL(k_csv_prev_start, dim3(1), dim3(1024), 0, st, w.last, nch, w.prev);
+        LAUNCHCHK("k_csv_prev_start");
+        if ((rc = launch_count(d_text, n, w, true, st))) return rc;
+    }
+    if ((rc = scan_u32_exclusive(w.cnt, w.row_base, nch, w.scratch, st))) return rc;
+    unsigned long long base = 0;
+    uint32_t last = 0;
+    HIPCHK(hipMemcpyAsync(&base, w.row_base + (nch - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last, w.cnt + (nch - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *h_rows = base + last;
+    return MQ_OK;
+}
+
+int mq_csv_parse_int32(const char* d_text, uint64_t n, int ncols, int32_t* const* d_cols,
+                       uint64_t rows, int32_t* d_minmax, void* d_ws, size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if ((rc = check_args(d_text, n, d_ws, ws_bytes, ncols))) return rc;
+    if (ncols && (!d_cols || !d_minmax)) return set_err(MQ_EINVAL, "mq_csv_parse_int32: NULL columns");
+    for (int j = 0; j < ncols; j++)
+        if (rows && !d_cols[j]) return set_err(MQ_EINVAL, "mq_csv_parse_int32: NULL column %d", j);
+    hipStream_t st = (hipStream_t)stream;
+    CsvWs w;
+    carve(d_ws, n, ncols, &w);
+    if (ncols == 0) return MQ_OK;
+    if (rows == 0 || n == 0) {
+        std::vector<int32_t> mm(2 * (size_t)ncols);
+        for (int j = 0; j < ncols; j++) mm[2 * j] = INT_MAX, mm[2 * j + 1] = INT_MIN;
+        HIPCHK(hipMemcpyAsync(d_minmax, mm.data(), mm.size() * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return MQ_OK;
+    }
+    const uint64_t nch = nchunks_of(n);
+    HIPCHK(hipMemcpyAsync(w.colptr, d_cols, (size_t)ncols * 8, hipMemcpyHostToDevice, st));
+    if ((rc = launch_parse(d_text, n, ncols, w, nullptr, st))) return rc;
+    unsigned flags[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(flags, w.flags, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    unsigned* zfill = nullptr;
+    void* scratch = nullptr;
+    if (flags[F_MISSING]) {  // rows with fewer than ncols tokens: the stale-value copy
+        const uint64_t ntiles = (rows + kFillTile - 1) / kFillTile;
+        const size_t b_nf = align16(rows * 2), b_t = align16(ntiles * (size_t)ncols * 8);
+        scratch = pool_alloc(b_nf + 2 * b_t + align16((size_t)ncols * 4));
+        if (!scratch) return set_err(MQ_ENOMEM, "mq_csv_parse_int32: fix-up scratch");
+        char* p = static_cast<char*>(scratch);
+        uint16_t* nf = reinterpret_cast<uint16_t*>(p);
+        long long* tl = reinterpret_cast<long long*>(p + b_nf);
+        long long* carry = reinterpret_cast<long long*>(p + b_nf + b_t);
+        zfill = reinterpret_cast<unsigned*>(p + b_nf + 2 * b_t);
+        HIPCHK(hipMemsetAsync(zfill, 0, (size_t)ncols * 4, st));
+        if ((rc = launch_parse(d_text, n, ncols, w, nf, st))) return rc;
+        hipLaunchKernelGGL(k_fill_tile_last, dim3((unsigned)ntiles), dim3(kTPB), 0, st, nf, rows, ncols, tl);
+        LAUNCHCHK("k_fill_tile_last");
+        hipLaunchKernelGGL(k_fill_carry, dim3((unsigned)ncols), dim3(1024), 0, st, tl, ntiles, ncols, carry);
+        LAUNCHCHK("k_fill_carry");
+        hipLaunchKernelGGL(k_fill_apply, dim3((unsigned)ntiles), dim3(kTPB), 0, st, nf, rows, ncols,
+                           w.colptr, carry, zfill);
+        LAUNCHCHK("k_fill_apply");
+    }
+    hipLaunchKernelGGL(k_csv_minmax, dim3((unsigned)ncols), dim3(kTPB), 0, st, w.partial, nch, ncols,
+                       zfill, d_minmax);
+    LAUNCHCHK("k_csv_minmax");
+    if (scratch) {
+        HIPCHK(hipStreamSynchronize(st));
+        pool_free(scratch);
+    }
+    return MQ_OK;
+}
+
+}  // extern "C"

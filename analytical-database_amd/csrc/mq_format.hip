@@ -69,9 +69,88 @@ __global__ __launch_bounds__(kTPB) void k_fmt_write(const int32_t* __restrict__ 
     }
 }
 
+// ---- a table as CSV rows: "%d" per cell, ',' between columns, '\n' after each row
+__device__ __forceinline__ uint32_t cell_len(int32_t x) { return ndigits(magnitude(x)) + (x < 0 ? 1u : 0u); }
+
+__device__ __forceinline__ char* put_int(char* p, int32_t x) {
+    uint32_t m = magnitude(x);
+    const uint32_t nd = ndigits(m);
+    if (x < 0) *p++ = '-';
+    for (uint32_t k = nd; k-- > 0;) {
+        p[k] = (char)('0' + m % 10u);
+        m /= 10u;
+    }
+    return p + nd;
+}
+
+__global__ __launch_bounds__(kTPB) void k_csv_row_len(const int32_t* const* __restrict__ cols, int ncols,
+                                                      uint64_t rows, uint32_t* __restrict__ len) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x; r < rows; r += stride) {
+        uint32_t l = 0;
+        for (int j = 0; j < ncols; j++) l += cell_len(cols[j][r]) + 1u;
+        len[r] = l;
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_csv_row_write(const int32_t* const* __restrict__ cols, int ncols,
+                                                        uint64_t rows, const unsigned long long* __restrict__ offs,
+                                                        char* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x; r < rows; r += stride) {
+        char* p = out + offs[r];
+        for (int j = 0; j < ncols; j++) {
+            p = put_int(p, cols[j][r]);
+            *p++ = j + 1 < ncols ? ',' : '\n';
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t mq_format_csv_workspace_bytes(uint64_t rows, int ncols) {
+    (void)ncols;
+    return 8192 + (size_t)rows * 4 + 16 + (size_t)rows * 8 + 16 + (size_t)scan_u32_scratch_elems(rows) * 8 + 16;
+}
+
+int mq_format_csv_int32(const int32_t* const* d_cols, int ncols, uint64_t rows, char* d_out,
+                        uint64_t* h_len, void* d_ws, size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!h_len || ncols < 1 || ncols > 1024 || (rows && (!d_cols || !d_out || !d_ws)))
+        return set_err(MQ_EINVAL, "mq_format_csv_int32: bad argument");
+    *h_len = 0;
+    if (rows == 0) return MQ_OK;
+    if (ws_bytes < mq_format_csv_workspace_bytes(rows, ncols))
+        return set_err(MQ_EINVAL, "mq_format_csv_int32: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* w = static_cast<char*>(d_ws);
+    const int32_t** dcols = reinterpret_cast<const int32_t**>(w);
+    w += 8192;
+    uint32_t* len = reinterpret_cast<uint32_t*>(w);
+    w += ((size_t)rows * 4 + 15) & ~(size_t)15;
+    unsigned long long* offs = reinterpret_cast<unsigned long long*>(w);
+    w += (size_t)rows * 8 + 16;
+    unsigned long long* scratch = reinterpret_cast<unsigned long long*>(w);
+    HIPCHK(hipMemcpyAsync(dcols, d_cols, (size_t)ncols * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_csv_row_len, dim3(stream_grid(s, rows)), dim3(kTPB), 0, st, dcols, ncols, rows, len);
+    LAUNCHCHK("k_csv_row_len");
+    if ((rc = scan_u32_exclusive(len, offs, rows, scratch, st))) return rc;
+    hipLaunchKernelGGL(k_csv_row_write, dim3(stream_grid(s, rows)), dim3(kTPB), 0, st, dcols, ncols, rows,
+                       offs, d_out);
+    LAUNCHCHK("k_csv_row_write");
+    unsigned long long last_off = 0;
+    uint32_t last_len = 0;
+    HIPCHK(hipMemcpyAsync(&last_off, offs + (rows - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last_len, len + (rows - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *h_len = last_off + last_len;
+    return MQ_OK;
+}
+
 
 size_t mq_format_workspace_bytes(uint64_t n) {
     return (size_t)n * 4 + 16 + (size_t)n * 8 + 16 + (size_t)scan_u32_scratch_elems(n) * 8 + 16;

@@ -112,6 +112,11 @@ _SIGS = {
     "mq_format_workspace_bytes": (_sz, [_u64]),
     "mq_format_int32": (_int, [_vp, _u64, _vp, C.POINTER(C.c_uint64), _vp, _sz, _vp]),
     "mq_trim": (None, []),
+    "mq_format_csv_workspace_bytes": (_sz, [_u64, _int]),
+    "mq_format_csv_int32": (_int, [_vp, _int, _u64, _vp, C.POINTER(C.c_uint64), _vp, _sz, _vp]),
+    "mq_csv_workspace_bytes": (_sz, [_u64, _int]),
+    "mq_csv_count_rows": (_int, [_vp, _u64, _int, C.POINTER(_u64), _vp, _sz, _vp]),
+    "mq_csv_parse_int32": (_int, [_vp, _u64, _int, _vp, _u64, _vp, _vp, _sz, _vp]),
     "mq_stream_read": (_int, [_vp, _u64, _vp, _sz, C.POINTER(C.c_uint64), _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,

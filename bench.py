@@ -388,8 +388,9 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
             "ms": t_pos, "rows_per_s": n / (t_pos * 1e-3), "k": k,
             "algorithmic_bytes": 4 * n + 4 * k,
             "gbs_algorithmic": (4 * n + 4 * k) / (t_pos * 1e-3) / 1e9,
-            "hbm_bytes_design": 4 * n + n // 4 + 4 * k,
-            "note": "k_scan<mask> (4N read + N/8 bit write) + k_compact (N/8 read + 4K write)"}
+            "hbm_bytes_design": 4 * n + 12 * k,
+            "note": "k_select_stage, one launch: 4N read; positions in an LDS ring per wave, "
+                    "spilled to the workspace (4K write + 4K read) at 1 %, then 4K output write"}
         out["config3_chain"] = {
             "ms": t_chain, "rows_per_s": n / (t_chain * 1e-3), "parity": chain_ok,
             "avg": (int(a[1]) / int(a[0])) if int(a[0]) else None,

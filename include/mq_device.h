@@ -135,6 +135,32 @@ size_t mq_format_workspace_bytes(uint64_t n);
 int mq_format_int32(const int32_t* d_vals, uint64_t n, char* d_out, uint64_t* h_len, void* d_ws,
                     size_t ws_bytes, void* stream);
 
+/* A table as CSV text, the way the reference's generators write the load files
+ * (value of column 0, ',' ... column ncols-1, '\n' per row; "%d" each). d_cols: host
+ * array of ncols device pointers; d_out capacity >= rows * ncols * 12 bytes; *h_len
+ * receives the byte count. Synchronises the stream. (Bench/test data for the load
+ * path; the reference loads such files with load_db.) */
+size_t mq_format_csv_workspace_bytes(uint64_t rows, int ncols);
+int mq_format_csv_int32(const int32_t* const* d_cols, int ncols, uint64_t rows, char* d_out,
+                        uint64_t* h_len, void* d_ws, size_t ws_bytes, void* stream);
+
+/* ---- load path: load_db's data loop (db_manager.c:304-318) + insert_row (:164-199) ----
+ * d_text: n bytes of CSV data lines in HBM (the header line already consumed; the
+ * header is what fgets returns first, <= 1023 bytes through '\n'). Rows are the
+ * reference's fgets(line, 1024) pieces: through the next '\n', at most 1023 bytes.
+ * Each row's first ncols ','-separated tokens go through atoi; a token missing from
+ * a row keeps the previous row's value (0 before the first row); extra tokens are
+ * ignored. Two steps on one workspace (mq_csv_workspace_bytes(n, ncols)):
+ * count: *h_rows = rows (synchronous);
+ * parse: d_cols[j] (host array of ncols device pointers, capacity >= rows) receive
+ *        column j; d_minmax (device, 2*ncols int32) min/max per column (INT32_MAX /
+ *        INT32_MIN when rows == 0), as insert_row folds them. ncols <= 1024. */
+size_t mq_csv_workspace_bytes(uint64_t n, int ncols);
+int mq_csv_count_rows(const char* d_text, uint64_t n, int ncols, uint64_t* h_rows, void* d_ws,
+                      size_t ws_bytes, void* stream);
+int mq_csv_parse_int32(const char* d_text, uint64_t n, int ncols, int32_t* const* d_cols,
+                       uint64_t rows, int32_t* d_minmax, void* d_ws, size_t ws_bytes, void* stream);
+
 /* ---- S10 add / sub (int32, two's-complement wrap) ---- */
 int mq_add(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);
 int mq_sub(const int32_t* d_a, const int32_t* d_b, uint64_t n, int32_t* d_out, void* stream);

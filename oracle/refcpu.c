@@ -497,3 +497,65 @@ size_t rc_nested_loop_join(const int32_t* c1, const int32_t* p1, size_t n1,
             }
     return m;
 }
+
+/* ------------------------------------------------------------------ */
+/* load path: src/db_manager.c:240-322 load_db + :164-199 insert_row    */
+/* ------------------------------------------------------------------ */
+
+/* fgets(line, MAX_LINE_SIZE = 1024, stream) over a memory buffer
+ * (db_manager.c:23,263,306): up to 1023 bytes, through the first '\n'. */
+static size_t csv_fgets(const char* text, size_t n, size_t at, char line[1024]) {
+    size_t k = 0;
+    while (at + k < n && k < 1023) {
+        line[k] = text[at + k];
+        k++;
+        if (line[k - 1] == '\n') break;
+    }
+    line[k] = '\0';
+    return k;
+}
+
+size_t rc_csv_header_len(const char* text, size_t n) {
+    char line[1024];
+    return csv_fgets(text, n, 0, line);
+}
+
+/* The data lines of load_db (db_manager.c:304-318): every fgets piece is one row;
+ * strsep(",") tokens, atoi, the first ncols tokens fill row[], a token missing from
+ * a line keeps the previous line's value (row[] is reused; the reference leaves it
+ * uninitialised before the first line, this restatement starts it at 0). Each row
+ * is appended to the columns and folds into min/max as insert_row does
+ * (db_manager.c:189-195). cols == NULL counts rows only. */
+size_t rc_load_csv(const char* text, size_t n, int ncols, int32_t** cols, size_t cap,
+                   int32_t* minmax) {
+    char line[1024];
+    int* row = calloc((size_t)(ncols > 0 ? ncols : 1), sizeof(int));
+    for (int j = 0; j < ncols && minmax; j++) {
+        minmax[2 * j] = INT32_MAX;
+        minmax[2 * j + 1] = INT32_MIN;
+    }
+    size_t rows = 0, at = 0;
+    while (at < n) {
+        at += csv_fgets(text, n, at, line);
+        char* temp = line;
+        char* token;
+        int index = 0;
+        while ((token = strsep(&temp, ",")) != NULL && index < ncols) row[index++] = atoi(token);
+        if (cols) {
+            if (rows >= cap) {
+                free(row);
+                return (size_t)-1;
+            }
+            for (int j = 0; j < ncols; j++) {
+                cols[j][rows] = row[j];
+                if (minmax) {
+                    if (row[j] < minmax[2 * j]) minmax[2 * j] = row[j];
+                    if (row[j] > minmax[2 * j + 1]) minmax[2 * j + 1] = row[j];
+                }
+            }
+        }
+        rows++;
+    }
+    free(row);
+    return rows;
+}

@@ -73,6 +73,15 @@ size_t rc_nested_loop_join(const int32_t* c1, const int32_t* p1, size_t n1,
                            int32_t* out1, int32_t* out2, size_t cap);
 int32_t rc_multimap_size(int32_t tuple_num);
 
+/* ---- load path (db_manager.c:240-322 load_db, :164-199 insert_row) ----
+ * rc_csv_header_len: bytes the header fgets consumes (<= 1023, through '\n').
+ * rc_load_csv: rows of the data text (header excluded); cols[j] (capacity cap)
+ * receive column j and minmax[2j], [2j+1] its min / max (INT32_MAX / INT32_MIN
+ * when there are no rows). cols == NULL counts only; (size_t)-1 when rows > cap. */
+size_t rc_csv_header_len(const char* text, size_t n);
+size_t rc_load_csv(const char* text, size_t n, int ncols, int32_t** cols, size_t cap,
+                   int32_t* minmax);
+
 #ifdef __cplusplus
 }
 #endif

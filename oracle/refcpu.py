@@ -60,6 +60,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rc_hash_join": (_sz, [_vp, _vp, _sz, _vp, _vp, _sz, _vp, _vp, _sz]),
         "rc_nested_loop_join": (_sz, [_vp, _vp, _sz, _vp, _vp, _sz, _vp, _vp, _sz]),
         "rc_multimap_size": (_i32, [_i32]),
+        "rc_csv_header_len": (_sz, [_vp, _sz]),
+        "rc_load_csv": (_sz, [_vp, _sz, C.c_int, _vp, _sz, _vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -212,3 +214,27 @@ def hash_join(c1, p1, c2, p2, nested: bool = False):
     m2 = fn(_a(c1), _a(p1), len(c1), _a(c2), _a(p2), len(c2), _a(o1), _a(o2), m)
     assert m2 == m
     return o1[:m].copy(), o2[:m].copy()
+
+
+def csv_header_len(text: bytes) -> int:
+    buf = C.create_string_buffer(text, len(text))
+    return int(lib().rc_csv_header_len(buf, len(text)))
+
+
+def load_csv(text: bytes, ncols: int):
+    """load_db's data-line loop (db_manager.c:304-318) over `text` (header already
+    removed): returns (columns int32[ncols][rows], minmax int32[ncols][2])."""
+    buf = C.create_string_buffer(text, len(text))
+    L = lib()
+    rows = int(L.rc_load_csv(buf, len(text), ncols, None, 0, None))
+    cols = np.empty((ncols, max(rows, 1)), dtype=np.int32)
+    ptrs = (C.c_void_p * max(ncols, 1))(*[cols[j].ctypes.data for j in range(ncols)])
+    mm = np.empty((max(ncols, 1), 2), dtype=np.int32)
+    got = int(L.rc_load_csv(buf, len(text), ncols, ptrs, rows, _a(mm)))
+    assert got == rows
+    return cols[:, :rows].copy(), mm[:ncols].copy()
+
+
+def fnv1a64_bytes(b: bytes) -> int:
+    buf = C.create_string_buffer(b, len(b))
+    return int(lib().rc_fnv1a64(buf, len(b)))
