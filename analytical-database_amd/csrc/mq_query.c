@@ -20,14 +20,18 @@
  *     is re-uploaded on mismatch. Shadows are evicted LRU beyond a byte budget
  *     (MQ_SHADOW_MB, default 65536 MB).
  */
-#define _POSIX_C_SOURCE 200809L
+#define _DEFAULT_SOURCE
 #include "mq_query.h"
 
+#include <fcntl.h>
 #include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "mq_device.h"
 
@@ -62,6 +66,11 @@ _Static_assert(offsetof(SelectOperator, db) == 88, "SelectOperator.db");
 _Static_assert(offsetof(SelectOperator, column) == 104, "SelectOperator.column");
 _Static_assert(offsetof(SelectOperator, comparator) == 128, "SelectOperator.comparator");
 _Static_assert(sizeof(ColumnIndex) == 16, "ColumnIndex size");
+_Static_assert(sizeof(Table) == 96, "Table size");
+_Static_assert(offsetof(Table, columns) == 64 && offsetof(Table, col_count) == 72, "Table.columns");
+_Static_assert(offsetof(Table, row_count) == 80 && offsetof(Table, table_length) == 88, "Table rows");
+_Static_assert(sizeof(Db) == 88, "Db size");
+_Static_assert(offsetof(Db, tables) == 64 && offsetof(Db, tables_size) == 72, "Db.tables");
 _Static_assert(INT == 0 && LONG == 1 && FLOAT == 2 && DOUBLE == 3, "DataType values");
 _Static_assert(OK == 0 && ERROR == 1, "StatusCode values");
 
@@ -760,6 +769,182 @@ char* print(Result** results, int result_num, Status* ret_status) {
     }
     ret_status->code = OK;
     return s;
+}
+
+/* ------------------------------------------------------------------ */
+/* load path: db_manager.c:240-322 load_db + :164-199 insert_row      */
+/* ------------------------------------------------------------------ */
+
+/* The server's own capacity helpers (db_manager.c:430 save_data, :736 start_data),
+ * resolved from the executable that links libmq; NULL when none does. */
+extern void save_data(Table* table, Column* column, Status* ret_status) __attribute__((weak));
+extern void start_data(Db* db, Table* table, Column* column, Status* ret_status)
+    __attribute__((weak));
+
+static void col_put(Column* c, void* dev) {
+    ColEntry* e = col_find(c);
+    if (e) col_drop(e);
+    if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
+    g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1};
+}
+
+static void load_fail(Status* st, const char* msg) {
+    fprintf(stderr, "libmq: load_db: %s\n", msg);
+    st->code = ERROR;
+    st->error_message = (char*)msg;
+}
+
+/* insert_row's growth (db_manager.c:168-187): the capacity doubles whenever a row
+ * arrives at a full table, so after the load it is the first table_length * 2^k
+ * that holds every row; reached here in one remap instead of k. */
+static int grow_table(Db* db, Table* t, size_t total, Status* st) {
+    size_t len = t->table_length;
+    if (len == 0) return -1;
+    while (len < total) len *= 2;
+    if (len == t->table_length) return 0;
+    if (!save_data || !start_data) {
+        load_fail(st, "the table must grow and the server's save_data/start_data are not linked");
+        return -1;
+    }
+    for (size_t i = 0; i < t->col_count; i++) {
+        Status s = {OK, NULL};
+        save_data(t, t->columns + i, &s);
+        if (s.code != OK) return -1;
+    }
+    t->table_length = len;
+    for (size_t i = 0; i < t->col_count; i++) {
+        Status s = {OK, NULL};
+        start_data(db, t, t->columns + i, &s);
+        if (s.code != OK) return -1;
+    }
+    return 0;
+}
+
+void load_db(Db* db, const char* path, Status* ret_status) {
+    ret_status->code = OK;
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) {
+        ret_status->code = ERROR;
+        ret_status->error_message = "Failed to open file to load db";
+        return;
+    }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0 || sb.st_size == 0) {
+        close(fd);
+        load_fail(ret_status, "empty or unreadable file");
+        return;
+    }
+    const size_t n = (size_t)sb.st_size;
+    const char* text = mmap(NULL, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (text == MAP_FAILED) {
+        load_fail(ret_status, "mmap failed");
+        return;
+    }
+    /* header: fgets(line, MAX_LINE_SIZE) then strsep(".") twice (:263-268) */
+    char line[1024];
+    size_t h = 0;
+    while (h < n && h < 1023) {
+        line[h] = text[h];
+        if (line[h++] == '\n') break;
+    }
+    line[h] = '\0';
+    char* temp = line;
+    const char* db_name = strsep(&temp, ".");
+    const char* table_name = strsep(&temp, ".");
+    Table* table = NULL;
+    if (db && db_name && table_name && strcmp(db->name, db_name) == 0)
+        for (size_t i = 0; i < db->tables_size; i++)
+            if (!strcmp(db->tables[i].name, table_name)) {
+                table = db->tables + i;
+                break;
+            }
+    if (!table) { /* :273-295 */
+        munmap((void*)text, n);
+        ret_status->code = ERROR;
+        return;
+    }
+    const int ncols = (int)table->col_count;
+    const char* data = text + h;
+    const size_t dn = n - h;
+    void *d_text = NULL, *d_ws = NULL, *d_mm = NULL;
+    void* dcol[1024] = {NULL};
+    int32_t* dparse[1024];
+    int32_t mm[2048];
+    int rc = 0;
+    if (table->col_count > 1024) {
+        load_fail(ret_status, "more than 1024 columns");
+        goto out;
+    }
+    if (ready(ret_status)) goto out;
+    const size_t wsb = mq_csv_workspace_bytes(dn, ncols);
+    if ((rc = mq_malloc(&d_text, dn ? dn : 16)) || (rc = mq_malloc(&d_ws, wsb)) ||
+        (rc = mq_malloc(&d_mm, 8 * (size_t)(ncols ? ncols : 1)))) {
+        fail(ret_status, "load_db allocation", rc);
+        goto out;
+    }
+    if (dn && (rc = h2d(d_text, data, dn))) {
+        fail(ret_status, "load_db upload", rc);
+        goto out;
+    }
+    uint64_t rows = 0;
+    if ((rc = mq_csv_count_rows(d_text, dn, ncols, &rows, d_ws, wsb, g_stream))) {
+        fail(ret_status, "mq_csv_count_rows", rc);
+        goto out;
+    }
+    const size_t old = table->row_count, total = old + rows;
+    /* HBM copies of the whole columns: the resident rows, then the parsed ones */
+    for (int j = 0; j < ncols; j++) {
+        Column* c = table->columns + j;
+        if ((rc = mq_malloc(&dcol[j], (total ? total : 1) * 4))) {
+            fail(ret_status, "load_db column allocation", rc);
+            goto out;
+        }
+        ColEntry* e = col_find(c);
+        if (old && e && e->host == c->data && e->rows == old)
+            rc = mq_memcpy_d2d(dcol[j], e->dev, old * 4, g_stream);
+        else if (old)
+            rc = h2d(dcol[j], c->data, old * 4);
+        if (rc) {
+            fail(ret_status, "load_db column copy", rc);
+            goto out;
+        }
+        dparse[j] = (int32_t*)dcol[j] + old;
+    }
+    if ((rc = mq_csv_parse_int32(d_text, dn, ncols, dparse, rows, d_mm, d_ws, wsb, g_stream))) {
+        fail(ret_status, "mq_csv_parse_int32", rc);
+        goto out;
+    }
+    if (rows && grow_table(db, table, total, ret_status)) {
+        ret_status->code = ERROR;
+        goto out;
+    }
+    if (ncols && (rc = d2h(mm, d_mm, 8 * (size_t)ncols))) {
+        fail(ret_status, "load_db min/max", rc);
+        goto out;
+    }
+    for (int j = 0; j < ncols; j++) {
+        Column* c = table->columns + j;
+        if (rows && (rc = d2h(c->data + old, dparse[j], rows * 4))) {
+            fail(ret_status, "load_db column download", rc);
+            goto out;
+        }
+        c->row_count += rows;
+        if (rows) { /* insert_row :193-194 */
+            c->max = c->max > mm[2 * j + 1] ? c->max : mm[2 * j + 1];
+            c->min = c->min < mm[2 * j] ? c->min : mm[2 * j];
+        }
+        col_put(c, dcol[j]); /* resident for the queries that follow */
+        dcol[j] = NULL;
+    }
+    table->row_count = total;
+out:
+    for (int j = 0; j < ncols && j < 1024; j++)
+        if (dcol[j]) mq_free(dcol[j]);
+    if (d_text) mq_free(d_text);
+    if (d_ws) mq_free(d_ws);
+    if (d_mm) mq_free(d_mm);
+    munmap((void*)text, n);
 }
 
 /* ------------------------------------------------------------------ */

@@ -66,6 +66,16 @@ class SelectOperator(C.Structure):  # db_manager.h:95-108
                 ("comparator", C.c_void_p)]
 
 
+class Table(C.Structure):  # cs165_api.h:110-116
+    _fields_ = [("name", C.c_char * 64), ("columns", C.POINTER(Column)), ("col_count", C.c_size_t),
+                ("row_count", C.c_size_t), ("table_length", C.c_size_t)]
+
+
+class Db(C.Structure):  # cs165_api.h:127-132
+    _fields_ = [("name", C.c_char * 64), ("tables", C.POINTER(Table)), ("tables_size", C.c_size_t),
+                ("tables_capacity", C.c_size_t)]
+
+
 ABI_LAYOUT = {  # SURVEY.md §8(b), measured on the reference with gcc 11 / x86-64
     "Result": (Result, 24, {"num_tuples": 0, "data_type": 8, "payload": 16}),
     "Column": (Column, 128, {"data": 64, "fd": 72, "row_count": 80, "sorted": 88,
@@ -77,6 +87,8 @@ ABI_LAYOUT = {  # SURVEY.md §8(b), measured on the reference with gcc 11 / x86-
                                              "has_low": 76, "has_high": 80, "db": 88,
                                              "table": 96, "column": 104, "col_result": 112,
                                              "pos_result": 120, "comparator": 128}),
+    "Table": (Table, 96, {"columns": 64, "col_count": 72, "row_count": 80, "table_length": 88}),
+    "Db": (Db, 88, {"tables": 64, "tables_size": 72, "tables_capacity": 80}),
 }
 
 _vp, _u64, _i32, _sz, _int = C.c_void_p, C.c_uint64, C.c_int32, C.c_size_t, C.c_int
@@ -154,6 +166,8 @@ _SIGS = {
     "hash_join": (C.POINTER(_PR), [_PR, _PR, _PR, _PR, _PS]),
     "log_result": (None, [_PR]),
     "should_use_index": (C.c_bool, [C.POINTER(Column), _int, _int]),
+    # load path (db_manager.h:254)
+    "load_db": (None, [C.POINTER(Db), C.c_char_p, _PS]),
     # residency
     "mq_column_attach": (_int, [C.POINTER(Column), _vp]),
     "mq_column_upload": (_int, [C.POINTER(Column)]),

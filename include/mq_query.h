@@ -85,6 +85,21 @@ typedef struct GeneralizedColumn {                                    /* cs165_a
     GeneralizedColumnPointer column_pointer;
 } GeneralizedColumn;
 
+typedef struct Table {                                                /* cs165_api.h:110-116 */
+    char name[MQ_MAX_SIZE_NAME];
+    Column* columns;
+    size_t col_count;
+    size_t row_count;
+    size_t table_length;
+} Table;
+
+typedef struct Db {                                                   /* cs165_api.h:127-132 */
+    char name[MQ_MAX_SIZE_NAME];
+    Table* tables;
+    size_t tables_size;
+    size_t tables_capacity;
+} Db;
+
 /* db_manager.h:95-108; only low/high/column are read by libmq (shared_select). */
 typedef struct SelectOperator {
     int select_type;            /* SelectType enum */
@@ -127,6 +142,17 @@ Result* select_column_sorted_index(Column* column, int low, int high,
                                    Status* ret_status);             /* query.c:165-198 */
 /* index.c:180-185 — exported weak so the reference's index.o definition wins. */
 bool should_use_index(Column* column, int low, int high);
+
+/* ---- the load path (db_manager.h:254) ----
+ * load_db (db_manager.c:240-322 with insert_row :164-199): same header check
+ * (db name, table name), same rows, values, min/max and table_length growth, with
+ * the data lines parsed on the GPU (mq_csv_parse_int32). Capacity grows through
+ * the server's own save_data / start_data (db_manager.c:430,736), which libmq
+ * references weakly: without them (no server linked) a load that must grow the
+ * table fails with ERROR. The loaded columns stay resident in HBM for the queries
+ * that follow. To use it, the server links this definition instead of
+ * db_manager.o's. */
+void load_db(Db* db, const char* path, Status* ret_status);
 
 /* ---- libmq residency control (not in the reference) ---- */
 /* Use an existing device copy of column->data (row_count int32 rows in HBM); the

@@ -56,12 +56,15 @@ int main(void){
  printf("%zu %zu %zu %zu %zu %zu\n", offsetof(Column,data), offsetof(Column,row_count),
         offsetof(Column,index), offsetof(Column,max), offsetof(SelectOperator,low),
         offsetof(SelectOperator,column));
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(Table), offsetof(Table,columns),
+        offsetof(Table,table_length), sizeof(Db), offsetof(Db,tables), offsetof(Db,tables_size));
  return 0;}
 ''')
     exe = tmp_path / "lay"
     subprocess.run(["gcc", "-std=c99", "-I", REF_INC, str(src), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
-    assert out == ["24", "128", "16", "16", "136", "64", "80", "96", "120", "68", "104"]
+    assert out == ["24", "128", "16", "16", "136", "64", "80", "96", "120", "68", "104",
+                   "96", "64", "88", "88", "64", "72"]  # = mq_query.c's _Static_asserts
 
 
 def test_libmq_has_no_oracle_code():

@@ -159,3 +159,101 @@ def gpu_load_dev(L, dtext_ptr, n, ncols, rows_expected):
     mq.check(L.mq_csv_parse_int32(dtext_ptr, n, ncols, ptrs, rows.value, mm.ptr, ws.ptr, ws.nbytes,
                                   None))
     return dcols, mm.get(np.int32, 2 * ncols).reshape(ncols, 2)
+
+
+# ---------------------------------------------------------------------------
+# the drop-in load_db (mq_query.c) through the reference's own types
+# ---------------------------------------------------------------------------
+def _table(ncols, capacity, rows_before=0, seed=0):
+    """A Db with one table 'tbl' of ncols columns (host buffers of `capacity` rows),
+    as create_db / create_table / create_column leave it (db_manager.c:34-148),
+    optionally holding rows_before rows already."""
+    rng = np.random.default_rng(seed)
+    bufs = [np.zeros(capacity, dtype=np.int32) for _ in range(ncols)]
+    cols = (mq.Column * ncols)()
+    for j in range(ncols):
+        c = cols[j]
+        c.name = f"c{j}".encode()
+        c.data = bufs[j].ctypes.data_as(C.POINTER(C.c_int))
+        c.fd = -1
+        c.max, c.min = -(2 ** 31), 2 ** 31 - 1
+        if rows_before:
+            bufs[j][:rows_before] = rng.integers(-1000, 1000, rows_before)
+            c.row_count = rows_before
+            c.max, c.min = int(bufs[j][:rows_before].max()), int(bufs[j][:rows_before].min())
+    t = mq.Table()
+    t.name = b"tbl"
+    t.columns = cols
+    t.col_count, t.row_count, t.table_length = ncols, rows_before, capacity
+    db = mq.Db()
+    db.name = b"db"
+    db.tables = C.pointer(t)
+    db.tables_size, db.tables_capacity = 1, 1
+    return db, t, cols, bufs
+
+
+def _write_csv(tmp_path, name, ncols, data, header=None):
+    path = tmp_path / f"{name}.csv"
+    hdr = header if header is not None else (",".join(f"db.tbl.c{j}" for j in range(ncols)) + "\n").encode()
+    path.write_bytes(hdr + data)
+    return str(path)
+
+
+@pytest.mark.parametrize("name", ["basic", "long_lines", "missing_extra", "random_4col", "fuzz_small"])
+def test_load_db_dropin_vs_reference(lib, refcpu, tmp_path, name):
+    """load_db into a table with room for every row (the server's save_data /
+    start_data are not linked into this process): rows, values, min/max as the
+    reference's load_db + insert_row leave them, and the columns stay resident."""
+    ncols, data = CASES[name]
+    path = _write_csv(tmp_path, name, ncols, data)
+    want, want_mm = refcpu.load_csv(data, ncols)
+    rows = want.shape[1]
+    db, t, cols, bufs = _table(ncols, max(rows, 1))
+    st = mq.Status(0, None)
+    lib.load_db(C.byref(db), path.encode(), C.byref(st))
+    assert st.code == mq.OK
+    assert t.row_count == rows and all(cols[j].row_count == rows for j in range(ncols))
+    g = GOLD[name]
+    for j in range(ncols):
+        assert np.array_equal(bufs[j][:rows], want[j]), j
+        if g["minmax"][j] is not None:
+            assert [cols[j].min, cols[j].max] == g["minmax"][j], j
+    check_against_golden(name, np.stack([b[:rows] for b in bufs]), [(c.min, c.max) for c in cols], rows)
+    # resident: a select on column 0 needs no upload
+    lib.mq_transfer_seconds(1)
+    lo, hi = C.c_int(-10 ** 6), C.c_int(10 ** 6)
+    r = lib.select_column(C.byref(cols[0]), C.byref(lo), C.byref(hi), C.byref(st))
+    assert st.code == mq.OK and r
+    k = r.contents.num_tuples
+    assert k == int(((want[0] >= -10 ** 6) & (want[0] < 10 ** 6)).sum())
+
+
+def test_load_db_appends_and_reports_errors(lib, refcpu, tmp_path):
+    ncols, data = CASES["random_4col"]
+    want, _ = refcpu.load_csv(data, ncols)
+    rows = want.shape[1]
+    db, t, cols, bufs = _table(ncols, rows + 100, rows_before=100, seed=3)
+    before = [b[:100].copy() for b in bufs]
+    mm_before = [(c.min, c.max) for c in cols]
+    path = _write_csv(tmp_path, "app", ncols, data)
+    st = mq.Status(0, None)
+    lib.load_db(C.byref(db), path.encode(), C.byref(st))
+    assert st.code == mq.OK and t.row_count == rows + 100
+    for j in range(ncols):
+        assert np.array_equal(bufs[j][:100], before[j]) and np.array_equal(bufs[j][100:], want[j])
+        assert cols[j].min == min(mm_before[j][0], int(want[j].min()))
+        assert cols[j].max == max(mm_before[j][1], int(want[j].max()))
+    # wrong db / table name in the header, missing file: ERROR, table untouched (:253-295)
+    for hdr in (b"other.tbl.c0\n", b"db.nope.c0\n", b"dbtbl\n"):
+        p = _write_csv(tmp_path, "bad", ncols, b"1,2,3,4\n", header=hdr)
+        st = mq.Status(0, None)
+        lib.load_db(C.byref(db), p.encode(), C.byref(st))
+        assert st.code == mq.ERROR and t.row_count == rows + 100
+    st = mq.Status(0, None)
+    lib.load_db(C.byref(db), str(tmp_path / "missing.csv").encode(), C.byref(st))
+    assert st.code == mq.ERROR
+    # growth needs the server's save_data/start_data: without them, ERROR
+    db2, t2, _, _ = _table(ncols, 16)
+    st = mq.Status(0, None)
+    lib.load_db(C.byref(db2), path.encode(), C.byref(st))
+    assert st.code == mq.ERROR and t2.row_count == 0
