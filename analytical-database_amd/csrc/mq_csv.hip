@@ -52,11 +52,12 @@ constexpr int kPre = 16;                 // LDS bytes before the chunk (byte cs-
 constexpr int kHalo = 1024;              // after the chunk: a piece has <= 1023 bytes
 constexpr int kLds = kPre + kChunk + kHalo;
 constexpr int kPiece = 1023;             // fgets(line, 1024)
+constexpr int kList = 4096;              // piece starts listed in LDS (else searched)
 constexpr int kRegCols = 8;              // columns whose min/max live in lane registers
 constexpr int kMaxCols = 1024;
 constexpr int kFillTile = 1024;          // rows per tile in the missing-token fix-up
 
-enum { F_LONG = 0, F_MISSING = 1 };
+enum { F_LONG = 0, F_MISSING = 1, F_MAYBE_LONG = 2 };
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
@@ -169,6 +170,11 @@ __device__ __forceinline__ T wave_incl_max(T v, int lane) {
         const T u = __shfl_up(v, o, 64);
         if (lane >= o) v = v > u ? v : u;
     }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
@@ -291,6 +297,59 @@ __global__ __launch_bounds__(kTPB) void k_csv_count(const char* __restrict__ tex
     if (tid == 0) cnt[c] = tot;
 }
 
+// ---- pass 1, streaming form (the default): row starts per chunk straight from
+// the loaded registers, no LDS. Starts in [cs, ce) are the '\n' bytes in
+// [cs-1, ce-1) (+ position 0). A line over 1023 bytes contains a whole aligned
+// 512-byte block without '\n', so "some such block has no '\n'" flags a possible
+// long line (never misses one); only then does the exact k_csv_count<., false>
+// run (and long mode if it confirms).
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_csv_count_stream(const char* __restrict__ text, uint64_t n,
+                                                            uint32_t* __restrict__ cnt, unsigned* flags) {
+    __shared__ uint32_t s_c[kWaves];
+    const uint64_t c = blockIdx.x, cs = c * kChunk;
+    const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t w[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // 4 x 16 B per lane, 4 KB apart: coalesced
+        const uint64_t g = cs + (uint64_t)q * 4096 + (uint64_t)tid * 16;
+        if (VEC && g + 16 <= ce) {
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + g));
+            w[q][0] = t.x, w[q][1] = t.y, w[q][2] = t.z, w[q][3] = t.w;
+        } else {
+            uint8_t t[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) t[k] = g + k < ce ? (uint8_t)text[g + k] : 0;
+            memcpy(w[q], t, 16);
+        }
+    }
+    uint32_t cntl = 0;
+    bool nolf_block = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t m = nl4(w[q][0]) | (nl4(w[q][1]) << 4) | (nl4(w[q][2]) << 8) | (nl4(w[q][3]) << 12);
+        cntl += __popc(m);
+        // 32 lanes x 16 B = one aligned 512-byte block; count only blocks wholly in the text
+        const unsigned long long b = __ballot(m != 0);
+        const uint64_t g = cs + (uint64_t)q * 4096 + (uint64_t)(tid & ~31) * 16;
+        const uint32_t half = (uint32_t)(b >> (lane & 32));
+        if (g + 512 <= n && half == 0) nolf_block = true;
+    }
+    cntl = (uint32_t)wave_sum_u32(cntl);
+    if (lane == 0) s_c[tid >> 6] = cntl;
+    if (__ballot(nolf_block) && lane == 0) atomicOr(&flags[F_MAYBE_LONG], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        // starts = '\n' in [cs-1, ce-1), plus position 0
+        if (cs == 0) t += 1;
+        else t += text[cs - 1] == '\n';
+        t -= text[ce - 1] == '\n';
+        cnt[c] = t;
+    }
+}
+
 // Long lines across chunks: a full chunk without a start lies inside a line of
 // more than 16 KB; otherwise compare each chunk's first start with the previous
 // chunk's last, and the text end with the final start.
@@ -385,6 +444,68 @@ __device__ __forceinline__ int32_t parse_token(const uint8_t* __restrict__ s, in
     return (int32_t)(uint32_t)(neg ? 0ull - acc : acc);
 }
 
+// Bytes of a word that are not ASCII digits: bit 7 of each such byte (exact, no
+// carries across bytes).
+__device__ __forceinline__ unsigned long long nondigit8(unsigned long long w) {
+    const unsigned long long y = w ^ 0x3030303030303030ull;
+    return (((y & 0x7F7F7F7F7F7F7F7Full) + 0x7676767676767676ull) | y) & 0x8080808080808080ull;
+}
+
+// The common token, from registers: [-]digits{0..10} ended by ',', '\n', NUL or the
+// piece end. The 16 bytes at k come from 5 aligned LDS dwords + alignbyte; the
+// non-digit flags of two 64-bit words locate the end (ctz), and the digits are
+// converted SWAR-style (8 at once: x*10 + x>>8, then two 64-bit multiplies).
+// Anything else (leading isspace, '+', junk after the digits, more than 10 digits)
+// returns false and the caller runs parse_token, the byte-at-a-time restatement
+// of strtol.
+__device__ __forceinline__ bool token_fast(const uint8_t* __restrict__ s, int& k, int kend, bool& more,
+                                           int32_t& out) {
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(s) + (k >> 2);
+    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+    const uint32_t r = (uint32_t)k & 3u;
+    unsigned long long lo = (unsigned long long)__builtin_amdgcn_alignbyte(d1, d0, r) |
+                            ((unsigned long long)__builtin_amdgcn_alignbyte(d2, d1, r) << 32);
+    unsigned long long hi = (unsigned long long)__builtin_amdgcn_alignbyte(d3, d2, r) |
+                            ((unsigned long long)__builtin_amdgcn_alignbyte(d4, d3, r) << 32);
+    const int lim = kend - k;  // bytes left in the piece (>= 0)
+    unsigned long long nlo = nondigit8(lo), nhi = nondigit8(hi);
+    constexpr unsigned long long kHi = 0x8080808080808080ull;
+    if (lim < 8) nlo |= kHi << (8 * lim), nhi = kHi;  // past the piece: terminators
+    else if (lim < 16) nhi |= kHi << (8 * (lim - 8));
+    const bool neg = lim > 0 && (lo & 0xFFu) == '-';
+    if (neg) nlo &= ~0x80ull;
+    const int e = nlo ? (__builtin_ctzll(nlo) >> 3) : nhi ? 8 + (__builtin_ctzll(nhi) >> 3) : 16;
+    const int L = e - (neg ? 1 : 0);
+    if (L > 10) return false;
+    bool m = false;
+    if (e < lim) {
+        const uint32_t c = (uint32_t)((e < 8 ? lo >> (8 * e) : hi >> (8 * (e - 8))) & 0xFFu);
+        if (c == ',') m = true;
+        else if (c != '\n' && c != 0) return false;  // isspace / '+' / junk: the slow path
+    }
+    if (neg) lo = (lo >> 8) | (hi << 56), hi >>= 8;
+    const int l8 = L < 8 ? L : 8;
+    unsigned long long x = lo - 0x3030303030303030ull;
+    x = l8 ? x << (8 * (8 - l8)) : 0ull;  // the first l8 digits, right-aligned
+    x = x * 10 + (x >> 8);
+    x = (((x & 0x000000FF000000FFull) * (100 + (1000000ull << 32))) +
+         (((x >> 16) & 0x000000FF000000FFull) * (1 + (10000ull << 32)))) >> 32;
+    unsigned long long v = x;
+    if (L > 8) v = v * 10 + ((hi & 0xFFu) - '0');
+    if (L > 9) v = v * 10 + (((hi >> 8) & 0xFFu) - '0');
+    out = (int32_t)(uint32_t)(neg ? 0ull - v : v);
+    more = m;
+    k += e + (m ? 1 : 0);
+    return true;
+}
+
+__device__ __forceinline__ int32_t next_token(const uint8_t* __restrict__ s, int& k, int kend,
+                                              bool& more) {
+    int32_t v;
+    if (token_fast(s, k, kend, more, v)) return v;
+    return parse_token(s, k, kend, more);
+}
+
 // ---- pass 2: parse. One block per chunk. The chunk's row starts stay as one
 // 64-bit mask per thread segment plus the exclusive prefix of their counts; lane i
 // takes pieces i, i+256, ... and finds piece i's byte by a binary search over the
@@ -396,8 +517,9 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
                                                      int32_t* const* __restrict__ cols,
                                                      int2* __restrict__ partial, uint16_t* __restrict__ nf,
                                                      unsigned* flags) {
-    __shared__ __attribute__((aligned(16))) uint8_t s[kLds];
+    __shared__ __attribute__((aligned(16))) uint8_t s[kLds + 32];  // + token_fast's over-read
     __shared__ unsigned long long s_mask[kTPB];
+    __shared__ uint16_t s_list[kList];
     __shared__ uint32_t s_off[kTPB];
     __shared__ long long s_w[kWaves];
     __shared__ uint32_t s_u[kWaves];
@@ -419,8 +541,13 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
         st = piece_starts(st, a, block_excl_max(mylast, prev[c], s_w), ce);
     }
     uint32_t nst;
-    s_off[tid] = block_excl_sum((uint32_t)__popcll(st), s_u, &nst);
+    const uint32_t o = block_excl_sum((uint32_t)__popcll(st), s_u, &nst);
+    s_off[tid] = o;
     s_mask[tid] = st;
+    if (nst <= (uint32_t)kList) {  // the usual case: an explicit start list
+        uint32_t q = o;
+        for (unsigned long long m = st; m; m &= m - 1) s_list[q++] = (uint16_t)(tid * kSeg + __builtin_ctzll(m));
+    }
     __syncthreads();
 
     const uint64_t r0 = row_base[c];
@@ -429,13 +556,18 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
     for (int j = 0; j < kRegCols; j++) mn[j] = INT_MAX, mx[j] = INT_MIN;
     bool missing = false;
     for (uint32_t i = tid; i < nst; i += kTPB) {
-        int t = 0;  // last segment whose prefix is <= i
+        int off;  // piece start within the chunk
+        if (nst <= (uint32_t)kList) {
+            off = s_list[i];
+        } else {  // more starts than the list holds: search the per-segment prefix
+            int t = 0;  // last segment whose prefix is <= i
 #pragma unroll
-        for (int step = kTPB / 2; step > 0; step >>= 1)
-            if (s_off[t + step] <= i) t += step;
-        unsigned long long m = s_mask[t];
-        for (uint32_t r = s_off[t]; r < i; r++) m &= m - 1;
-        const int off = t * kSeg + __builtin_ctzll(m);  // piece start within the chunk
+            for (int step = kTPB / 2; step > 0; step >>= 1)
+                if (s_off[t + step] <= i) t += step;
+            unsigned long long m = s_mask[t];
+            for (uint32_t r = s_off[t]; r < i; r++) m &= m - 1;
+            off = t * kSeg + __builtin_ctzll(m);
+        }
         const uint64_t p = cs + (uint64_t)off;
         const uint64_t pe = p + kPiece < n ? p + kPiece : n;  // fgets cap / EOF
         int k = kPre + off;
@@ -446,7 +578,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
 #pragma unroll
         for (int j = 0; j < kRegCols; j++) {
             if (j < ncols && more) {
-                const int32_t v = parse_token(s, k, kend, more);
+                const int32_t v = next_token(s, k, kend, more);
                 cols[j][row] = v;
                 mn[j] = min(mn[j], v);
                 mx[j] = max(mx[j], v);
@@ -454,7 +586,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
             }
         }
         for (int j = kRegCols; j < ncols && more; j++) {
-            const int32_t v = parse_token(s, k, kend, more);
+            const int32_t v = next_token(s, k, kend, more);
             cols[j][row] = v;
             atomicMin(&s_mm[2 * j], v);
             atomicMax(&s_mm[2 * j + 1], v);
@@ -649,13 +781,22 @@ int mq_csv_count_rows(const char* d_text, uint64_t n, int ncols, uint64_t* h_row
     HIPCHK(hipMemsetAsync(w.flags, 0, 64, st));
     if (n == 0) return MQ_OK;
     const uint64_t nch = nchunks_of(n);
-    if ((rc = launch_count(d_text, n, w, false, st))) return rc;
-    hipLaunchKernelGGL(k_csv_long_check, dim3((unsigned)((nch + kTPB - 1) / kTPB)), dim3(kTPB), 0, st,
-                       w.cnt, w.first, w.last, nch, n, w.flags);
-    LAUNCHCHK("k_csv_long_check");
-    unsigned flags[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(flags, w.flags, 8, hipMemcpyDeviceToHost, st));
+    if (aligned16(d_text))
+        hipLaunchKernelGGL((k_csv_count_stream<true>), dim3((unsigned)nch), dim3(kTPB), 0, st, d_text, n, w.cnt, w.flags);
+    else
+        hipLaunchKernelGGL((k_csv_count_stream<false>), dim3((unsigned)nch), dim3(kTPB), 0, st, d_text, n, w.cnt, w.flags);
+    LAUNCHCHK("k_csv_count_stream");
+    unsigned flags[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(flags, w.flags, 16, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (flags[F_MAYBE_LONG]) {  // exact check: a gap of more than 1023 bytes between starts?
+        if ((rc = launch_count(d_text, n, w, false, st))) return rc;
+        hipLaunchKernelGGL(k_csv_long_check, dim3((unsigned)((nch + kTPB - 1) / kTPB)), dim3(kTPB), 0, st,
+                           w.cnt, w.first, w.last, nch, n, w.flags);
+        LAUNCHCHK("k_csv_long_check");
+        HIPCHK(hipMemcpyAsync(flags, w.flags, 16, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     if (flags[F_LONG]) {  // lines over 1023 bytes: rows are fgets pieces
         hipLaunchKernelGGL(k_csv_prev_start, dim3(1), dim3(1024), 0, st, w.last, nch, w.prev);
         LAUNCHCHK("k_csv_prev_start");
