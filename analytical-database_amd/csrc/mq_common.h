@@ -30,6 +30,13 @@ uint64_t scan_u32_scratch_elems(uint64_t n);
 int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st);
 
+// Stable LSD radix sort (4 x 8-bit digits) of (int32 key, u32 value) pairs by key
+// (mq_join.hip). vals == nullptr sorts (key, row id). *keys_out receives the keys
+// as (uint32)key ^ 0x80000000 (ascending as unsigned), *vals_out the values; both
+// are pool_alloc'd (the caller pool_frees them). Synchronises the stream.
+int radix_sort_pairs(const int* keys, const int* vals, uint64_t n, uint32_t** keys_out,
+                     uint32_t** vals_out, hipStream_t st, const DevState* s);
+
 // Caching device allocator for per-call scratch (join tables and partitions,
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
 // idle blocks are released by mq_trim(). A freed block may be handed out again at

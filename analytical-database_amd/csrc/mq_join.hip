@@ -548,6 +548,11 @@ __global__ __launch_bounds__(kTPB) void k_ht_set_len(const uint32_t* __restrict_
     }
 }
 
+__global__ __launch_bounds__(kTPB) void k_iota_u32(uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] = (uint32_t)i;
+}
+
 __global__ __launch_bounds__(kTPB) void k_flip_keys(const int* __restrict__ in, uint64_t n,
                                                     uint32_t* __restrict__ out) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
@@ -720,8 +725,12 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     return done(MQ_OK);
 }
 
-int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, uint32_t** vals_out,
-               hipStream_t st, const DevState* s) {
+}  // namespace
+
+namespace mqi {
+
+int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out,
+                     uint32_t** vals_out, hipStream_t st, const DevState* s) {
     // buffers: keys/vals double buffers, histogram, its scan, scan scratch
     uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *hist = nullptr;
     u64 *hscan = nullptr, *scratch = nullptr;
@@ -745,10 +754,14 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
     hscan = (u64*)pool_alloc(nh * 8);
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
     if (!k0 || !v0 || !k1 || !v1 || !hist || !hscan || !scratch)
-        return fail(set_err(MQ_ENOMEM, "join: sort buffers (%llu rows)", (unsigned long long)n));
+        return fail(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
     hipLaunchKernelGGL(k_flip_keys, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, n, k0);
-    if (hipMemcpyAsync(v0, p1, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return fail(set_err(MQ_EHIP, "join: copy positions"));
+    if (p1) {
+        if (hipMemcpyAsync(v0, p1, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return fail(set_err(MQ_EHIP, "sort: copy values"));
+    } else {
+        hipLaunchKernelGGL(k_iota_u32, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, n, v0);
+    }
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
         hipLaunchKernelGGL(k_sort_hist, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, n, shift,
@@ -757,7 +770,7 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
         if (rc) return fail(rc);
         hipLaunchKernelGGL(k_sort_scatter, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, v0, k1,
                            v1, n, shift, hscan, (uint32_t)ntiles);
-        if (hipGetLastError() != hipSuccess) return fail(set_err(MQ_EHIP, "join: sort launch"));
+        if (hipGetLastError() != hipSuccess) return fail(set_err(MQ_EHIP, "sort: launch"));
         uint32_t* t = k0;
         k0 = k1;
         k1 = t;
@@ -765,7 +778,7 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
         v0 = v1;
         v1 = t;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_err(MQ_EHIP, "join: sort sync"));
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_err(MQ_EHIP, "sort: sync"));
     pool_free(k1);
     pool_free(v1);
     pool_free(hist);
@@ -776,7 +789,7 @@ int sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out, ui
     return MQ_OK;
 }
 
-}  // namespace
+}  // namespace mqi
 
 extern "C" {
 
@@ -827,7 +840,7 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
                 return rc;
             }
             uint32_t *skeys, *svals;
-            if ((rc = sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) {
+            if ((rc = radix_sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) {
                 jfree_all(j);
                 delete j;
                 return rc;

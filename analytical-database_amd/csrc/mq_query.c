@@ -948,6 +948,130 @@ out:
 }
 
 /* ------------------------------------------------------------------ */
+/* index build: index.c:152-178 build_index                           */
+/* ------------------------------------------------------------------ */
+
+#define MQ_BIN_NUM 100 /* cs165_api.h:46 */
+typedef struct MqHistogram { /* cs165_api.h:71-75 */
+    int bin_size;
+    int values[MQ_BIN_NUM];
+    size_t counts[MQ_BIN_NUM];
+} MqHistogram;
+_Static_assert(sizeof(MqHistogram) == 1208, "Histogram size");
+
+static void idx_put(ColumnIndex* ix, size_t n, void* d_values, void* d_positions) {
+    for (int i = 0; i < g_nidx; i++)
+        if (g_idx[i].index == ix) {
+            mq_free(g_idx[i].d_values);
+            mq_free(g_idx[i].d_positions);
+            g_idx[i] = g_idx[--g_nidx];
+            break;
+        }
+    if (g_nidx == MAX_INDEXES) {
+        mq_free(g_idx[0].d_values);
+        mq_free(g_idx[0].d_positions);
+        g_idx[0] = g_idx[--g_nidx];
+    }
+    g_idx[g_nidx++] = (IndexEntry){ix, ix->values, ix->positions, n, d_values, d_positions};
+}
+
+/* One indexed column (index.c:119-143 + :63-84). Returns 0 or an MQ_E code. */
+static int index_one(Table* t, Column* c, Status* st) {
+    const size_t n = c->row_count;
+    const int32_t* dcol;
+    int rc;
+    if ((rc = column_device(c, &dcol, st))) return rc;
+    void *dv = NULL, *dp = NULL, *dh = NULL;
+    ColumnIndex* ix = malloc(sizeof(ColumnIndex)); /* init_column_index :89-100 */
+    int* hv = malloc((n ? n : 1) * sizeof(int));
+    size_t* hp = malloc((n ? n : 1) * sizeof(size_t));
+    if (!ix || !hv || !hp) {
+        rc = MQ_ENOMEM;
+        goto bad;
+    }
+    if ((rc = mq_malloc(&dv, (n ? n : 1) * 4)) || (rc = mq_malloc(&dp, (n ? n : 1) * 8))) goto bad;
+    if ((rc = mq_index_build(dcol, n, dv, dp, g_stream))) goto bad;
+    if (n && (rc = d2h(hv, dv, n * 4))) goto bad;
+    ix->values = hv;
+    if (c->clustered) {
+        /* build_clustered_index :119-135: the sort ran on a copy of the positions, so
+         * index->positions stays 0..n-1; the permutation reorders every other column */
+        for (size_t i = 0; i < n; i++) hp[i] = i;
+        for (size_t j = 0; j < t->col_count; j++) {
+            Column* o = t->columns + j;
+            if (!strcmp(o->name, c->name)) continue;
+            const int32_t* dsrc;
+            void* dnew = NULL;
+            if ((rc = column_device(o, &dsrc, st))) goto bad;
+            if ((rc = mq_malloc(&dnew, (n ? n : 1) * 4))) goto bad;
+            if ((rc = mq_gather_u64(dsrc, (const uint64_t*)dp, n, dnew, g_stream)) ||
+                (n && (rc = d2h(o->data, dnew, n * 4)))) {
+                mq_free(dnew);
+                goto bad;
+            }
+            col_put(o, dnew); /* the reordered rows stay resident */
+        }
+        if (n && (rc = mq_memcpy_h2d(dp, hp, n * 8, g_stream))) goto bad;
+    } else {
+        /* build_unclustered_index :140-143 + build_histogram :63-84 */
+        if (n && (rc = d2h(hp, dp, n * 8))) goto bad;
+        MqHistogram* h = malloc(sizeof(MqHistogram));
+        if (!h) {
+            rc = MQ_ENOMEM;
+            goto bad;
+        }
+        h->bin_size = (c->max - c->min) / (MQ_BIN_NUM - 1);
+        memset(h->values, 0, sizeof h->values);
+        memset(h->counts, 0, sizeof h->counts);
+        size_t bin_start = 0;
+        for (int b = 0; b < MQ_BIN_NUM; b++) {
+            h->values[b] = (int)bin_start;
+            bin_start += (size_t)(long)h->bin_size;
+        }
+        if (h->bin_size == 0) {
+            fprintf(stderr, "libmq: build_index: column %s spans < %d values; histogram counts left 0 "
+                            "(the reference divides by zero here)\n", c->name, MQ_BIN_NUM - 1);
+        } else {
+            uint64_t counts[MQ_BIN_NUM + 1];
+            if ((rc = mq_malloc(&dh, sizeof counts)) ||
+                (rc = mq_histogram(dcol, n, c->min, h->bin_size, dh, g_stream)) ||
+                (rc = d2h(counts, dh, sizeof counts))) {
+                free(h);
+                goto bad;
+            }
+            for (int b = 0; b < MQ_BIN_NUM; b++) h->counts[b] = counts[b];
+        }
+        c->histogram = (struct Histogram*)h;
+    }
+    ix->positions = hp;
+    c->index = ix;
+    idx_put(ix, n, dv, dp); /* resident for select_column_sorted_index */
+    mq_free(dh);
+    return 0;
+bad:
+    free(ix);
+    free(hv);
+    free(hp);
+    mq_free(dv);
+    mq_free(dp);
+    mq_free(dh);
+    fail(st, "build_index", rc);
+    return rc;
+}
+
+void build_index(Db* db) {
+    Status st = {OK, NULL};
+    if (!db || ready(&st)) return;
+    for (size_t i = 0; i < db->tables_size; i++) {
+        Table* t = db->tables + i;
+        for (size_t j = 0; j < t->col_count; j++) {
+            Column* c = t->columns + j;
+            if (c->has_index && index_one(t, c, &st)) return; /* build_btree is a no-op */
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* residency control                                                  */
 /* ------------------------------------------------------------------ */
 

@@ -135,6 +135,9 @@ _SIGS = {
                                    _vp]),
     "mq_index_select": (_int, [_vp, _vp, _u64, _i32, _i32, _vp, _vp, _vp]),
     "mq_fetch": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "mq_index_build": (_int, [_vp, _u64, _vp, _vp, _vp]),
+    "mq_gather_u64": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "mq_histogram": (_int, [_vp, _u64, _i32, _i32, _vp, _vp]),
     "mq_reduce": (_int, [_vp, _u64, _vp, _vp, _sz, _vp]),
     "mq_add": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "mq_sub": (_int, [_vp, _vp, _u64, _vp, _vp]),
@@ -168,6 +171,7 @@ _SIGS = {
     "should_use_index": (C.c_bool, [C.POINTER(Column), _int, _int]),
     # load path (db_manager.h:254)
     "load_db": (None, [C.POINTER(Db), C.c_char_p, _PS]),
+    "build_index": (None, [C.POINTER(Db)]),
     # residency
     "mq_column_attach": (_int, [C.POINTER(Column), _vp]),
     "mq_column_upload": (_int, [C.POINTER(Column)]),

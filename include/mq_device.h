@@ -120,6 +120,22 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
 int mq_index_select(const int32_t* d_values, const uint64_t* d_positions, uint64_t n, int32_t low,
                     int32_t high, int32_t* d_pos_out, uint64_t* d_count, void* stream);
 
+/* ---- index build (index.c:89-143) ----
+ * Sorted copy of d_col (n < 2^32 rows): d_values_out ascending (may be NULL) and
+ * d_positions_out[i] (size_t, may be NULL) the row it came from, equal values in
+ * ascending row order. (The reference's quicksort orders equal values its own way;
+ * the values, and the positions of distinct values, are identical.) */
+int mq_index_build(const int32_t* d_col, uint64_t n, int32_t* d_values_out,
+                   uint64_t* d_positions_out, void* stream);
+/* reorder_column (index.c:105-114): d_out[i] = d_col[d_positions[i]] (size_t positions) */
+int mq_gather_u64(const int32_t* d_col, const uint64_t* d_positions, uint64_t n, int32_t* d_out,
+                  void* stream);
+/* build_histogram's counts (index.c:63-84): d_counts[b] (101 u64) = rows with
+ * (int)(v - col_min) / bin_size == b for b in [0, 100); d_counts[100] = rows outside
+ * (the reference writes those past its 100-entry array). bin_size != 0. */
+int mq_histogram(const int32_t* d_col, uint64_t n, int32_t col_min, int32_t bin_size,
+                 uint64_t* d_counts, void* stream);
+
 /* ---- S5 fetch_column: d_out[i] = d_col[d_pos[i]] ---- */
 int mq_fetch(const int32_t* d_col, const int32_t* d_pos, uint64_t k, int32_t* d_out, void* stream);
 

@@ -154,6 +154,18 @@ bool should_use_index(Column* column, int low, int high);
  * db_manager.o's. */
 void load_db(Db* db, const char* path, Status* ret_status);
 
+/* ---- the index build (index.c:152-178 build_index, db_manager.h:282) ----
+ * For every column with has_index: the sorted copy and its positions on the GPU
+ * (mq_index_build), then, as the reference does, clustered: index->positions left
+ * 0..n-1 and every other column of the table reordered by the sort permutation;
+ * unclustered: index->positions = the permutation plus the 100-bin histogram. The
+ * index arrays, histogram and reordered rows are host memory as in the reference
+ * (malloc'd / the mmap'd column data); their HBM copies stay resident. Equal values
+ * come out in ascending row order (the reference's quicksort orders them its own
+ * way). Used like load_db: the server links this definition
+ * instead of index.o's. */
+void build_index(Db* db);
+
 /* ---- libmq residency control (not in the reference) ---- */
 /* Use an existing device copy of column->data (row_count int32 rows in HBM); the
  * caller keeps ownership of d_data and must keep it alive while attached. */

@@ -559,3 +559,44 @@ size_t rc_load_csv(const char* text, size_t n, int ncols, int32_t** cols, size_t
     free(row);
     return rows;
 }
+
+/* ------------------------------------------------------------------ */
+/* index build: src/index.c:25-143 (sorted copy + positions)           */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    int32_t v;
+    uint64_t row;
+} IdxPair;
+
+static int idx_cmp(const void* a, const void* b) {
+    const IdxPair* x = a;
+    const IdxPair* y = b;
+    if (x->v != y->v) return x->v < y->v ? -1 : 1;
+    return x->row < y->row ? -1 : (x->row > y->row);
+}
+
+/* init_column_index + quicksort (index.c:89-100, :25-46): the values sorted
+ * ascending and the row each came from. Equal values in ascending row order — the
+ * reference's Lomuto quicksort leaves them in an order of its own; the restatement
+ * pins the values exactly and, per value, the set of rows. */
+void rc_index_build(const int32_t* col, size_t n, int32_t* values, uint64_t* positions) {
+    IdxPair* p = malloc((n ? n : 1) * sizeof(IdxPair));
+    for (size_t i = 0; i < n; i++) p[i] = (IdxPair){col[i], i};
+    qsort(p, n, sizeof(IdxPair), idx_cmp);
+    for (size_t i = 0; i < n; i++) {
+        values[i] = p[i].v;
+        positions[i] = p[i].row;
+    }
+    free(p);
+}
+
+/* build_histogram (index.c:63-84): counts[(v - min) / bin_size]; rows whose bin is
+ * outside [0, 100) go to counts[100] (the reference writes past its array). */
+void rc_histogram(const int32_t* col, size_t n, int32_t mn, int32_t bin_size, uint64_t* counts) {
+    memset(counts, 0, 101 * sizeof(uint64_t));
+    for (size_t i = 0; i < n; i++) {
+        const int b = (int)((uint32_t)col[i] - (uint32_t)mn) / bin_size;
+        counts[(b >= 0 && b < 100) ? b : 100]++;
+    }
+}

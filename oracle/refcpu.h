@@ -79,6 +79,11 @@ int32_t rc_multimap_size(int32_t tuple_num);
  * receive column j and minmax[2j], [2j+1] its min / max (INT32_MAX / INT32_MIN
  * when there are no rows). cols == NULL counts only; (size_t)-1 when rows > cap. */
 size_t rc_csv_header_len(const char* text, size_t n);
+
+/* ---- index build (index.c:25-143): stable sort of (value, row) ---- */
+void rc_index_build(const int32_t* col, size_t n, int32_t* values, uint64_t* positions);
+/* build_histogram counts (index.c:63-84); counts has 101 entries, [100] = out of range */
+void rc_histogram(const int32_t* col, size_t n, int32_t mn, int32_t bin_size, uint64_t* counts);
 size_t rc_load_csv(const char* text, size_t n, int ncols, int32_t** cols, size_t cap,
                    int32_t* minmax);
 

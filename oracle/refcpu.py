@@ -62,6 +62,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rc_multimap_size": (_i32, [_i32]),
         "rc_csv_header_len": (_sz, [_vp, _sz]),
         "rc_load_csv": (_sz, [_vp, _sz, C.c_int, _vp, _sz, _vp]),
+        "rc_index_build": (None, [_vp, _sz, _vp, _vp]),
+        "rc_histogram": (None, [_vp, _sz, _i32, _i32, _vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -238,3 +240,19 @@ def load_csv(text: bytes, ncols: int):
 def fnv1a64_bytes(b: bytes) -> int:
     buf = C.create_string_buffer(b, len(b))
     return int(lib().rc_fnv1a64(buf, len(b)))
+
+
+def index_build(col: np.ndarray):
+    """(sorted values int32, positions uint64), equal values in ascending row order."""
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    v = np.empty(max(len(col), 1), dtype=np.int32)
+    p = np.empty(max(len(col), 1), dtype=np.uint64)
+    lib().rc_index_build(_a(col), len(col), _a(v), _a(p))
+    return v[:len(col)].copy(), p[:len(col)].copy()
+
+
+def histogram(col: np.ndarray, mn: int, bin_size: int) -> np.ndarray:
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    out = np.zeros(101, dtype=np.uint64)
+    lib().rc_histogram(_a(col), len(col), mn, bin_size, _a(out))
+    return out

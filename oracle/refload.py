@@ -48,12 +48,22 @@ class Db(C.Structure):  # cs165_api.h:127-132
                 ("tables_capacity", C.c_size_t)]
 
 
+class ColumnIndex(C.Structure):  # cs165_api.h:117-120
+    _fields_ = [("values", C.POINTER(C.c_int)), ("positions", C.POINTER(C.c_size_t))]
+
+
+class Histogram(C.Structure):  # cs165_api.h:71-75
+    _fields_ = [("bin_size", C.c_int), ("values", C.c_int * 100), ("counts", C.c_size_t * 100)]
+
+
 def have() -> bool:
     return os.path.exists(LIBDBM)
 
 
-def run(csv_path: str, ncols: int) -> dict:
-    """Child-process entry: the reference's load of csv_path into a fresh table."""
+def run(csv_path: str, ncols: int, index_spec: str = "") -> dict:
+    """Child-process entry: the reference's load of csv_path into a fresh table.
+    index_spec "j:c,k:u" declares create(idx, col j, sorted, clustered) / col k
+    unclustered before the load; then build_index runs as server.c:125 does."""
     with tempfile.TemporaryDirectory() as tmp:
         os.makedirs(os.path.join(tmp, "database"))
         os.chdir(tmp)
@@ -73,8 +83,15 @@ def run(csv_path: str, ncols: int) -> dict:
         for j in range(ncols):
             L.create_column(tbl, f"c{j}".encode(), False, C.byref(s))
             assert s.code == 0, j
+        L.create_index.argtypes = [C.POINTER(Column), C.c_bool, C.c_bool, C.POINTER(Status)]
+        L.build_index.argtypes = [C.POINTER(Db)]
+        spec = [(int(a), b == "c") for a, b in (x.split(":") for x in index_spec.split(",") if x)]
+        for j, clustered in spec:
+            L.create_index(C.pointer(tbl.contents.columns[j]), clustered, True, C.byref(s))
         s = Status()
         L.load_db(db, csv_path.encode(), C.byref(s))
+        if spec and s.code == 0:
+            L.build_index(db)
         t = tbl.contents
         rows = int(t.row_count)
         cols = np.zeros((ncols, rows), dtype=np.int32)
@@ -84,20 +101,31 @@ def run(csv_path: str, ncols: int) -> dict:
             if rows:
                 cols[j] = np.ctypeslib.as_array(c.data, shape=(rows,))
             mm[j] = (c.min, c.max)
-        return {"code": int(s.code), "rows": rows, "table_length": int(t.table_length),
-                "cols": cols, "minmax": mm}
+        out = {"code": int(s.code), "rows": rows, "table_length": int(t.table_length),
+               "cols": cols, "minmax": mm}
+        for j, clustered in spec:
+            c = t.columns[j]
+            ix = C.cast(c.index, C.POINTER(ColumnIndex)).contents
+            out[f"ix{j}_values"] = np.ctypeslib.as_array(ix.values, shape=(rows,)).copy()
+            out[f"ix{j}_positions"] = np.ctypeslib.as_array(ix.positions, shape=(rows,)).copy()
+            if not clustered:
+                h = C.cast(c.histogram, C.POINTER(Histogram)).contents
+                out[f"hist{j}_bin_size"] = np.int64(h.bin_size)
+                out[f"hist{j}_values"] = np.array(h.values[:], dtype=np.int64)
+                out[f"hist{j}_counts"] = np.array(h.counts[:], dtype=np.uint64)
+        return out
 
 
-def load(csv_path: str, ncols: int) -> dict:
-    """The reference's load of csv_path, run in a child process."""
+def load(csv_path: str, ncols: int, index_spec: str = "") -> dict:
+    """The reference's load (and index build) of csv_path, run in a child process."""
     with tempfile.TemporaryDirectory() as tmp:
         out = os.path.join(tmp, "out.npz")
         subprocess.run([sys.executable, os.path.abspath(__file__), os.path.abspath(csv_path),
-                        str(ncols), out], check=True, stdout=subprocess.DEVNULL)
+                        str(ncols), out, index_spec], check=True, stdout=subprocess.DEVNULL)
         z = np.load(out)
         return {k: (z[k] if z[k].ndim else int(z[k])) for k in z.files}
 
 
 if __name__ == "__main__":
-    r = run(sys.argv[1], int(sys.argv[2]))
+    r = run(sys.argv[1], int(sys.argv[2]), sys.argv[4] if len(sys.argv) > 4 else "")
     np.savez(sys.argv[3], **r)

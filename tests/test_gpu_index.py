@@ -1,0 +1,157 @@
+"""The index build on gfx950 (mq_index_build / mq_gather_u64 / mq_histogram,
+csrc/mq_index.hip, and the build_index drop-in in mq_query.c) — bit-exact against
+the oracle's stable restatement, and against the reference's own build_index
+goldens in their tie-order-free form (tests/test_oracle_index.py).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from devbuf import Dev
+from indexcases import cases, model
+from refapi import mq
+from test_oracle_index import check_index_result
+
+pytestmark = pytest.mark.gpu
+CASES = {name: (cols, spec) for name, cols, spec in cases()}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    L = mq.load()
+    mq.check(L.mq_init(0), "mq_init")
+    return L
+
+
+def gpu_index(L, col: np.ndarray):
+    n = len(col)
+    d = Dev.of(col.astype(np.int32))
+    v, p = Dev(max(n, 1) * 4), Dev(max(n, 1) * 8)
+    mq.check(L.mq_index_build(d.ptr, n, v.ptr, p.ptr, None), "mq_index_build")
+    return v.get(np.int32, n), p.get(np.uint64, n)
+
+
+@pytest.mark.parametrize("n,lo,hi", [(0, 0, 1), (1, 0, 1), (1000, -5, 5), (4097, -2**31, 2**31 - 1),
+                                     (100_003, 0, 1000), (1_000_000, -2**31, 2**31 - 1)])
+def test_index_build_vs_oracle(lib, refcpu, n, lo, hi):
+    rng = np.random.default_rng(n)
+    col = rng.integers(lo, hi, n, dtype=np.int64).astype(np.int32) if n else np.zeros(0, np.int32)
+    if n > 4:
+        col[:3] = [-2**31, 2**31 - 1, 0]
+    v, p = gpu_index(lib, col)
+    wv, wp = refcpu.index_build(col)
+    assert np.array_equal(v, wv) and np.array_equal(p, wp)
+
+
+def test_gather_and_histogram_vs_oracle(lib, refcpu):
+    rng = np.random.default_rng(9)
+    col = rng.integers(-10**6, 10**6, 300_000).astype(np.int32)
+    pos = rng.integers(0, len(col), 200_000).astype(np.uint64)
+    dc, dp, out = Dev.of(col), Dev.of(pos), Dev(len(pos) * 4)
+    mq.check(lib.mq_gather_u64(dc.ptr, dp.ptr, len(pos), out.ptr, None))
+    assert np.array_equal(out.get(np.int32, len(pos)), col[pos.astype(np.int64)])
+    for mn, bs in ((int(col.min()), (int(col.max()) - int(col.min())) // 99), (0, 7), (-10, -3)):
+        h = Dev(101 * 8)
+        mq.check(lib.mq_histogram(dc.ptr, len(col), mn, bs, h.ptr, None))
+        assert np.array_equal(h.get(np.uint64, 101), refcpu.histogram(col, mn, bs)), (mn, bs)
+    h = Dev(101 * 8)
+    assert lib.mq_histogram(dc.ptr, len(col), 0, 0, h.ptr, None) == mq.MQ_EINVAL
+
+
+def _db(cols: np.ndarray, spec):
+    """A table as the server holds it after load_db, with create(idx,...) applied."""
+    ncols, n = cols.shape
+    bufs = [np.ascontiguousarray(cols[j].astype(np.int32)) for j in range(ncols)]
+    cs = (mq.Column * ncols)()
+    for j in range(ncols):
+        c = cs[j]
+        c.name = f"c{j}".encode()
+        c.data = bufs[j].ctypes.data_as(C.POINTER(C.c_int))
+        c.row_count = n
+        c.max, c.min = int(bufs[j].max()), int(bufs[j].min())
+    for j, clustered in spec:
+        cs[j].has_index, cs[j].clustered, cs[j].sorted = True, clustered, True
+    t = mq.Table()
+    t.name = b"tbl"
+    t.columns = cs
+    t.col_count, t.row_count, t.table_length = ncols, n, n
+    db = mq.Db()
+    db.name = b"db"
+    db.tables = C.pointer(t)
+    db.tables_size = db.tables_capacity = 1
+    return db, t, cs, bufs
+
+
+class Histogram(C.Structure):  # cs165_api.h:71-75
+    _fields_ = [("bin_size", C.c_int), ("values", C.c_int * 100), ("counts", C.c_size_t * 100)]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_build_index_dropin(lib, refcpu, name):
+    cols, spec = CASES[name]
+    db, t, cs, bufs = _db(cols, spec)
+    lib.build_index(C.byref(db))
+    n = cols.shape[1]
+    got = {"cols": np.stack(bufs)}
+    for j, clustered in spec:
+        ix = cs[j].index.contents
+        got[f"ix{j}_values"] = np.ctypeslib.as_array(ix.values, shape=(n,)).copy()
+        got[f"ix{j}_positions"] = np.ctypeslib.as_array(ix.positions, shape=(n,)).copy()
+        if not clustered:
+            h = C.cast(cs[j].histogram, C.POINTER(Histogram)).contents
+            got[f"hist{j}_bin_size"] = h.bin_size
+            got[f"hist{j}_values"] = np.array(h.values[:], dtype=np.int64)
+            got[f"hist{j}_counts"] = np.array(h.counts[:], dtype=np.uint64)
+    want = model(refcpu, cols, spec)
+    for k, v in want.items():  # bit-exact vs the stable restatement
+        assert np.array_equal(np.asarray(got[k]), np.asarray(v)), (name, k)
+    check_index_result(refcpu, name, got)  # and vs the reference, tie order aside
+    # the index and the reordered columns are resident: a sorted-index select and a
+    # select on a reordered column agree with the host arrays
+    st = mq.Status(0, None)
+    j0 = spec[0][0]
+    lo, hi = int(want[f"ix{j0}_values"][n // 4]), int(want[f"ix{j0}_values"][n // 2])
+    r = lib.select_column_sorted_index(C.byref(cs[j0]), lo, hi, C.byref(st))
+    assert st.code == mq.OK and r
+    k = r.contents.num_tuples
+    pos = np.ctypeslib.as_array(C.cast(r.contents.payload, C.POINTER(C.c_int32)), shape=(k,))
+    v = want[f"ix{j0}_values"]
+    a, b = np.searchsorted(v, lo), np.searchsorted(v, hi)
+    assert k == b - a
+    assert np.array_equal(pos, want[f"ix{j0}_positions"][a:b].astype(np.int32))
+    other = (j0 + 1) % cols.shape[0]
+    lo2, hi2 = C.c_int(int(np.median(bufs[other]))), C.c_int(2**31 - 1)
+    r2 = lib.select_column_scan(C.byref(cs[other]), C.byref(lo2), C.byref(hi2), C.byref(st))
+    k2 = r2.contents.num_tuples
+    p2 = np.ctypeslib.as_array(C.cast(r2.contents.payload, C.POINTER(C.c_int32)), shape=(k2,))
+    assert np.array_equal(p2, np.flatnonzero(bufs[other] >= lo2.value).astype(np.int32))
+
+
+@pytest.mark.big
+def test_index_build_1e9_properties(lib):
+    """Full size: the 1e9-row uniform column (seed 42). Sorted values ascending, the
+    positions a permutation that maps to them, ties in ascending row order."""
+    n = 1_000_000_000
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, 42, n, None))
+    v, p = Dev(n * 4), Dev(n * 8)
+    mq.check(lib.mq_index_build(col.ptr, n, v.ptr, p.ptr, None))
+    g = Dev(n * 4)
+    mq.check(lib.mq_gather_u64(col.ptr, p.ptr, n, g.ptr, None))
+    # gathered == sorted values (difference all zero), values ascending
+    d = Dev(n * 4)
+    mq.check(lib.mq_sub(g.ptr, v.ptr, n, d.ptr, None))
+    ws = Dev(lib.mq_scan_workspace_bytes(n))
+    a = Dev(32)
+    mq.check(lib.mq_reduce(d.ptr, n, a.ptr, ws.ptr, ws.nbytes, None))
+    agg = mq.MqAgg.from_buffer_copy(a.get(np.uint8, 32).tobytes())
+    assert (agg.min, agg.max) == (0, 0)
+    vs = v.get(np.int32, n)
+    assert np.all(vs[1:] >= vs[:-1])
+    ps = p.get(np.uint64, n)
+    tie = vs[1:] == vs[:-1]
+    assert np.all(ps[1:][tie] > ps[:-1][tie])
+    seen = np.zeros(n, dtype=np.bool_)
+    seen[ps.astype(np.int64)] = True
+    assert seen.all()
