@@ -171,3 +171,25 @@ def test_libmq_dropin_server_passes_suite_and_matches_reference(tmp_path):
         del os.environ["MQ_PRINT_GPU_MIN"]
     differ = [t for t in TESTS if _ws(gpu_print[t][0]) != _ws(mine[t][0])]
     assert not differ, f"GPU-formatted print differs on tests {differ}"
+
+
+@pytest.mark.gpu
+@needs_bins
+@pytest.mark.skipif(not _have("server_mq_ix"), reason="server_mq_ix not built")
+@pytest.mark.timeout(900)
+def test_libmq_dropin_with_gpu_index_build(tmp_path):
+    """server_mq_ix also links libmq's build_index (GPU radix sort). Its verdicts
+    must be the reference's; its output must equal the reference server's except
+    where the reference's quicksort ordered equal indexed values differently, and
+    there it must equal it line-for-line after sorting (same rows, other order)."""
+    mine = run_suite(os.path.join(REFBIN, "server_mq_ix"), str(tmp_path / "mqix"))
+    ref = run_suite(os.path.join(REFBIN, "server_ref"), str(tmp_path / "ref"))
+    failed = sorted(t for t, (_, v) in mine.items() if v == "fail")
+    assert set(failed) <= {25}, f"server_mq_ix failed {failed}"
+    order_only = []
+    for t in TESTS:
+        if t in REF_FAILS or _ws(mine[t][0]) == _ws(ref[t][0]):
+            continue
+        assert sorted(_ws(mine[t][0]), key=_sortkey) == sorted(_ws(ref[t][0]), key=_sortkey), t
+        order_only.append(t)
+    print(f"tests whose output differs from the reference only in tie order: {order_only}")
