@@ -201,7 +201,8 @@ def main() -> None:
 
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra:
-        extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold)
+        extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold,
+                           cpu=not args.no_cpu)
 
     if rank == 0:
         ms_step = 1e3 * elapsed / args.steps
@@ -266,7 +267,7 @@ def achievable_read_peak(lib, mq, torch, stream, col, ws, launches: int = 20) ->
             "bytes": nbytes.value, "ms_median": med}
 
 
-def print_leg(lib, mq, torch, dev, stream, pos, k) -> dict:
+def print_leg(lib, mq, torch, dev, stream, pos, k, cpu: bool = True) -> dict:
     """print (query.c:245-304) of config 2's K positions: GPU formatting
     (mq_format_int32 + D2H of the text) vs the reference's sprintf loop on the
     same values (oracle/_ref/libref.so, host)."""
@@ -290,7 +291,7 @@ def print_leg(lib, mq, torch, dev, stream, pos, k) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import refcpu  # baseline only
-    if refcpu.have_reference():
+    if cpu and refcpu.have_reference():
         from refapi import Api
         vals = pos[:k].cpu().numpy()
         api = Api(refcpu.reference())
@@ -318,7 +319,7 @@ def traffic_per_launch(n: int):
     return None
 
 
-def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) -> dict:
+def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, cpu=True) -> dict:
     """Secondary measurements (rank 0, N=1): the API path with positions
     materialized (config 2's 4N+4K), and config 3 (select col0 -> fetch col1 ->
     avg) both as the three-operator chain and fused."""
@@ -383,7 +384,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
         t_fused = timed(fused)
         a2 = agg.cpu()
         fused_ok = bool(c3) and (int(a2[0]), int(a2[1])) == (c3[0]["k"], c3[0]["sum"])
-        out["print_positions"] = print_leg(lib, mq, torch, dev, stream, pos, k)
+        out["print_positions"] = print_leg(lib, mq, torch, dev, stream, pos, k, cpu=cpu)
         out["config2_positions"] = {
             "ms": t_pos, "rows_per_s": n / (t_pos * 1e-3), "k": k,
             "algorithmic_bytes": 4 * n + 4 * k,
@@ -401,7 +402,9 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold) 
             "note": "select col0 + gather col1 at matches, one kernel"}
         del pos, col1, vals
     out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
-    out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold)
+    out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
+    out["load_csv_config3_table"] = load_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
+    out["index_build"] = index_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     return out
 
 
@@ -446,7 +449,7 @@ def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:
     return res
 
 
-def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28) -> dict:
+def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True) -> dict:
     """Config 5: 2^28 x 2^28 hash join (build + probe + pair write), keys of
     SURVEY.md §8(c); parity = M and the FNV-1a-64 of the pairs vs the reference."""
     import numpy as np
@@ -488,7 +491,7 @@ def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28) -> dict:
            "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9, "parity": ok,
            "note": "wall time of build+probe+write incl. 2 host syncs (dup flag, M); "
                    "unique-key build path (keys are a bijection)"}
-    if refcpu.have_reference():  # the reference's own join, at a size it finishes quickly
+    if cpu and refcpu.have_reference():  # the reference's own join, at a size it finishes quickly
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from refapi import Api
         api = Api(refcpu.reference())
@@ -499,6 +502,118 @@ def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28) -> dict:
         tr = time.perf_counter() - t0
         res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1,
                                      "kind": "reference"}
+    return res
+
+
+def _events_ms(torch, stream, fn, reps):
+    """Median of reps timed calls (HIP events on the launch stream) after one warm-up."""
+    ms = []
+    for i in range(reps + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        b.synchronize()
+        if i:
+            ms.append(a.elapsed_time(b))
+    return statistics.median(ms)
+
+
+def load_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
+    """SURVEY 8(f) row 1, the load path: config 3's table (4 int32 columns of n rows,
+    seeds 42..45) as CSV text in HBM (mq_format_csv_int32, "v,v,v,v\n" rows), then
+    load_db's data loop on the GPU: mq_csv_count_rows + mq_csv_parse_int32 (events).
+    Parity: every parsed column equals its source. CPU: the reference's own load_db
+    (oracle/_ref/libdbm.so) on the first 2M rows of the same text."""
+    import numpy as np
+    sp = mq.stream_of(stream)
+    ncols = 4
+    with torch.cuda.stream(stream):
+        cols = [col] + [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(ncols - 1)]
+        for j in range(1, ncols):
+            mq.check(lib.mq_gen_uniform(cols[j].data_ptr(), n, 42 + j, n, sp), "gen")
+        fws = torch.empty(lib.mq_format_csv_workspace_bytes(n, ncols), dtype=torch.uint8, device=dev)
+        text = torch.empty(n * ncols * 11 + 16, dtype=torch.uint8, device=dev)
+        ptrs = (C.c_void_p * ncols)(*[c.data_ptr() for c in cols])
+        nb = C.c_uint64()
+        mq.check(lib.mq_format_csv_int32(ptrs, ncols, n, text.data_ptr(), C.byref(nb), fws.data_ptr(),
+                                         fws.numel(), sp), "format_csv")
+        del fws
+        tb = nb.value
+        ws = torch.empty(lib.mq_csv_workspace_bytes(tb, ncols), dtype=torch.uint8, device=dev)
+        outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(ncols)]
+        optrs = (C.c_void_p * ncols)(*[o.data_ptr() for o in outs])
+        mm = torch.empty(2 * ncols, dtype=torch.int32, device=dev)
+        rows = C.c_uint64()
+        count = lambda: mq.check(lib.mq_csv_count_rows(text.data_ptr(), tb, ncols, C.byref(rows),  # noqa: E731
+                                                       ws.data_ptr(), ws.numel(), sp), "csv_count")
+        parse = lambda: mq.check(lib.mq_csv_parse_int32(text.data_ptr(), tb, ncols, optrs, rows.value,  # noqa: E731
+                                                        mm.data_ptr(), ws.data_ptr(), ws.numel(), sp),
+                                 "csv_parse")
+        ms_count = _events_ms(torch, stream, count, 3)
+        ms_parse = _events_ms(torch, stream, parse, 3)
+        ok = rows.value == n and all(torch.equal(o, c) for o, c in zip(outs, cols))
+        sample = None
+        head = text[: min(tb, 2_000_000 * ncols * 11)].cpu().numpy().tobytes()
+        del outs, ws, text, cols[1:]
+    t = (ms_count + ms_parse) * 1e-3
+    res = {"rows": n, "ncols": ncols, "text_bytes": tb, "ms_count": ms_count, "ms_parse": ms_parse,
+           "rows_per_s": n / t, "text_gbs": tb / t / 1e9,
+           "hbm_bytes_design": 2 * tb + 4 * n * ncols,
+           "gbs_design": (2 * tb + 4 * n * ncols) / t / 1e9, "parity": bool(ok),
+           "note": "count pass (streaming '\\n' count, 1 read of the text) + parse pass (LDS-staged, "
+                   "SWAR tokens, 1 read + 4 B per cell written)"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refload  # the reference's load_db, baseline only
+    if cpu and refload.have():
+        import tempfile
+        cut = head.rfind(b"\n", 0, len(head)) + 1
+        sample = head[:cut]
+        srows = sample.count(b"\n")
+        with tempfile.TemporaryDirectory() as tmp:
+            path = os.path.join(tmp, "t.csv")
+            with open(path, "wb") as f:
+                f.write((",".join(f"db.tbl.c{j}" for j in range(ncols)) + "\n").encode() + sample)
+            r = refload.load(path, ncols)
+        res["cpu_reference"] = {"rows": srows, "s": r["load_s"], "rows_per_s": srows / r["load_s"],
+                                "cores": 1, "kind": "reference",
+                                "what": "load_db + insert_row (libdbm.so, gcc -O2), incl. table growth"}
+    return res
+
+
+def index_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
+    """the sorted index of the 1e9-row column (mq_index_build:
+    stable radix sort of (value, row) -> values + size_t positions). Parity: gather
+    through the positions reproduces the values (and they ascend). CPU: the
+    reference's quicksort (index.c:25-46, libdbm.so) on 1e6 rows of the same column."""
+    import numpy as np
+    sp = mq.stream_of(stream)
+    with torch.cuda.stream(stream):
+        v = torch.empty(n, dtype=torch.int32, device=dev)
+        p = torch.empty(n, dtype=torch.int64, device=dev)
+        ms = _events_ms(torch, stream, lambda: mq.check(
+            lib.mq_index_build(col.data_ptr(), n, v.data_ptr(), p.data_ptr(), sp), "index_build"), 2)
+        g = torch.empty(n, dtype=torch.int32, device=dev)
+        mq.check(lib.mq_gather_u64(col.data_ptr(), p.data_ptr(), n, g.data_ptr(), sp))
+        ok = bool(torch.equal(g, v)) and bool((v[1:] >= v[:-1]).all())
+        del v, p, g
+    res = {"rows": n, "ms": ms, "rows_per_s": n / (ms * 1e-3), "parity": ok,
+           "hbm_bytes_design": 4 * 20 * n,
+           "note": "4 LSD passes of 8 bits: histogram (4N read) + scatter (8N read + 8N write) each, "
+                   "+ key flip and emit"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refload  # the reference's quicksort, baseline only
+    if cpu and refload.have():
+        k = 1_000_000
+        vals = col[:k].cpu().numpy().astype(np.int32).copy()
+        pos = np.arange(k, dtype=np.uint64)
+        L = C.CDLL(refload.LIBDBM)
+        L.quicksort.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        t0 = time.perf_counter()
+        L.quicksort(vals.ctypes.data, pos.ctypes.data, 0, k - 1)
+        tq = time.perf_counter() - t0
+        res["cpu_reference"] = {"rows": k, "s": tq, "rows_per_s": k / tq, "cores": 1,
+                                "kind": "reference", "what": "quicksort (index.c:25-46, libdbm.so -O2)"}
     return res
 
 

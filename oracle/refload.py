@@ -89,7 +89,10 @@ def run(csv_path: str, ncols: int, index_spec: str = "") -> dict:
         for j, clustered in spec:
             L.create_index(C.pointer(tbl.contents.columns[j]), clustered, True, C.byref(s))
         s = Status()
+        import time
+        t0 = time.perf_counter()
         L.load_db(db, csv_path.encode(), C.byref(s))
+        load_s = time.perf_counter() - t0
         if spec and s.code == 0:
             L.build_index(db)
         t = tbl.contents
@@ -102,7 +105,7 @@ def run(csv_path: str, ncols: int, index_spec: str = "") -> dict:
                 cols[j] = np.ctypeslib.as_array(c.data, shape=(rows,))
             mm[j] = (c.min, c.max)
         out = {"code": int(s.code), "rows": rows, "table_length": int(t.table_length),
-               "cols": cols, "minmax": mm}
+               "cols": cols, "minmax": mm, "load_s": np.float64(load_s)}
         for j, clustered in spec:
             c = t.columns[j]
             ix = C.cast(c.index, C.POINTER(ColumnIndex)).contents
@@ -123,7 +126,7 @@ def load(csv_path: str, ncols: int, index_spec: str = "") -> dict:
         subprocess.run([sys.executable, os.path.abspath(__file__), os.path.abspath(csv_path),
                         str(ncols), out, index_spec], check=True, stdout=subprocess.DEVNULL)
         z = np.load(out)
-        return {k: (z[k] if z[k].ndim else int(z[k])) for k in z.files}
+        return {k: (z[k] if z[k].ndim else z[k].item()) for k in z.files}
 
 
 if __name__ == "__main__":
