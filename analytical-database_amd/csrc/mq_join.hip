@@ -140,11 +140,28 @@ int scan_exclusive(const Tin* in, u64* out, uint64_t n, u64* scratch, hipStream_
 }
 
 // ---------------------------------------------------------------------------
-// stable LSD radix sort of (u32 key, u32 value), 8-bit digits
+// stable LSD radix sort of packed words {key ^ 2^31 (low 32), value (high 32)},
+// 8-bit digits. Per 4096-word tile: an LDS histogram (k_sortw_hist), an exclusive
+// scan over (digit, tile), then a scatter that ranks equal digits with 8 wave
+// ballots (stable) and stages the tile in LDS, so every digit run leaves the block
+// as contiguous stores. (Element-by-element scatter measured 0.5 TB/s at 1e9 rows.)
+// FIRST: the words are built from the int32 keys (and values, or row ids).
+// LAST : the sorted words are written split into key and value arrays.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kTPB) void k_sort_hist(const uint32_t* __restrict__ keys, uint64_t n,
-                                                    int shift, uint32_t* __restrict__ hist,
-                                                    uint32_t ntiles) {
+template <bool FIRST>
+__device__ __forceinline__ u64 sort_word(const int* c1, const int* p1, const u64* in, uint64_t i) {
+    if constexpr (FIRST) {
+        const uint32_t v = p1 ? (uint32_t)p1[i] : (uint32_t)i;
+        return (u64)((uint32_t)c1[i] ^ 0x80000000u) | ((u64)v << 32);
+    } else {
+        return in[i];
+    }
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1, const u64* __restrict__ in,
+                                                     uint64_t n, int shift, uint32_t* __restrict__ hist,
+                                                     uint32_t ntiles) {
     __shared__ uint32_t h[kRadix];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -152,38 +169,42 @@ __global__ __launch_bounds__(kTPB) void k_sort_hist(const uint32_t* __restrict__
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
-        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 0xFF], 1u);
+        if (i < n) {
+            const uint32_t key = FIRST ? ((uint32_t)c1[i] ^ 0x80000000u) : (uint32_t)in[i];
+            atomicAdd(&h[(key >> shift) & 0xFF], 1u);
+        }
     }
     __syncthreads();
     hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Tile = 4 waves x 16 items x 64 lanes; wave w owns tile rows [w*1024, (w+1)*1024),
-// item k of lane l is row w*1024 + k*64 + l, so (w, k, l) order = input order.
-// Within a wave, equal digits are ranked with 8 ballots (stable); per-wave digit
-// counters in LDS carry the rank across items; a per-digit prefix over the 4
-// waves and the global offset of (digit, tile) give the destination.
-__global__ __launch_bounds__(kTPB) void k_sort_scatter(const uint32_t* __restrict__ kin,
-                                                       const uint32_t* __restrict__ vin,
-                                                       uint32_t* __restrict__ kout,
-                                                       uint32_t* __restrict__ vout, uint64_t n,
-                                                       int shift, const u64* __restrict__ goff,
-                                                       uint32_t ntiles) {
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
+                                                        const u64* __restrict__ in, uint64_t n, int shift,
+                                                        const u64* __restrict__ goff, uint32_t ntiles,
+                                                        u64* __restrict__ out, uint32_t* __restrict__ kout,
+                                                        uint32_t* __restrict__ vout) {
     __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    __shared__ uint32_t loff[kRadix];
+    __shared__ u64 gofs[kRadix];
+    __shared__ u64 stage[kSortTile];
+    __shared__ uint32_t wsum[kTPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    gofs[tid] = goff[(uint64_t)tid * ntiles + blockIdx.x];
     __syncthreads();
-    const uint64_t seg = (uint64_t)blockIdx.x * kSortTile + (uint64_t)wave * (64 * kSortItems);
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint32_t key[kSortItems], val[kSortItems], dr[kSortItems];
+    u64 el[kSortItems];
+    uint32_t dr[kSortItems];
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool valid = i < n;
-        key[k] = valid ? kin[i] : 0u;
-        val[k] = valid ? vin[i] : 0u;
-        const uint32_t d = (key[k] >> shift) & 0xFF;
+        el[k] = valid ? sort_word<FIRST>(c1, p1, in, i) : 0ull;
+        const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
         u64 peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -196,27 +217,50 @@ __global__ __launch_bounds__(kTPB) void k_sort_scatter(const uint32_t* __restric
         __builtin_amdgcn_wave_barrier();
         if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
         __builtin_amdgcn_wave_barrier();
-        dr[k] = (d << 16) | (cur + lt);
+        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    {  // exclusive prefix of the per-wave counts, per digit (thread tid = digit)
-        uint32_t off = 0;
+    uint32_t tot = 0;
 #pragma unroll
-        for (int w = 0; w < kTPB / 64; w++) {
-            const uint32_t c = wcnt[w][tid];
-            wcnt[w][tid] = off;
-            off += c;
-        }
+    for (int w = 0; w < kTPB / 64; w++) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = tot;
+        tot += c;
     }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t excl = incl - tot;
+    for (int w = 0; w < wave; w++) excl += wsum[w];
+    loff[tid] = excl;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        if (i < n) {
+        if (dr[k] != 0xFFFFFFFFu) {
             const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
-            const u64 dest = goff[(uint64_t)d * ntiles + blockIdx.x] + wcnt[wave][d] + r;
-            kout[dest] = key[k];
-            vout[dest] = val[k];
+            stage[loff[d] + wcnt[wave][d] + r] = el[k];
+        }
+    }
+    __syncthreads();
+    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t e = (uint32_t)(k * kTPB + tid);
+        if (e < tn) {
+            const u64 v = stage[e];
+            const uint32_t d = ((uint32_t)v >> shift) & 0xFF;
+            const u64 dst = gofs[d] + (e - loff[d]);
+            if constexpr (LAST) {
+                kout[dst] = (uint32_t)v;
+                vout[dst] = (uint32_t)(v >> 32);
+            } else {
+                out[dst] = v;
+            }
         }
     }
 }
@@ -353,7 +397,7 @@ __global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
     hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter (k_sort_scatter's ballot ranking), staged through LDS so that each
+// Stable scatter (k_sortw_scatter's ballot ranking), staged through LDS so that each
 // digit's run leaves the block as contiguous, coalesced stores.
 template <bool FROM_COLS>
 __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1,
@@ -548,18 +592,6 @@ __global__ __launch_bounds__(kTPB) void k_ht_set_len(const uint32_t* __restrict_
     }
 }
 
-__global__ __launch_bounds__(kTPB) void k_iota_u32(uint64_t n, uint32_t* __restrict__ out) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] = (uint32_t)i;
-}
-
-__global__ __launch_bounds__(kTPB) void k_flip_keys(const int* __restrict__ in, uint64_t n,
-                                                    uint32_t* __restrict__ out) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
-        out[i] = (uint32_t)in[i] ^ 0x80000000u;
-}
-
 __global__ __launch_bounds__(kTPB) void k_ht_probe(const int* __restrict__ pkeys, uint64_t n2,
                                                    const u64* words,
                                                    const uint32_t* __restrict__ start,
@@ -731,61 +763,66 @@ namespace mqi {
 
 int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out,
                      uint32_t** vals_out, hipStream_t st, const DevState* s) {
-    // buffers: keys/vals double buffers, histogram, its scan, scan scratch
-    uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *hist = nullptr;
-    u64 *hscan = nullptr, *scratch = nullptr;
+    // packed {key ^ 2^31, value} words double-buffered; the last pass writes the
+    // split outputs; histogram + its scan + scan scratch
+    u64 *w0 = nullptr, *w1 = nullptr, *hscan = nullptr, *scratch = nullptr;
+    uint32_t *ko = nullptr, *vo = nullptr, *hist = nullptr;
     const uint64_t ntiles = ceil_div(n, kSortTile);
     const uint64_t nh = ntiles * kRadix;
-    auto fail = [&](int rc) {
-        pool_free(k1);
-        pool_free(v1);
+    auto release = [&]() {
+        pool_free(w0);
+        pool_free(w1);
         pool_free(hist);
         pool_free(hscan);
         pool_free(scratch);
-        pool_free(k0);
-        pool_free(v0);
+    };
+    auto fail = [&](int rc) {
+        release();
+        pool_free(ko);
+        pool_free(vo);
         return rc;
     };
-    k0 = (uint32_t*)pool_alloc(n * 4);
-    v0 = (uint32_t*)pool_alloc(n * 4);
-    k1 = (uint32_t*)pool_alloc(n * 4);
-    v1 = (uint32_t*)pool_alloc(n * 4);
+    if (n == 0) {
+        *keys_out = (uint32_t*)pool_alloc(16);
+        *vals_out = (uint32_t*)pool_alloc(16);
+        return MQ_OK;
+    }
+    w0 = (u64*)pool_alloc(n * 8);
+    w1 = (u64*)pool_alloc(n * 8);
+    ko = (uint32_t*)pool_alloc(n * 4);
+    vo = (uint32_t*)pool_alloc(n * 4);
     hist = (uint32_t*)pool_alloc(nh * 4);
     hscan = (u64*)pool_alloc(nh * 8);
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
-    if (!k0 || !v0 || !k1 || !v1 || !hist || !hscan || !scratch)
+    if (!w0 || !w1 || !ko || !vo || !hist || !hscan || !scratch)
         return fail(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
-    hipLaunchKernelGGL(k_flip_keys, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, n, k0);
-    if (p1) {
-        if (hipMemcpyAsync(v0, p1, n * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-            return fail(set_err(MQ_EHIP, "sort: copy values"));
-    } else {
-        hipLaunchKernelGGL(k_iota_u32, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, n, v0);
-    }
+    const dim3 g((uint32_t)ntiles), b(kTPB);
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
-        hipLaunchKernelGGL(k_sort_hist, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, n, shift,
-                           hist, (uint32_t)ntiles);
+        if (pass == 0)
+            hipLaunchKernelGGL((k_sortw_hist<true>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
+        else
+            hipLaunchKernelGGL((k_sortw_hist<false>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return fail(rc);
-        hipLaunchKernelGGL(k_sort_scatter, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, k0, v0, k1,
-                           v1, n, shift, hscan, (uint32_t)ntiles);
+        if (pass == 0)
+            hipLaunchKernelGGL((k_sortw_scatter<true, false>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan,
+                               (uint32_t)ntiles, w1, nullptr, nullptr);
+        else if (pass < 3)
+            hipLaunchKernelGGL((k_sortw_scatter<false, false>), g, b, 0, st, nullptr, nullptr, w0, n, shift,
+                               hscan, (uint32_t)ntiles, w1, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_sortw_scatter<false, true>), g, b, 0, st, nullptr, nullptr, w0, n, shift,
+                               hscan, (uint32_t)ntiles, nullptr, ko, vo);
         if (hipGetLastError() != hipSuccess) return fail(set_err(MQ_EHIP, "sort: launch"));
-        uint32_t* t = k0;
-        k0 = k1;
-        k1 = t;
-        t = v0;
-        v0 = v1;
-        v1 = t;
+        u64* t = w0;
+        w0 = w1;
+        w1 = t;
     }
     if (hipStreamSynchronize(st) != hipSuccess) return fail(set_err(MQ_EHIP, "sort: sync"));
-    pool_free(k1);
-    pool_free(v1);
-    pool_free(hist);
-    pool_free(hscan);
-    pool_free(scratch);
-    *keys_out = k0;
-    *vals_out = v0;
+    release();
+    *keys_out = ko;
+    *vals_out = vo;
     return MQ_OK;
 }
 
