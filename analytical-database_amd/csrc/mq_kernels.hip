@@ -1196,6 +1196,120 @@ __global__ __launch_bounds__(kTPB) void k_gen_uniform(int* __restrict__ out, uin
         out[i] = (int)(sm64(base + i) % modulus);
 }
 
+// ---------------------------------------------------------------------------
+// k_scan_gather: config 3 fused (select col -> fetch aux -> agg; query.c:92-137,
+// 223-243, 306-354) with the gather deferred. k_scan<kAux> loads aux[row] inline at
+// each match, so every tile with a match waits a full random-read latency before
+// the next tile's loads go out. Here the scan streams like k_scan<kSum> (8 tiles of
+// nt dwordx4 in flight) and each wave appends its matching rows (as offsets from
+// the block's first row) to a 1024-entry LDS buffer, ranked with 4 ballots +
+// mbcnt. When a tile would overflow the buffer, and at the end, the wave drains it:
+// 8 independent aux loads per lane in flight, folded into count/sum/min/max. The
+// same aggregates as k_scan<kAux>, in the same partial slab and in-kernel combine.
+// ---------------------------------------------------------------------------
+constexpr int kGBuf = 1024;
+
+template <bool VEC>
+__global__ __launch_bounds__(kTPB, 6) void k_scan_gather(const int* __restrict__ col,
+                                                         const int* __restrict__ aux, uint64_t n,
+                                                         uint64_t rows_per_block, Pred pred,
+                                                         Partial* __restrict__ part,
+                                                         mq_agg* __restrict__ out, uint32_t slot) {
+    __shared__ uint32_t s_buf[kWaves][kGBuf];
+    const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
+    uint64_t end = start + rows_per_block;
+    if (end > n) end = n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t lo = pred.lo, wm1 = pred.wm1;
+    uint32_t* buf = s_buf[wave];
+    const int* auxb = aux + start;
+    uint32_t fill = 0;  // wave-uniform
+    unsigned long long cnt = 0;
+    long long sumv = 0;
+    int mnv = INT_MAX, mxv = INT_MIN;
+
+    auto drain = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i0 = 0; i0 < fill; i0 += 64u * 8u) {
+            int x[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t i = i0 + (uint32_t)j * 64u + (uint32_t)lane;
+                x[j] = i < fill ? auxb[buf[i]] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t i = i0 + (uint32_t)j * 64u + (uint32_t)lane;
+                if (i < fill) {
+                    sumv += x[j];
+                    mnv = min(mnv, x[j]);
+                    mxv = max(mxv, x[j]);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        fill = 0;
+    };
+    auto consume = [&](int4 v, uint64_t tile_row, bool full) {
+        const uint64_t row = tile_row + (uint64_t)tid * 4;
+        bool p0 = ((uint32_t)v.x - lo) <= wm1, p1 = ((uint32_t)v.y - lo) <= wm1,
+             p2 = ((uint32_t)v.z - lo) <= wm1, p3 = ((uint32_t)v.w - lo) <= wm1;
+        if (!full) {
+            p0 = p0 && row + 0 < end;
+            p1 = p1 && row + 1 < end;
+            p2 = p2 && row + 2 < end;
+            p3 = p3 && row + 3 < end;
+        }
+        const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
+                                 m3 = __ballot(p3);
+        const uint32_t c = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3)));
+        if (c == 0) return;
+        cnt += c;
+        if (fill + c > (uint32_t)kGBuf) drain();
+        uint32_t k = rank_lt(m3, rank_lt(m2, rank_lt(m1, rank_lt(m0, fill))));
+        const uint32_t r = (uint32_t)(row - start);
+        if (p0) buf[k++] = r + 0;
+        if (p1) buf[k++] = r + 1;
+        if (p2) buf[k++] = r + 2;
+        if (p3) buf[k++] = r + 3;
+        fill = __builtin_amdgcn_readfirstlane(fill + c);
+    };
+
+    constexpr int U = 8;
+    uint64_t t = start;
+    for (; t + (uint64_t)U * kTileRows <= end; t += (uint64_t)U * kTileRows) {
+        int4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
+#pragma unroll
+        for (int u = 0; u < U; u++) consume(v[u], t + (uint64_t)u * kTileRows, true);
+    }
+    for (; t < end; t += kTileRows) {
+        const uint64_t row = t + (uint64_t)tid * 4;
+        int4 v;
+        if (row + 3 < end) {
+            v = load4_nt<VEC>(col + row);
+        } else {
+            v.x = row + 0 < end ? col[row + 0] : 0;
+            v.y = row + 1 < end ? col[row + 1] : 0;
+            v.z = row + 2 < end ? col[row + 2] : 0;
+            v.w = row + 3 < end ? col[row + 3] : 0;
+        }
+        consume(v, t, row + 3 < end);
+    }
+    drain();
+    // cnt is wave-uniform: count it once per wave (lane 0) in the block sum
+    const unsigned long long c_lane = lane == 0 ? cnt : 0ull;
+    if (out) {
+        block_store_partial<true>(c_lane, sumv, mnv, mxv, part);
+        if (block_arrive_last(gridDim.x, slot)) block_combine(part, gridDim.x, out);
+    } else {
+        block_store_partial(c_lane, sumv, mnv, mxv, part);
+    }
+}
+
 __global__ __launch_bounds__(kTPB) void k_gen_join(int* __restrict__ out, uint64_t n, int kind) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     const uint64_t mask = 2 * n - 1;
@@ -1403,6 +1517,25 @@ int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Part
     return MQ_OK;
 }
 
+// Launch k_scan_gather (config 3 fused, deferred gather) with the partials folded
+// in-kernel into *out.
+int launch_gather(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
+                  mq_agg* out, hipStream_t st, const DevState* s) {
+    static std::atomic<uint32_t> next_slot{0};
+    const uint32_t slot = next_slot.fetch_add(1, std::memory_order_relaxed) % kArriveSlots;
+    const bool vec = aligned16(col);
+    const void* fn = vec ? (const void*)&k_scan_gather<true> : (const void*)&k_scan_gather<false>;
+    uint32_t g;
+    uint64_t rpb;
+    geometry(s, n, fn, &g, &rpb);
+    if (vec)
+        hipLaunchKernelGGL((k_scan_gather<true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, slot);
+    else
+        hipLaunchKernelGGL((k_scan_gather<false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, slot);
+    LAUNCHCHK("k_scan_gather");
+    return MQ_OK;
+}
+
 size_t mask_bytes(uint64_t n) {  // 1 KiB (4 waves x 256 B) per 8192-row super-tile
     return (size_t)((n + 8 * kTileRows - 1) / (8 * kTileRows)) * kWaves * 32 * sizeof(unsigned long long);
 }
@@ -1427,8 +1560,11 @@ int run_agg(const int32_t* col, const int32_t* aux, uint64_t n, Pred pred, mq_ag
         return set_err(MQ_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, partial_bytes());
     Partial* part = static_cast<Partial*>(d_ws);
     uint32_t g;
-    return aux ? launch_scan<kAux>(col, aux, n, pred, part, d_out, st, s, &g)
-               : launch_scan<kAgg>(col, nullptr, n, pred, part, d_out, st, s, &g);
+    if (!aux) return launch_scan<kAgg>(col, nullptr, n, pred, part, d_out, st, s, &g);
+    // MQ_AUX_IMPL=inline keeps k_scan<kAux> (gather at each match) for A/B
+    const char* e = getenv("MQ_AUX_IMPL");
+    if (e && strcmp(e, "inline") == 0) return launch_scan<kAux>(col, aux, n, pred, part, d_out, st, s, &g);
+    return launch_gather(col, aux, n, pred, part, d_out, st, s);
 }
 
 // Ordered compaction implementations (MQ_POSITIONS_IMPL, read per call):

@@ -399,7 +399,8 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
         out["config3_fused"] = {
             "ms": t_fused, "rows_per_s": n / (t_fused * 1e-3), "parity": fused_ok,
             "algorithmic_bytes": 4 * n + 8 * k,
-            "note": "select col0 + gather col1 at matches, one kernel"}
+            "note": "select col0 + gather col1 at matches, one kernel (k_scan_gather: matches "
+                    "staged per wave in LDS, gathered 8 loads in flight per lane)"}
         del pos, col1, vals
     out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
