@@ -17,8 +17,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "mq_common.h"
 #include "mq_device.h"
@@ -187,6 +192,229 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Many queries (q >= kEiMinQ): elementary intervals. The 2q query bounds cut the
+// int32 line into m+1 <= 2q+1 "elementary intervals" (EIs); every value lies in
+// exactly one, e(v) = #{bounds <= v}, and query i covers the EIs [ea_i, eb_i).
+// e(v) comes from a 4096-bucket table over [bmin, bmax] (each entry: the EI range
+// [e0, e1] its values can fall in; one LDS read when the bucket holds no bound,
+// a binary search over its few bounds otherwise).
+//   count: per wave-chunk, an LDS histogram of e over the covered rows; query i's
+//          count = P[eb_i] - P[ea_i] from the histogram's prefix. Cost per row: the
+//          lookup, not q compares.
+//   write: per 256-row wave-tile, the (query, row) pairs of its covered rows
+//          (query lists per EI, CSR) are listed in LDS in row order; a pair's rank
+//          among earlier pairs of its query (one broadcast LDS read per pair of
+//          the tile) gives its slot after the query's running offset. Tiles with
+//          many pairs (dense queries) take the per-query ballot loop instead.
+// ---------------------------------------------------------------------------
+constexpr int kEiMinQ = 24;
+constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
+constexpr int kBuckets = 4096;
+constexpr int kPairCap = 512;
+
+struct EiMeta {
+    int m;          // number of bounds
+    int shift;      // bucket width 2^shift
+    int bmin, bmax; // first / last bound
+};
+
+struct EiTables {  // device copies, filled by the host (ss_count)
+    const int32_t* bounds;      // m sorted bounds
+    const uint32_t* bucket;     // kBuckets x {e0 (low 16), e1 (high 16)}
+    const uint32_t* qoff;       // m + 2: CSR offsets of the per-EI query lists
+    const uint16_t* qlist;      // queries covering each EI, ascending
+    const uint32_t* qab;        // per query: ea (low 16) | eb (high 16)
+};
+
+__device__ __forceinline__ int ei_of(int32_t v, const EiMeta& M, const uint32_t* s_bkt,
+                                     const int32_t* s_b) {
+    if (v < M.bmin) return 0;
+    if (v > M.bmax) return M.m;
+    const uint32_t ent = s_bkt[((uint32_t)v - (uint32_t)M.bmin) >> M.shift];
+    int lo = (int)(ent & 0xFFFFu), hi = (int)(ent >> 16);  // e(v) in [lo, hi]
+    while (lo < hi) {  // first j in [lo, hi) with bound[j] > v, else hi
+        const int mid = (lo + hi) >> 1;
+        if (s_b[mid] <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_ssi_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
+                                                    EiMeta M, EiTables T, int q,
+                                                    uint32_t* __restrict__ counts, uint64_t nwc) {
+    __shared__ uint32_t s_bkt[kBuckets];
+    __shared__ int32_t s_b[kEiMax];
+    __shared__ uint32_t s_qoff[kEiMax];
+    __shared__ uint32_t hist[kWaves][kEiMax];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < kBuckets; i += kTPB) s_bkt[i] = T.bucket[i];
+    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
+    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
+    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    uint64_t s, e;
+    wave_chunk(n, rpb, wave, &s, &e);
+    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
+        int4 v[kSsUnroll];
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++)
+            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++) {
+            const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
+            const int x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (row + k < e) {
+                    const int ei = ei_of(x[k], M, s_bkt, s_b);
+                    if (s_qoff[ei + 1] > s_qoff[ei]) atomicAdd(&hist[wave][ei], 1u);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // exclusive prefix over the m+1 EIs, in place (P[m+1] = total): this wave only
+    uint32_t* h = hist[wave];
+    const int ne = M.m + 2;
+    const int per = (ne + 63) / 64;
+    uint32_t loc = 0;
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) loc += h[j];
+    }
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    uint32_t run = incl - loc;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) {
+            const uint32_t c = h[j];
+            h[j] = run;
+            run += c;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    for (int i = lane; i < q; i += 64) {
+        const uint32_t ab = T.qab[i];
+        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col, uint64_t n, uint64_t rpb,
+                                                    EiMeta M, EiTables T, const Pred* __restrict__ preds,
+                                                    int q, const unsigned long long* __restrict__ offs,
+                                                    uint64_t nwc, int* const* __restrict__ outs) {
+    __shared__ uint32_t s_bkt[kBuckets];
+    __shared__ int32_t s_b[kEiMax];
+    __shared__ uint32_t s_qoff[kEiMax];
+    __shared__ unsigned long long run[kWaves][kMaxQ];
+    __shared__ uint32_t pairs[kWaves][kPairCap];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int i = tid; i < kBuckets; i += kTPB) s_bkt[i] = T.bucket[i];
+    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
+    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
+    for (int i = tid; i < q; i += kTPB) {
+        const unsigned long long base = offs[(uint64_t)i * nwc];
+#pragma unroll
+        for (int w = 0; w < kWaves; w++)
+            run[w][i] = offs[(uint64_t)i * nwc + (uint64_t)blockIdx.x * kWaves + w] - base;
+    }
+    __syncthreads();
+    // tiles with more pairs than this take the per-query ballot loop (cost ~ 12 q)
+    int cap = (int)sqrtf(768.0f * (float)q);
+    if (cap > kPairCap) cap = kPairCap;
+    uint64_t s, e;
+    wave_chunk(n, rpb, wave, &s, &e);
+    uint32_t* pl = pairs[wave];
+    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
+        int4 v[kSsUnroll];
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++)
+            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++) {
+            const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
+            const int x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t qa[4], qn[4];
+            uint32_t np = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                qa[k] = 0;
+                qn[k] = 0;
+                if (row + k < e) {
+                    const int ei = ei_of(x[k], M, s_bkt, s_b);
+                    qa[k] = s_qoff[ei];
+                    qn[k] = s_qoff[ei + 1] - qa[k];
+                }
+                np += qn[k];
+            }
+            uint32_t incl = np;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t tot = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+            if (tot == 0) continue;
+            if (tot > (uint32_t)cap) {
+                // dense tile: every query's ballot, as k_ss_write
+                for (int j = 0; j < q; j++) {
+                    const Pred p = preds[j];
+                    unsigned long long o = run[wave][j];
+                    const uint32_t b = match4(v[u], p, row, e);
+                    ss_emit(outs[j], o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
+                            __ballot(b & 8u), lane, ltmask);
+                    if (lane == 0) run[wave][j] = o;
+                }
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+            // list the pairs in row order: (query << 16) | row offset in the wave-tile
+            uint32_t at = incl - np;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                for (uint32_t i = 0; i < qn[k]; i++) pl[at++] = ((uint32_t)T.qlist[qa[k] + i] << 16) | (uint32_t)(lane * 4 + k);
+            __builtin_amdgcn_wave_barrier();
+            // rank of each pair among earlier pairs of its query; the last pair of a
+            // query advances that query's running offset
+            const uint64_t tile0 = t + (uint64_t)u * kWaveTile;
+            for (uint32_t i0 = 0; i0 < tot; i0 += 64) {
+                const uint32_t i = i0 + (uint32_t)lane;
+                const uint32_t me = i < tot ? pl[i] : 0xFFFFFFFFu;
+                const uint32_t mq = me >> 16;
+                uint32_t rank = 0;
+                bool later = false;
+                for (uint32_t j = 0; j < tot; j++) {  // broadcast read
+                    const uint32_t oq = pl[j] >> 16;
+                    if (oq == mq) {
+                        rank += j < i ? 1u : 0u;
+                        later = later || j > i;
+                    }
+                }
+                unsigned long long base = 0;
+                if (i < tot) {
+                    base = run[wave][mq];
+                    outs[mq][base + rank] = (int)(tile0 + (me & 0xFFFFu));
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (i < tot && !later) run[wave][mq] = base + rank + 1;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+}
+
 // totals[j] = offs[j*nwc + nwc-1] + counts[j*nwc + nwc-1] - offs[j*nwc]
 __global__ void k_ss_totals(const uint32_t* __restrict__ counts,
                             const unsigned long long* __restrict__ offs, uint64_t nwc, int q,
@@ -200,8 +428,14 @@ __global__ void k_ss_totals(const uint32_t* __restrict__ counts,
 }
 
 struct SsLayout {
-    size_t preds, outs, slot, counts, offs, scratch, total;
+    size_t preds, outs, slot, counts, offs, scratch, ei, total;
 };
+
+// EI tables in the workspace: bounds, bucket table, qoff, qab, then qlist
+constexpr size_t kEiBoundsB = (size_t)kEiMax * 4, kEiBucketB = (size_t)kBuckets * 4,
+                 kEiQoffB = (size_t)kEiMax * 4, kEiQabB = (size_t)kMaxQ * 4,
+                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2;
+constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiQlistB;
 
 SsLayout ss_layout(uint64_t nwc, int q) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -219,6 +453,8 @@ SsLayout ss_layout(uint64_t nwc, int q) {
     at += al((size_t)q * nwc * sizeof(unsigned long long));
     L.scratch = at;
     at += al((size_t)scan_u32_scratch_elems((uint64_t)q * nwc) * sizeof(unsigned long long));
+    L.ei = at;
+    at += al(kEiBytes);
     L.total = at;
     return L;
 }
@@ -238,7 +474,83 @@ struct SsState {
     int q, qk;
     uint64_t n;
     const int32_t* col;
+    bool ei;    // elementary-interval kernels (qk >= kEiMinQ)
+    EiMeta meta;
 };
+
+// Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
+// the bucket table, written to the workspace's EI region (ss_layout).
+int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, hipStream_t st) {
+    std::vector<long long> L(qk), H(qk), b;
+    b.reserve(2 * qk);
+    for (int i = 0; i < qk; i++) {
+        L[i] = (long long)(int32_t)hp[i].lo;
+        H[i] = L[i] + (long long)hp[i].wm1;
+        b.push_back(L[i]);
+        if (H[i] + 1 <= (long long)INT32_MAX) b.push_back(H[i] + 1);
+    }
+    std::sort(b.begin(), b.end());
+    b.erase(std::unique(b.begin(), b.end()), b.end());
+    const int m = (int)b.size();
+    auto eof = [&](long long x) { return (int)(std::upper_bound(b.begin(), b.end(), x) - b.begin()); };
+    static thread_local int32_t hb[kEiMax];
+    static thread_local uint32_t hbkt[kBuckets], hqoff[kEiMax], hqab[kMaxQ];
+    static thread_local uint16_t hql[(size_t)kEiMax * kMaxQ];
+    for (int j = 0; j < m; j++) hb[j] = (int32_t)b[j];
+    std::vector<int> ea(qk), eb(qk);
+    for (int i = 0; i < qk; i++) {
+        ea[i] = eof(L[i]);
+        eb[i] = eof(H[i]) + 1;
+        hqab[i] = (uint32_t)ea[i] | ((uint32_t)eb[i] << 16);
+    }
+    uint32_t at = 0;
+    for (int e = 0; e <= m; e++) {
+        hqoff[e] = at;
+        for (int i = 0; i < qk; i++)
+            if (ea[i] <= e && e < eb[i]) hql[at++] = (uint16_t)i;
+    }
+    hqoff[m + 1] = at;
+    const long long bmin = b[0], bmax = b[m - 1];
+    int shift = 0;
+    while (((bmax - bmin) >> shift) >= kBuckets) shift++;
+    for (int k = 0; k < kBuckets; k++) {
+        const long long lo = bmin + ((long long)k << shift);
+        if (lo > bmax) {
+            hbkt[k] = (uint32_t)m | ((uint32_t)m << 16);
+            continue;
+        }
+        long long hi = lo + (1ll << shift) - 1;
+        if (hi > bmax) hi = bmax;
+        hbkt[k] = (uint32_t)eof(lo) | ((uint32_t)eof(hi) << 16);
+    }
+    *meta = EiMeta{m, shift, (int)bmin, (int)bmax};
+    size_t o = 0;
+    HIPCHK(hipMemcpyAsync(region + o, hb, (size_t)m * 4, hipMemcpyHostToDevice, st));
+    o += kEiBoundsB;
+    HIPCHK(hipMemcpyAsync(region + o, hbkt, kEiBucketB, hipMemcpyHostToDevice, st));
+    o += kEiBucketB;
+    HIPCHK(hipMemcpyAsync(region + o, hqoff, (size_t)(m + 2) * 4, hipMemcpyHostToDevice, st));
+    o += kEiQoffB;
+    HIPCHK(hipMemcpyAsync(region + o, hqab, (size_t)qk * 4, hipMemcpyHostToDevice, st));
+    o += kEiQabB;
+    if (at) HIPCHK(hipMemcpyAsync(region + o, hql, (size_t)at * 2, hipMemcpyHostToDevice, st));
+    return MQ_OK;
+}
+
+EiTables ei_tables(char* region) {
+    EiTables T;
+    size_t o = 0;
+    T.bounds = reinterpret_cast<const int32_t*>(region + o);
+    o += kEiBoundsB;
+    T.bucket = reinterpret_cast<const uint32_t*>(region + o);
+    o += kEiBucketB;
+    T.qoff = reinterpret_cast<const uint32_t*>(region + o);
+    o += kEiQoffB;
+    T.qab = reinterpret_cast<const uint32_t*>(region + o);
+    o += kEiQabB;
+    T.qlist = reinterpret_cast<const uint16_t*>(region + o);
+    return T;
+}
 
 int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int32_t* h_highs,
              int q, uint64_t* d_totals, void* d_ws, size_t ws_bytes, hipStream_t st,
@@ -267,7 +579,9 @@ int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int3
     }
     char* w = static_cast<char*>(d_ws);
     const bool vec = aligned16(d_col);
-    const void* fn = vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>;
+    const bool ei = qk >= kEiMinQ && getenv("MQ_SS_IMPL") == nullptr;  // MQ_SS_IMPL=ballot: A/B
+    const void* fn = ei ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
+                        : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
     uint32_t g = 1;
     uint64_t rpb = kGranule;
     if (n) geometry(s, n, fn, &g, &rpb, kGranule);
@@ -275,15 +589,25 @@ int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int3
     const SsLayout L = ss_layout(nwc, qk > 0 ? qk : 1);
     HIPCHK(hipMemcpyAsync(w + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(w + L.slot, hslot, sizeof(int) * q, hipMemcpyHostToDevice, st));
+    EiMeta meta{0, 0, 0, 0};
+    if (ei && (rc = ei_build(hp, qk, w + L.ei, &meta, st))) return rc;
     HIPCHK(hipStreamSynchronize(st));  // the staging arrays are reused by the next call
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
     unsigned long long* offs = reinterpret_cast<unsigned long long*>(w + L.offs);
     if (qk > 0) {
-        if (vec)
+        if (ei) {
+            const EiTables T = ei_tables(w + L.ei);
+            if (vec)
+                hipLaunchKernelGGL(k_ssi_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
+            else
+                hipLaunchKernelGGL(k_ssi_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
+            LAUNCHCHK("k_ssi_count");
+        } else if (vec) {
             hipLaunchKernelGGL(k_ss_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc);
-        else
+        } else {
             hipLaunchKernelGGL(k_ss_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc);
+        }
         LAUNCHCHK("k_ss_count");
         if ((rc = scan_u32_exclusive(counts, offs, (uint64_t)qk * nwc,
                                      reinterpret_cast<unsigned long long*>(w + L.scratch), st)))
@@ -292,7 +616,7 @@ int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int3
     hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
                        reinterpret_cast<const int*>(w + L.slot), d_totals, q);
     LAUNCHCHK("k_ss_totals");
-    *state = SsState{g, rpb, q, qk, n, d_col};
+    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta};
     return MQ_OK;
 }
 
@@ -312,6 +636,15 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
     int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
+    if (S.ei) {
+        const EiTables T = ei_tables(w + L.ei);
+        if (aligned16(S.col))
+            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs);
+        else
+            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs);
+        LAUNCHCHK("k_ssi_write");
+        return MQ_OK;
+    }
     if (aligned16(S.col))
         hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs);
     else

@@ -208,15 +208,27 @@ def test_add_sub_vs_oracle(lib, refcpu, n):
     assert np.array_equal(out.get(np.int32, n), refcpu.sub(a, b))
 
 
-def test_fused_select_fetch_agg_vs_oracle(lib, refcpu):
-    n = 2_000_003
-    d0, d1 = refcpu.gen_uniform(n, 42), refcpu.gen_uniform(n, 43)
-    D0, D1 = Dev.of(d0), Dev.of(d1)
-    for lo, hi in ((500_000, 520_000), (None, 1000), (0, None), (5, 5)):
-        pos = refcpu.select_scan(d0, lo, hi)
-        vals = d1[pos]
-        a = _agg(lib, D0.ptr, n, lo, hi, fused_val_ptr=D1.ptr)
-        assert a.count == len(pos) and a.sum == int(vals.astype(np.int64).sum())
+@pytest.mark.parametrize("aux_impl", ["gather", "inline"])
+def test_fused_select_fetch_agg_vs_oracle(lib, refcpu, monkeypatch, aux_impl):
+    """config 3 fused: k_scan_gather (default) and k_scan<kAux> (MQ_AUX_IMPL=inline);
+    dense selections overflow the per-wave LDS buffer many times."""
+    if aux_impl == "inline":
+        monkeypatch.setenv("MQ_AUX_IMPL", "inline")
+    for n in (1, 1023, 4099, 2_000_003):
+        d0, d1 = refcpu.gen_uniform(n, 42), refcpu.gen_uniform(n, 43)
+        d1[: min(n, 3)] = [I32MIN, I32MAX, -1][: min(n, 3)]
+        for off in (0, 1):
+            D0, D1 = Dev.of(d0, offset_elems=off), Dev.of(d1, offset_elems=off)
+            for lo, hi in ((n // 4, n // 4 + n // 100 + 1), (None, n // 2), (0, None), (5, 5),
+                           (None, None)):
+                pos = refcpu.select_scan(d0, lo, hi)
+                vals = d1[pos]
+                a = _agg(lib, D0.ptr, n, lo, hi, fused_val_ptr=D1.ptr)
+                assert a.count == len(pos) and a.sum == int(vals.astype(np.int64).sum()), (n, lo, hi)
+                if len(vals):
+                    assert (a.min, a.max) == (int(vals.min()), int(vals.max())), (n, lo, hi)
+                else:
+                    assert (a.min, a.max) == (I32MAX, I32MIN)
 
 
 def test_generators_match_oracle(lib, refcpu):
@@ -650,3 +662,61 @@ def test_shared_select_vs_oracle(lib, refcpu, n, q):
         kk = dk.get(np.uint64, q)
         for j in range(q):
             assert np.array_equal(full[j].get(np.int32, int(kk[j])), want[j]), (n, q, j)
+
+
+def _shared_run(lib, d, lows, highs):
+    n, q = len(d), len(lows)
+    dd = Dev.of(d)
+    ws = Dev(lib.mq_shared_select_workspace_bytes(n, q))
+    k = (C.c_uint64 * q)()
+    lo_c = (C.c_int32 * q)(*[int(x) for x in lows])
+    hi_c = (C.c_int32 * q)(*[int(x) for x in highs])
+    mq.check(lib.mq_shared_select_count(dd.ptr, n, lo_c, hi_c, q, k, ws.ptr, ws.nbytes, None))
+    outs = [Dev(max(int(x), 1) * 4) for x in k]
+    ptrs = (C.c_void_p * q)(*[o.ptr for o in outs])
+    mq.check(lib.mq_shared_select_write(ws.ptr, ptrs, None))
+    return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
+
+
+@pytest.mark.parametrize("impl", ["ei", "ballot"])
+@pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
+                                  "mixed256", "narrow_domain"])
+def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
+    """q >= 24 runs the elementary-interval kernels (k_ssi_count / k_ssi_write,
+    MQ_SS_IMPL=ballot forces the per-query ballot kernels): sparse and dense
+    queries (dense tiles fall back to ballots inside k_ssi_write), nested and
+    identical ranges, INT32 extremes, all 256 queries, a 7-value domain."""
+    if impl == "ballot":
+        monkeypatch.setenv("MQ_SS_IMPL", "ballot")
+    rng = np.random.default_rng(hash(case) % 2 ** 32)
+    n = 1_000_003
+    d = rng.integers(0, 10 ** 6, n).astype(np.int32)
+    if case == "sparse150":
+        lows = rng.integers(0, 10 ** 6 - 1000, 150)
+        highs = lows + 1000
+    elif case == "nested":
+        c = rng.integers(300_000, 700_000, 40)
+        w = rng.integers(1, 300_000, 40)
+        lows, highs = c - w, c + w
+    elif case == "identical":
+        lows, highs = np.full(30, 123_456), np.full(30, 654_321)
+    elif case == "dense":
+        lows = rng.integers(0, 500_000, 48)
+        highs = lows + rng.integers(100_000, 500_000, 48)
+    elif case == "extremes":
+        d[:6] = [I32MIN, I32MAX, I32MIN + 1, I32MAX - 1, 0, -1]
+        lows = np.array([I32MIN, I32MIN, 0, -5, I32MAX - 1, I32MIN + 1] + list(rng.integers(0, 10 ** 6, 30)))
+        highs = np.array([I32MAX, I32MIN + 2, I32MAX, 5, I32MAX, 0] + list(rng.integers(0, 10 ** 6, 30)))
+    elif case == "mixed256":
+        lows = rng.integers(-10, 10 ** 6, 256)
+        highs = lows + rng.integers(-100, 20_000, 256)  # some empty/inverted
+    else:  # narrow_domain: 7 distinct values, many queries share bounds
+        d = rng.integers(0, 7, n).astype(np.int32)
+        lows = rng.integers(-1, 7, 64)
+        highs = lows + rng.integers(0, 4, 64)
+    lows = np.asarray(lows, dtype=np.int64).astype(np.int32)
+    highs = np.asarray(highs, dtype=np.int64).astype(np.int32)
+    got = _shared_run(lib, d, lows, highs)
+    for j in range(len(lows)):
+        want = refcpu.select_scan(d, int(lows[j]), int(highs[j]))
+        assert np.array_equal(got[j], want), (case, impl, j, int(lows[j]), int(highs[j]))
