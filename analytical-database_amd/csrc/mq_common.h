@@ -36,6 +36,9 @@ int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
 // are pool_alloc'd (the caller pool_frees them). Synchronises the stream.
 int radix_sort_pairs(const int* keys, const int* vals, uint64_t n, uint32_t** keys_out,
                      uint32_t** vals_out, hipStream_t st, const DevState* s);
+// The same sort of (col[i], i) written straight out as an index: values ascending
+// (int32, may be NULL) and positions (size_t rows, may be NULL). Synchronises.
+int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* positions, hipStream_t st);
 
 // Caching device allocator for per-call scratch (join tables and partitions,
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,

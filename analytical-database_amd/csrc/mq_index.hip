@@ -9,12 +9,12 @@
 //   unclustered (:140-143): index->positions is the permutation; plus a 100-bin
 //     histogram of the column (build_histogram :63-84).
 // Here the sort is the stable LSD radix sort of (value, row) pairs shared with the
-// join (4 passes of 8 bits: histogram, scan, ballot-ranked scatter), so rows of equal
+// join (4 passes of 8 bits: histogram, scan, ballot-ranked LDS-staged scatter; the
+// last pass writes int32 values and size_t positions), so rows of equal
 // value come out in ascending row order. The reference's quicksort leaves equal
 // values in an order of its own making (Lomuto partitions rotate the >= side); the
 // sorted values and, for distinct values, the positions are identical, and for
 // equal values each value's set of positions is.
-//   k_index_emit : keys back to int32, positions widened to size_t
 //   k_gather_u64 : reorder_column / fetch through size_t positions
 //   k_histogram  : build_histogram's bins, LDS-privatised counts
 
@@ -32,17 +32,6 @@ using namespace mqi;
 
 constexpr int kTPB = 256;
 constexpr int kBins = 100;  // BIN_NUM (cs165_api.h:46)
-
-__global__ __launch_bounds__(kTPB) void k_index_emit(const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ rows, uint64_t n,
-                                                      int32_t* __restrict__ values,
-                                                      unsigned long long* __restrict__ positions) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        if (values) values[i] = (int32_t)(keys[i] ^ 0x80000000u);
-        if (positions) positions[i] = rows[i];
-    }
-}
 
 __global__ __launch_bounds__(kTPB) void k_gather_u64(const int32_t* __restrict__ col,
                                                       const unsigned long long* __restrict__ pos,
@@ -82,18 +71,8 @@ int mq_index_build(const int32_t* d_col, uint64_t n, int32_t* d_values_out,
         return set_err(MQ_EINVAL, "mq_index_build: NULL pointer");
     if (n >= (1ull << 32)) return set_err(MQ_EINVAL, "mq_index_build: n >= 2^32");
     if (n == 0) return MQ_OK;
-    hipStream_t st = (hipStream_t)stream;
-    uint32_t *keys = nullptr, *rows = nullptr;
-    if ((rc = radix_sort_pairs(d_col, nullptr, n, &keys, &rows, st, s))) return rc;
-    hipLaunchKernelGGL(k_index_emit, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, keys, rows, n,
-                       d_values_out, reinterpret_cast<unsigned long long*>(d_positions_out));
-    const hipError_t e = hipGetLastError();
-    const hipError_t e2 = hipStreamSynchronize(st);
-    pool_free(keys);
-    pool_free(rows);
-    if (e != hipSuccess || e2 != hipSuccess)
-        return set_err(MQ_EHIP, "k_index_emit: %s", hipGetErrorString(e != hipSuccess ? e : e2));
-    return MQ_OK;
+    // the last radix pass writes the values and size_t positions directly
+    return radix_sort_index(d_col, n, d_values_out, d_positions_out, (hipStream_t)stream);
 }
 
 int mq_gather_u64(const int32_t* d_col, const uint64_t* d_positions, uint64_t n, int32_t* d_out,

@@ -178,12 +178,14 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1,
     hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-template <bool FIRST, bool LAST>
+// LAST: 0 = packed words to out, 1 = split into kout (flipped keys) / vout,
+// 2 = an index: kout as int32 values (key ^ 2^31 undone), pout as size_t rows.
+template <bool FIRST, int LAST>
 __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
                                                         const u64* __restrict__ in, uint64_t n, int shift,
                                                         const u64* __restrict__ goff, uint32_t ntiles,
                                                         u64* __restrict__ out, uint32_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout) {
+                                                        uint32_t* __restrict__ vout, u64* __restrict__ pout) {
     __shared__ uint32_t wcnt[kTPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
@@ -255,9 +257,12 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
             const u64 v = stage[e];
             const uint32_t d = ((uint32_t)v >> shift) & 0xFF;
             const u64 dst = gofs[d] + (e - loff[d]);
-            if constexpr (LAST) {
+            if constexpr (LAST == 1) {
                 kout[dst] = (uint32_t)v;
                 vout[dst] = (uint32_t)(v >> 32);
+            } else if constexpr (LAST == 2) {
+                if (kout) kout[dst] = (uint32_t)v ^ 0x80000000u;
+                if (pout) pout[dst] = v >> 32;
             } else {
                 out[dst] = v;
             }
@@ -761,41 +766,28 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
 
 namespace mqi {
 
-int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out,
-                     uint32_t** vals_out, hipStream_t st, const DevState* s) {
-    // packed {key ^ 2^31, value} words double-buffered; the last pass writes the
-    // split outputs; histogram + its scan + scan scratch
+// The 4 passes; the last writes per `mode` (see k_sortw_scatter's LAST).
+int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
+                   u64* pout, hipStream_t st) {
     u64 *w0 = nullptr, *w1 = nullptr, *hscan = nullptr, *scratch = nullptr;
-    uint32_t *ko = nullptr, *vo = nullptr, *hist = nullptr;
+    uint32_t* hist = nullptr;
     const uint64_t ntiles = ceil_div(n, kSortTile);
     const uint64_t nh = ntiles * kRadix;
-    auto release = [&]() {
+    auto done = [&](int rc) {
         pool_free(w0);
         pool_free(w1);
         pool_free(hist);
         pool_free(hscan);
         pool_free(scratch);
-    };
-    auto fail = [&](int rc) {
-        release();
-        pool_free(ko);
-        pool_free(vo);
         return rc;
     };
-    if (n == 0) {
-        *keys_out = (uint32_t*)pool_alloc(16);
-        *vals_out = (uint32_t*)pool_alloc(16);
-        return MQ_OK;
-    }
     w0 = (u64*)pool_alloc(n * 8);
     w1 = (u64*)pool_alloc(n * 8);
-    ko = (uint32_t*)pool_alloc(n * 4);
-    vo = (uint32_t*)pool_alloc(n * 4);
     hist = (uint32_t*)pool_alloc(nh * 4);
     hscan = (u64*)pool_alloc(nh * 8);
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
-    if (!w0 || !w1 || !ko || !vo || !hist || !hscan || !scratch)
-        return fail(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
+    if (!w0 || !w1 || !hist || !hscan || !scratch)
+        return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
     const dim3 g((uint32_t)ntiles), b(kTPB);
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
@@ -804,26 +796,55 @@ int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_o
         else
             hipLaunchKernelGGL((k_sortw_hist<false>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
-        if (rc) return fail(rc);
+        if (rc) return done(rc);
+        const uint32_t nt = (uint32_t)ntiles;
         if (pass == 0)
-            hipLaunchKernelGGL((k_sortw_scatter<true, false>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan,
-                               (uint32_t)ntiles, w1, nullptr, nullptr);
+            hipLaunchKernelGGL((k_sortw_scatter<true, 0>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan, nt, w1,
+                               nullptr, nullptr, nullptr);
         else if (pass < 3)
-            hipLaunchKernelGGL((k_sortw_scatter<false, false>), g, b, 0, st, nullptr, nullptr, w0, n, shift,
-                               hscan, (uint32_t)ntiles, w1, nullptr, nullptr);
+            hipLaunchKernelGGL((k_sortw_scatter<false, 0>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+                               nt, w1, nullptr, nullptr, nullptr);
+        else if (mode == 1)
+            hipLaunchKernelGGL((k_sortw_scatter<false, 1>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+                               nt, nullptr, kout, vout, nullptr);
         else
-            hipLaunchKernelGGL((k_sortw_scatter<false, true>), g, b, 0, st, nullptr, nullptr, w0, n, shift,
-                               hscan, (uint32_t)ntiles, nullptr, ko, vo);
-        if (hipGetLastError() != hipSuccess) return fail(set_err(MQ_EHIP, "sort: launch"));
+            hipLaunchKernelGGL((k_sortw_scatter<false, 2>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+                               nt, nullptr, kout, nullptr, pout);
+        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "sort: launch"));
         u64* t = w0;
         w0 = w1;
         w1 = t;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return fail(set_err(MQ_EHIP, "sort: sync"));
-    release();
+    // the temporaries go back to the pool only after the passes have run
+    if (hipStreamSynchronize(st) != hipSuccess) return done(set_err(MQ_EHIP, "sort: sync"));
+    return done(MQ_OK);
+}
+
+int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_out,
+                     uint32_t** vals_out, hipStream_t st, const DevState* s) {
+    (void)s;
+    uint32_t* ko = (uint32_t*)pool_alloc(n ? n * 4 : 16);
+    uint32_t* vo = (uint32_t*)pool_alloc(n ? n * 4 : 16);
+    if (!ko || !vo) {
+        pool_free(ko);
+        pool_free(vo);
+        return set_err(MQ_ENOMEM, "sort: outputs (%llu rows)", (unsigned long long)n);
+    }
+    int rc = n ? radix_sort_run(c1, p1, n, 1, ko, vo, nullptr, st) : MQ_OK;
+    if (rc) {
+        pool_free(ko);
+        pool_free(vo);
+        return rc;
+    }
     *keys_out = ko;
     *vals_out = vo;
     return MQ_OK;
+}
+
+int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* positions, hipStream_t st) {
+    return n ? radix_sort_run(col, nullptr, n, 2, reinterpret_cast<uint32_t*>(values), nullptr,
+                              reinterpret_cast<u64*>(positions), st)
+             : MQ_OK;
 }
 
 }  // namespace mqi
