@@ -6,7 +6,8 @@ A step is one pass of the hot path over one batch: range select [N/4, N/4 + N/10
 already resident in HBM (libmq mq_select_agg: k_scan + k_final). N=1 is
 BASELINE configs[1]; with --gpus G each rank scans its own 1e9-row column
 (seeds 42..42+G-1, configs[3]) and the per-rank {count, sum} are combined by one
-RCCL all-reduce inside the step ("weak" scaling). Data are synthetic
+RCCL all-reduce inside the step ("weak" scaling); the all-reduce runs on its own
+stream, overlapped with the next step's scan (double-buffered aggregates). Data are synthetic
 (SURVEY.md §8(c) generator), generated on the device.
 
   python bench.py [--gpus N --steps K --warmup W] [--rows R] [--no-cpu] [--no-extra]
@@ -147,10 +148,21 @@ def main() -> None:
         col = torch.empty(n, dtype=torch.int32, device=dev)
         ws_bytes = lib.mq_scan_workspace_bytes(n)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        agg = mqd.agg_tensor(dev)
+        # two aggregate buffers: step i scans into aggs[i % 2] on `stream` while the
+        # RCCL all-reduce of step i-1 runs on `comm`, so the combine (N > 1) is off
+        # the scan's critical path; a buffer is rescanned only after its all-reduce
+        aggs = [mqd.agg_tensor(dev), mqd.agg_tensor(dev)]
+        comm = torch.cuda.Stream(device=dev)
+        pending = [None, None]
+        counter = [0]
         mq.check(lib.mq_gen_uniform(col.data_ptr(), n, seed, n, sp), "gen")
 
         def step(ev0=None, ev1=None):
+            b = counter[0] % 2
+            counter[0] += 1
+            agg = aggs[b]
+            if pending[b] is not None:
+                stream.wait_event(pending[b])
             # one launch: k_scan<kSum> with the partials folded by the last block
             if ev0 is not None:
                 ev0.record(stream)
@@ -158,7 +170,15 @@ def main() -> None:
                                        ws.data_ptr(), ws_bytes, sp), "select_sum")
             if ev1 is not None:
                 ev1.record(stream)
-            mqd.combine_count_sum(agg)
+            if world > 1:
+                scanned = torch.cuda.Event()
+                scanned.record(stream)
+                comm.wait_event(scanned)
+                with torch.cuda.stream(comm):
+                    mqd.combine_count_sum(agg)
+                    fin = torch.cuda.Event()
+                    fin.record(comm)
+                pending[b] = fin
 
         for _ in range(args.warmup):
             step()
@@ -175,6 +195,7 @@ def main() -> None:
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        agg = aggs[(counter[0] - 1) % 2]  # the last step's combined aggregate
         kernel_ms = [a.elapsed_time(b) for a, b in evs]
 
     if world > 1:
