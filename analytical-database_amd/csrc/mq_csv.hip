@@ -101,29 +101,71 @@ size_t carve(void* ws, uint64_t n, int ncols, CsvWs* w) {
     return o;
 }
 
+// A column pointer read from the workspace is a generic (flat) pointer to the
+// compiler; its stores would be flat_store, which count in lgkmcnt, so every later
+// LDS read of the parse waited for them to reach memory. The columns are global.
+typedef int32_t __attribute__((address_space(1))) gint32;
+__device__ __forceinline__ gint32* global_ptr(int32_t* p) { return (gint32*)p; }
+
 // ---- staging: text[cs - kPre, cs + kChunk + kHalo) -> s (0 outside [0, n), except
-// that the byte before position 0 reads as '\n': position 0 starts a row).
+// that the byte before position 0 reads as '\n': position 0 starts a row). Every
+// lane issues all of its 16-byte loads before it stores any (a load/store loop
+// left one HBM round trip per piece on the block's critical path).
+constexpr int kPieces = kLds / 16;                  // 16-byte pieces staged per chunk
+constexpr int kPf = (kPieces + kTPB - 1) / kTPB;    // ... per lane
+static_assert(kLds % 16 == 0, "staging is in 16-byte pieces");
+
+// Whole 16-byte pieces inside the text are loaded (nt, dwordx4) into registers;
+// the others (before position 0, across or past EOF, or all of them when the text
+// is not 16-byte aligned) are filled byte by byte straight into LDS at store time.
+template <bool VEC>
+__device__ __forceinline__ bool piece_vec(uint64_t n, long long g) {
+    return VEC && g >= 0 && (uint64_t)g + 16 <= n;
+}
+
+// text[cs - kPre, cs + kChunk + kHalo) -> registers (stage_chunk's bytes)
+template <bool VEC>
+__device__ __forceinline__ void prefetch_chunk(const char* __restrict__ text, uint64_t n, uint64_t cs,
+                                               uint4 (&pf)[kPf]) {
+    const long long base = (long long)cs - kPre;
+#pragma unroll
+    for (int q = 0; q < kPf; q++) {
+        const int i = threadIdx.x + q * kTPB;
+        const long long g = base + (long long)i * 16;
+        if (i < kPieces && piece_vec<VEC>(n, g)) {
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + g));
+            pf[q] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    }
+}
+
+// registers -> LDS; the byte before position 0 reads as '\n', bytes past EOF as 0
+template <bool VEC>
+__device__ __forceinline__ void store_chunk(const char* __restrict__ text, uint64_t n, uint64_t cs,
+                                            const uint4 (&pf)[kPf], uint8_t* s) {
+    const long long base = (long long)cs - kPre;
+#pragma unroll
+    for (int q = 0; q < kPf; q++) {
+        const int i = threadIdx.x + q * kTPB;
+        if (i >= kPieces) continue;
+        const long long g = base + (long long)i * 16;
+        if (piece_vec<VEC>(n, g)) {
+            *reinterpret_cast<uint4*>(s + i * 16) = pf[q];
+        } else {
+            for (int k = 0; k < 16; k++) {
+                const long long x = g + k;
+                s[i * 16 + k] = x == -1 ? (uint8_t)'\n' : (x >= 0 && (uint64_t)x < n) ? (uint8_t)text[x] : 0;
+            }
+        }
+    }
+}
+
 template <bool VEC>
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ text, uint64_t n, uint64_t cs,
                                             uint8_t* s) {
-    const long long base = (long long)cs - kPre;
-    for (int i = threadIdx.x; i < kLds / 16; i += kTPB) {
-        const long long g = base + (long long)i * 16;
-        uint4 v;
-        if (VEC && g >= 0 && (uint64_t)g + 16 <= n) {
-            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + g));
-            v = make_uint4(t.x, t.y, t.z, t.w);
-        } else {
-            uint8_t t[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const long long q = g + k;
-                t[k] = q == -1 ? (uint8_t)'\n' : (q >= 0 && (uint64_t)q < n) ? (uint8_t)text[q] : 0;
-            }
-            memcpy(&v, t, 16);
-        }
-        *reinterpret_cast<uint4*>(s + i * 16) = v;
-    }
+    uint4 pf[kPf];
+    prefetch_chunk<VEC>(text, n, cs, pf);
+    store_chunk<VEC>(text, n, cs, pf, s);
 }
 
 // bit k set <=> byte k of the 4 is '\n' (exact SWAR zero-byte test)
@@ -506,6 +548,77 @@ __device__ __forceinline__ int32_t next_token(const uint8_t* __restrict__ s, int
     return parse_token(s, k, kend, more);
 }
 
+// Non-digit flags of a word: bit 7 of byte b set when byte b is not an ASCII digit.
+// Exact up to and including the first flagged byte (a carry leaves a byte only when
+// that byte is itself flagged, and only toward later bytes), which is all the
+// token scan needs.
+__device__ __forceinline__ uint32_t nondigit_first(uint32_t w) {
+    const uint32_t y = w ^ 0x30303030u;
+    return ((y + 0x76767676u) | y) & 0x80808080u;
+}
+
+// a * b + c on the low 24 bits of a (b < 2^24): the mask is free, it lets the
+// compiler pick v_mul_u32_u24 (full rate) instead of widening the product to
+// v_mad_u64_u32 / v_mul_lo_u32 (quarter rate).
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return (a & 0xFFFFFFu) * b + c; }
+
+// Four ASCII digits of a word (byte 0 the most significant) -> 0..9999, by two
+// v_dot4_u32_u8 (the accumulator removes 48 x the weights) and one 24-bit mad.
+__device__ __forceinline__ uint32_t digits4(uint32_t x) {
+    constexpr uint32_t kMinus48x11 = 0u - 48u * 11u;
+    const uint32_t hi = __builtin_amdgcn_udot4(x, 0x0000010Au, kMinus48x11, false);  // 10 b0 + b1
+    const uint32_t lo = __builtin_amdgcn_udot4(x, 0x010A0000u, kMinus48x11, false);  // 10 b2 + b3
+    return mad24(hi, 100u, lo);
+}
+
+// Index of the lowest set bit, or 0xFFFFFFFF for 0 (v_ffbl_b32 as it is).
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return (uint32_t)__builtin_ctzg(x, -1); }
+
+// next_token for the usual case, where every piece ends with its '\n' or at EOF
+// (no line over 1023 bytes: a token never runs past its piece, and past EOF the
+// staged bytes are NUL). The fast rule is token_fast's: [-]digits{0..10} then ',',
+// '\n' or NUL; anything else goes to parse_token (the strtol restatement). Written
+// branch-free up to that one decision:
+//   * 12 bytes at k (4 aligned LDS dwords + alignbyte): the first non-digit byte
+//     after an optional '-' is the end e (min3 over the three words' ffbl);
+//   * the 12 bytes ENDING at k+e are read again, so the digits sit right-aligned;
+//     the bytes before them become '0' (one bitfield insert per word) and the value
+//     is digits4 of the three words combined by 24-bit mads, mod 2^32: strtol
+//     saturates only past 18 digits, so (int)strtol is the low 32 bits.
+__device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, int& k, int kend,
+                                                 bool& more) {
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(s);
+    const int a = k >> 2;
+    const uint32_t r = (uint32_t)k & 3u;
+    const uint32_t d0 = d[a], d1 = d[a + 1], d2 = d[a + 2], d3 = d[a + 3];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, r), w1 = __builtin_amdgcn_alignbyte(d2, d1, r),
+                   w2 = __builtin_amdgcn_alignbyte(d3, d2, r);
+    const uint32_t neg = (w0 & 0xFFu) == '-' ? 1u : 0u;
+    const uint32_t f0 = nondigit_first(w0) & ~(neg << 7), f1 = nondigit_first(w1),
+                   f2 = nondigit_first(w2) | 0x80000000u;  // byte 11 ends the scan
+    const uint32_t bit = min(min(ffbl(f0), ffbl(f1) | 32u), ffbl(f2) | 64u);
+    const int e = (int)(bit >> 3);
+    const uint32_t L = (uint32_t)e - neg;  // digits
+    const uint32_t c = s[k + e];
+    const bool ok = (L <= 10u) & ((c == (uint32_t)',') | (c == (uint32_t)'\n') | (c == 0u));
+    if (!ok) return parse_token(s, k, kend, more);  // isspace / '+' / junk / 11+ digits
+    const int b = k + e - 12;  // >= kPre - 12 >= 0
+    const int a2 = b >> 2;
+    const uint32_t r2 = (uint32_t)b & 3u;
+    const uint32_t e0 = d[a2], e1 = d[a2 + 1], e2 = d[a2 + 2], e3 = d[a2 + 3];
+    const uint32_t z8 = 8u * (12u - L);  // leading bits that are not digits: 16..96
+    const uint64_t m01 = z8 >= 64u ? 0ull : (~0ull << z8);
+    const uint32_t m2 = (uint32_t)(0xFFFFFFFFull << (z8 > 64u ? z8 - 64u : 0u));
+    const uint32_t m0 = (uint32_t)m01, m1 = (uint32_t)(m01 >> 32);
+    const uint32_t x0 = (__builtin_amdgcn_alignbyte(e1, e0, r2) & m0) | (0x30303030u & ~m0);
+    const uint32_t x1 = (__builtin_amdgcn_alignbyte(e2, e1, r2) & m1) | (0x30303030u & ~m1);
+    const uint32_t x2 = (__builtin_amdgcn_alignbyte(e3, e2, r2) & m2) | (0x30303030u & ~m2);
+    const uint32_t v = mad24(mad24(digits4(x0), 100u, 0u), 1000000u, mad24(digits4(x1), 10000u, digits4(x2)));
+    more = c == ',';
+    k += e + (more ? 1 : 0);
+    return (int32_t)(neg ? 0u - v : v);
+}
+
 // ---- pass 2: parse. One block per chunk. The chunk's row starts stay as one
 // 64-bit mask per thread segment plus the exclusive prefix of their counts; lane i
 // takes pieces i, i+256, ... and finds piece i's byte by a binary search over the
@@ -578,16 +691,16 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
 #pragma unroll
         for (int j = 0; j < kRegCols; j++) {
             if (j < ncols && more) {
-                const int32_t v = next_token(s, k, kend, more);
-                cols[j][row] = v;
+                const int32_t v = lmode ? next_token(s, k, kend, more) : next_token_nl(s, k, kend, more);
+                global_ptr(cols[j])[row] = v;
                 mn[j] = min(mn[j], v);
                 mx[j] = max(mx[j], v);
                 got = j + 1;
             }
         }
         for (int j = kRegCols; j < ncols && more; j++) {
-            const int32_t v = next_token(s, k, kend, more);
-            cols[j][row] = v;
+            const int32_t v = lmode ? next_token(s, k, kend, more) : next_token_nl(s, k, kend, more);
+            global_ptr(cols[j])[row] = v;
             atomicMin(&s_mm[2 * j], v);
             atomicMax(&s_mm[2 * j + 1], v);
             got = j + 1;

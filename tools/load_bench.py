@@ -3,6 +3,7 @@ generator, seeds 42..) formatted as CSV text in HBM, then mq_csv_count_rows +
 mq_csv_parse_int32 timed with HIP events on the library stream; checks the parsed
 columns against the originals.
     python tools/load_bench.py [rows] [ncols] [reps]
+MQ_LIB=<path to another libmq.so build> times that build instead (A/B of kernel variants).
 """
 import ctypes as C
 import json
@@ -10,11 +11,13 @@ import sys
 import time
 
 sys.path[:0] = ["tests", "oracle"]
+import os  # noqa: E402
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from refapi import mq  # noqa: E402
 
-L = mq.load()
+L = mq.load(os.environ['MQ_LIB']) if os.environ.get('MQ_LIB') else mq.load()
 mq.check(L.mq_init(0))
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000_000
 ncols = int(sys.argv[2]) if len(sys.argv) > 2 else 4
