@@ -129,8 +129,14 @@ __global__ __launch_bounds__(kTPB) void k_ss_count(const int* __restrict__ col, 
     }
 }
 
+// Output pointers come from a device array, so the compiler sees generic (flat)
+// pointers; flat stores count in lgkmcnt and every later LDS wait would also wait
+// for them to reach memory. The outputs are global memory: store through that.
+typedef int __attribute__((address_space(1))) gint;
+__device__ __forceinline__ gint* global_ptr(int* p) { return (gint*)p; }
+
 // Writes one wave-tile's matches of one query; o advances by the match count.
-__device__ __forceinline__ void ss_emit(int* __restrict__ out, unsigned long long& o, uint64_t row,
+__device__ __forceinline__ void ss_emit(gint* __restrict__ out, unsigned long long& o, uint64_t row,
                                        unsigned long long m0, unsigned long long m1,
                                        unsigned long long m2, unsigned long long m3, int lane,
                                        unsigned long long ltmask) {
@@ -139,7 +145,7 @@ __device__ __forceinline__ void ss_emit(int* __restrict__ out, unsigned long lon
     const unsigned int pre = (unsigned int)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) +
                                             __popcll(m2 & ltmask) + __popcll(m3 & ltmask));
     const unsigned long long bit = 1ull << lane;
-    int* w = out + o + pre;
+    gint* w = out + o + pre;
     unsigned int k = 0;
     if (m0 & bit) w[k++] = (int)(row + 0);
     if (m1 & bit) w[k++] = (int)(row + 1);
@@ -174,7 +180,7 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
         for (int j = 0; j < q; j++) {
             const Pred p = preds[j];  // uniform index: scalar-cache load
             unsigned long long o = run[wave][j];
-            int* const out = outs[j];
+            gint* const out = global_ptr(outs[j]);
 #pragma unroll
             for (int u = 0; u < kSsUnroll; u++) {
                 const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                     const Pred p = preds[j];
                     unsigned long long o = run[wave][j];
                     const uint32_t b = match4(v[u], p, row, e);
-                    ss_emit(outs[j], o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
+                    ss_emit(global_ptr(outs[j]), o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
                             __ballot(b & 8u), lane, ltmask);
                     if (lane == 0) run[wave][j] = o;
                 }
@@ -405,7 +411,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                 unsigned long long base = 0;
                 if (i < tot) {
                     base = run[wave][mq];
-                    outs[mq][base + rank] = (int)(tile0 + (me & 0xFFFFu));
+                    global_ptr(outs[mq])[base + rank] = (int)(tile0 + (me & 0xFFFFu));
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (i < tot && !later) run[wave][mq] = base + rank + 1;
