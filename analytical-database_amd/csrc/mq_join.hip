@@ -591,6 +591,25 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
     }
 }
 
+// Diagnostic: k_ht_probe_unique's memory pattern alone (mq_random_read). Read j
+// goes to slot hash32(j) of a 2^k-slot table; 8 reads per lane in flight.
+__global__ __launch_bounds__(kTPB) void k_random_read(const u64* __restrict__ t, uint64_t mask, uint64_t n,
+                                                      u64* __restrict__ out) {
+    u64 acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB * kProbeILP;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x; j0 < n; j0 += stride) {
+        u64 v[kProbeILP];
+#pragma unroll
+        for (int u = 0; u < kProbeILP; u++) {
+            const uint64_t j = j0 + (uint64_t)u * kTPB;
+            v[u] = j < n ? t[hash32((uint32_t)j ^ (uint32_t)(j >> 32)) & mask] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kProbeILP; u++) acc ^= v[u];
+    }
+    if (acc == 0x5EED5EED5EED5EEDull) out[0] = acc;  // keeps the loads; never true for a memset table
+}
+
 // sorted keys are (key ^ 0x80000000); a run head claims its slot and stores the start
 __global__ __launch_bounds__(kTPB) void k_ht_insert_heads(const uint32_t* __restrict__ skeys,
                                                           uint64_t n, u64* words,
@@ -994,6 +1013,20 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     hipLaunchKernelGGL(k_join_write, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                        j->pstart, j->plen, j->offs, d_p2, j->bpos, j->n2, d_out1, d_out2);
     LAUNCHCHK("k_join_write");
+    return MQ_OK;
+}
+
+int mq_random_read(const uint64_t* d_table, int slots_log2, uint64_t n_reads, void* d_ws, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!d_table || !d_ws) return set_err(MQ_EINVAL, "mq_random_read: NULL pointer");
+    if (slots_log2 < 0 || slots_log2 > 40) return set_err(MQ_EINVAL, "mq_random_read: slots_log2 %d", slots_log2);
+    if (n_reads == 0) return MQ_OK;
+    hipLaunchKernelGGL(k_random_read, dim3(stream_grid(s, (n_reads + kProbeILP - 1) / kProbeILP)), dim3(kTPB), 0,
+                       (hipStream_t)stream, reinterpret_cast<const u64*>(d_table), (1ull << slots_log2) - 1,
+                       n_reads, static_cast<u64*>(d_ws));
+    LAUNCHCHK("k_random_read");
     return MQ_OK;
 }
 

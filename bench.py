@@ -508,7 +508,18 @@ def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True
         fnv = refcpu.fnv1a64_pairs(o1.cpu().numpy(), o2.cpu().numpy())
         ok = bool(want) and (m, f"{fnv:016x}") == (want[0]["m"], want[0]["pairs_fnv1a64"])
         del a, b, p, o1, o2
+        # the probe's random-access ceiling: n random 8-byte reads of a table of the
+        # join's size (2^(logn+1) slots), k_ht_probe_unique's pattern without compares
+        tbl = torch.zeros(1 << (logn + 1), dtype=torch.int64, device=dev)
+        wsr = torch.empty(1, dtype=torch.int64, device=dev)
+        ceil_ms = _events_ms(torch, stream, lambda: mq.check(
+            lib.mq_random_read(tbl.data_ptr(), logn + 1, n, wsr.data_ptr(), sp), "random_read"), 5)
+        del tbl
     res = {"n_build": n, "n_probe": n, "m": m, "ms": 1e3 * t,
+           "random_read_ceiling": {"kernel": "k_random_read", "reads": n, "table_bytes": 8 << (logn + 1),
+                                   "ms": ceil_ms, "g_reads_per_s": n / ceil_ms / 1e6,
+                                   "note": "n random 8-byte slot reads = the probe's table traffic; "
+                                           "k_ht_probe_unique's own time is in the rocprof stats"},
            "rows_per_s": 2 * n / t, "algorithmic_bytes": 8 * n + 8 * n + 8 * m,
            "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9, "parity": ok,
            "note": "wall time of build+probe+write incl. 2 host syncs (dup flag, M); "

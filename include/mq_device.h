@@ -100,6 +100,12 @@ int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void*
 int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes,
                    uint64_t* bytes_read, void* stream);
 
+/* Diagnostic (no reference counterpart): the random-access ceiling of the join
+ * probe. n_reads 8-byte reads of d_table (2^slots_log2
+ * u64 slots) at hashed slots, 8 per lane in flight: k_ht_probe_unique's pattern
+ * without the key compare or the output. d_ws: >= 8 bytes. */
+int mq_random_read(const uint64_t* d_table, int slots_log2, uint64_t n_reads, void* d_ws, void* stream);
+
 /* Config-3 fused: aggregate of d_val[i] over rows i where d_sel[i] is in range. */
 int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,
                         int32_t low, int has_high, int32_t high, mq_agg* d_out, void* d_ws,

@@ -1,0 +1,93 @@
+// random_read.hip — random-access ceiling probe for the join (not product code).
+// Times P random 8-byte reads from a table of S slots (u64), the access pattern of
+// k_ht_probe_unique (one slot per probe row, ILP loads in flight per lane), against
+// the same launch reading the slots in order. Prints G reads/s and the implied
+// bytes at 32/64/128-byte granules.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/random_read.hip -o tools/random_read
+//   tools/random_read [log2 slots=29] [log2 probes=28]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e = (x);                                                      \
+        if (e != hipSuccess) {                                                   \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));               \
+            exit(1);                                                             \
+        }                                                                        \
+    } while (0)
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+template <int ILP, bool RANDOM>
+__global__ __launch_bounds__(256) void k_read(const unsigned long long* __restrict__ t, uint64_t mask, uint64_t p,
+                                              unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * ILP;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * 256 * ILP + threadIdx.x; j0 < p; j0 += stride) {
+        unsigned long long v[ILP];
+#pragma unroll
+        for (int u = 0; u < ILP; u++) {
+            const uint64_t j = j0 + (uint64_t)u * 256;
+            const uint64_t h = RANDOM ? ((uint64_t)mix((uint32_t)j) ^ ((uint64_t)mix((uint32_t)(j >> 32) + 7u) << 32)) & mask : j & mask;
+            v[u] = j < p ? t[h] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < ILP; u++) acc ^= v[u];
+    }
+    if (acc == 0x123456789ull) out[0] = acc;  // keep the loads
+}
+
+template <int ILP, bool RANDOM>
+float run(const unsigned long long* t, uint64_t mask, uint64_t p, unsigned long long* o, int grid) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<float> ms;
+    for (int r = 0; r < 7; r++) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL((k_read<ILP, RANDOM>), dim3(grid), dim3(256), 0, 0, t, mask, p, o);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float x;
+        CK(hipEventElapsedTime(&x, a, b));
+        if (r >= 2) ms.push_back(x);
+    }
+    std::sort(ms.begin(), ms.end());
+    return ms[ms.size() / 2];
+}
+
+int main(int argc, char** argv) {
+    const int ls = argc > 1 ? atoi(argv[1]) : 29, lp = argc > 2 ? atoi(argv[2]) : 28;
+    const uint64_t S = 1ull << ls, P = 1ull << lp;
+    unsigned long long *t, *o;
+    CK(hipMalloc(&t, S * 8));
+    CK(hipMalloc(&o, 8));
+    CK(hipMemset(t, 1, S * 8));
+    hipDeviceProp_t pr;
+    CK(hipGetDeviceProperties(&pr, 0));
+    const int cus = pr.multiProcessorCount;
+    for (int grid_mul : {8, 16, 32}) {
+        const int grid = cus * grid_mul;
+        const float r1 = run<1, true>(t, S - 1, P, o, grid), r4 = run<4, true>(t, S - 1, P, o, grid),
+                    r8 = run<8, true>(t, S - 1, P, o, grid), r16 = run<16, true>(t, S - 1, P, o, grid),
+                    sq = run<8, false>(t, S - 1, P, o, grid);
+        printf("{\"slots_log2\": %d, \"probes_log2\": %d, \"grid\": %d, \"ms_random_ilp1\": %.3f, "
+               "\"ms_random_ilp4\": %.3f, \"ms_random_ilp8\": %.3f, \"ms_random_ilp16\": %.3f, "
+               "\"ms_sequential\": %.3f, \"best_g_reads_per_s\": %.2f}\n",
+               ls, lp, grid, r1, r4, r8, r16, sq, P / (std::min(std::min(r1, r4), std::min(r8, r16)) * 1e-3) / 1e9);
+    }
+    return 0;
+}
