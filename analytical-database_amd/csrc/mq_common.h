@@ -24,6 +24,10 @@ int current_device(int* dev);
 int ensure_ready(DevState** out);
 // Grid for a grid-stride streaming kernel of 256-thread blocks.
 uint32_t stream_grid(const DevState* s, uint64_t work_items);
+// The same, capped at the blocks of fn that are resident at once (a grid-stride
+// kernel whose registers allow fewer than 8 blocks per CU would otherwise run a
+// second, partial round of blocks).
+uint32_t resident_grid(const DevState* s, uint64_t work_items, const void* fn);
 // Device exclusive scan u32[n] -> u64[n] (mq_join.hip); scratch holds
 // scan_u32_scratch_elems(n) u64.
 uint64_t scan_u32_scratch_elems(uint64_t n);

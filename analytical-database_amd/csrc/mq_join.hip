@@ -344,6 +344,16 @@ __device__ __forceinline__ uint32_t win_id(uint32_t key, const Win& t) {
     return (uint32_t)((hash32(key) & t.mask) >> t.wlog);
 }
 
+// Unique-key tables start a key's linear probe at the first slot of its aligned
+// 4-slot bucket (32 B), not at its own slot: a probe then reads the whole bucket
+// with two 16-byte loads and rarely needs a second, dependent read (with the probe
+// starting at the hashed slot itself, about every other probe at load 1/2 went on
+// to the next slot after its first read returned).
+constexpr uint32_t kBucket = 4;
+__device__ __forceinline__ uint64_t ht_home(uint32_t key, uint64_t mask) {
+    return hash32(key) & mask & ~(uint64_t)(kBucket - 1);
+}
+
 // Global-CAS insert (builds below kWindowBuildRows): sets *general on a duplicate
 // key, the empty marker, or a full window.
 __global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict__ keys,
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_insert_unique(const int* __restrict
             continue;
         }
         const uint32_t key = (uint32_t)w;
-        uint64_t h = hash32(key) & t.mask;
+        uint64_t h = ht_home(key, t.mask);
         bool placed = false;
         for (uint64_t step = 0; step <= t.wmask; step++) {
             const u64 old = atomicCAS(&words[h], kEmpty, w);
@@ -525,7 +535,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
                 continue;
             }
             const uint32_t key = (uint32_t)v;
-            uint32_t h = (uint32_t)(hash32(key) & t.wmask);
+            uint32_t h = (uint32_t)ht_home(key, t.wmask);
             for (uint32_t step = 0; step < W; step++) {
                 const u64 old = atomicCAS(&tab[h], kEmpty, v);
                 if (old == kEmpty) break;
@@ -543,10 +553,10 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
 }
 
 // kProbeILP probes per thread per step: the keys are loaded coalesced, then all
-// their first slots are requested before any is examined, so a wave keeps
-// 64 x kProbeILP random reads in flight (one at a time measured 8.4 ms at 2^28);
-// collisions continue along the window from there (the next slot is usually in
-// the same line).
+// their home buckets (4 slots, 32 B, two 16-byte loads) are requested before any
+// is examined, so a wave keeps 64 x kProbeILP random reads in flight (one at a
+// time measured 8.4 ms at 2^28). Only a full bucket without the key continues
+// along the window, slot by slot.
 constexpr int kProbeILP = 8;
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
@@ -556,7 +566,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
     for (uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x; j0 < n2; j0 += stride) {
         uint32_t key[kProbeILP];
         uint64_t h[kProbeILP];
-        u64 cur[kProbeILP];
+        ulonglong2 b0[kProbeILP], b1[kProbeILP];  // the home bucket, slots 0-1 and 2-3
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
@@ -564,26 +574,42 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
         }
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
-            h[u] = hash32(key[u]) & t.mask;
-            cur[u] = j0 + (uint64_t)u * kTPB < n2 ? words[h[u]] : kEmpty;
+            h[u] = ht_home(key[u], t.mask);
+            if (j0 + (uint64_t)u * kTPB < n2) {
+                const ulonglong2* q = reinterpret_cast<const ulonglong2*>(words + h[u]);
+                b0[u] = q[0];
+                b1[u] = q[1];
+            } else {
+                b0[u] = b1[u] = make_ulonglong2(kEmpty, kEmpty);
+            }
         }
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
             if (j >= n2) continue;
-            bool hit = false;
+            const u64 sl[kBucket] = {b0[u].x, b0[u].y, b1[u].x, b1[u].y};
+            bool hit = false, done = false;
             uint32_t payload = 0;
-            u64 c = cur[u];
-            uint64_t hh = h[u];
-            for (uint64_t step = 0; step <= t.wmask; step++) {
-                if (c == kEmpty) break;
-                if ((uint32_t)c == key[u]) {
-                    hit = true;
-                    payload = (uint32_t)(c >> 32);
-                    break;
+#pragma unroll
+            for (uint32_t i = 0; i < kBucket; i++) {
+                if (done) break;
+                const u64 c = sl[i];
+                if (c == kEmpty) done = true;
+                else if ((uint32_t)c == key[u]) hit = done = true, payload = (uint32_t)(c >> 32);
+            }
+            if (!done) {  // a full bucket without the key: on along the window
+                uint64_t hh = h[u];
+                for (uint32_t i = 0; i < kBucket; i++) hh = win_next(hh, t);
+                for (uint64_t step = kBucket; step <= t.wmask; step++) {
+                    const u64 c = words[hh];
+                    if (c == kEmpty) break;
+                    if ((uint32_t)c == key[u]) {
+                        hit = true;
+                        payload = (uint32_t)(c >> 32);
+                        break;
+                    }
+                    hh = win_next(hh, t);
                 }
-                hh = win_next(hh, t);
-                c = words[hh];
             }
             pstart[j] = payload;  // unique path: the build position itself
             plen[j] = hit ? 1u : 0u;
@@ -986,7 +1012,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (!j->pstart || !j->plen || !j->offs || !j->scan_scratch)
         return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
     if (j->unique)
-        hipLaunchKernelGGL(k_ht_probe_unique, dim3(stream_grid(s, (n2 + kProbeILP - 1) / kProbeILP)), dim3(kTPB), 0, st, d_c2, n2,
+        hipLaunchKernelGGL(k_ht_probe_unique, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)&k_ht_probe_unique)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, j->plen);
     else
         hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,

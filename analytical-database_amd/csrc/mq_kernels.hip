@@ -1435,6 +1435,12 @@ uint32_t stream_grid(const DevState* s, uint64_t work_items) {
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
+uint32_t resident_grid(const DevState* s, uint64_t work_items, const void* fn) {
+    const uint32_t g = stream_grid(s, work_items);
+    const uint64_t cap = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
+    return cap && g > cap ? (uint32_t)cap : g;
+}
+
 // Fold (has_low, low, has_high, high) into one unsigned range compare.
 // Returns false for an empty range.
 bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
