@@ -33,7 +33,7 @@ using namespace mqi;
 constexpr int kTPB = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kTPB * kScanItems;  // 4096
-constexpr int kSortItems = 16;
+constexpr int kSortItems = 16;  // 8: 36.3 ms, 32: 40.5 ms for the 1e9-row index (16: 31.2)
 constexpr int kSortTile = kTPB * kSortItems;  // 4096
 constexpr int kRadix = 256;
 

@@ -1,5 +1,6 @@
 """Index-build timing (not product code): mq_index_build on an n-row uniform column
 (seed 42), HIP events on the library stream, median of reps after one warm-up."""
+import os
 import sys
 import time
 
@@ -7,7 +8,7 @@ sys.path[:0] = ["tests", "oracle"]
 import torch  # noqa: E402
 from refapi import mq  # noqa: E402
 
-L = mq.load()
+L = mq.load(os.environ['MQ_LIB']) if os.environ.get('MQ_LIB') else mq.load()
 mq.check(L.mq_init(0))
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
