@@ -392,29 +392,33 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
             for (int k = 0; k < 4; k++)
                 for (uint32_t i = 0; i < qn[k]; i++) pl[at++] = ((uint32_t)T.qlist[qa[k] + i] << 16) | (uint32_t)(lane * 4 + k);
             __builtin_amdgcn_wave_barrier();
-            // rank of each pair among earlier pairs of its query; the last pair of a
-            // query advances that query's running offset
+            // rank of each pair among earlier pairs of its query: 64 pairs at a time,
+            // lanes holding the same query found by 8 ballots over its bits (was a
+            // broadcast-read loop over all the tile's pairs: one dependent LDS
+            // read per pair); the group's last pair of a query advances that
+            // query's running offset, so later groups start after it
             const uint64_t tile0 = t + (uint64_t)u * kWaveTile;
             for (uint32_t i0 = 0; i0 < tot; i0 += 64) {
                 const uint32_t i = i0 + (uint32_t)lane;
-                const uint32_t me = i < tot ? pl[i] : 0xFFFFFFFFu;
-                const uint32_t mq = me >> 16;
-                uint32_t rank = 0;
-                bool later = false;
-                for (uint32_t j = 0; j < tot; j++) {  // broadcast read
-                    const uint32_t oq = pl[j] >> 16;
-                    if (oq == mq) {
-                        rank += j < i ? 1u : 0u;
-                        later = later || j > i;
-                    }
+                const bool valid = i < tot;
+                const uint32_t me = valid ? pl[i] : 0u;
+                const uint32_t mq = me >> 16;  // < q <= kMaxQ = 256: 8 bits
+                unsigned long long peers = __ballot(valid);
+#pragma unroll
+                for (int bt = 0; bt < 8; bt++) {
+                    const bool bit = (mq >> bt) & 1u;
+                    const unsigned long long m = __ballot(bit);
+                    peers &= bit ? m : ~m;
                 }
+                const uint32_t rank = (uint32_t)__popcll(peers & ltmask);
+                const bool last = (peers & ~ltmask & ~(1ull << lane)) == 0;
                 unsigned long long base = 0;
-                if (i < tot) {
+                if (valid) {
                     base = run[wave][mq];
                     global_ptr(outs[mq])[base + rank] = (int)(tile0 + (me & 0xFFFFu));
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (i < tot && !later) run[wave][mq] = base + rank + 1;
+                if (valid && last) run[wave][mq] = base + rank + 1;
                 __builtin_amdgcn_wave_barrier();
             }
         }
