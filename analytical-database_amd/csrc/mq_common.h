@@ -51,6 +51,33 @@ int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* posi
 void* pool_alloc(size_t bytes);
 void pool_free(void* p);
 
+// Lanes of the wave (within `among`) whose 8-bit value d equals this lane's: a
+// match-any from 8 ballots. Per bit: one v_bfe_i32 (the bit as 0 / all-ones),
+// one ballot and one or-of-xor per half, accumulating the lanes that differ from
+// this lane in some bit (written as `peers &= bit ? m : ~m`, the compiler spent
+// 9 VALU per bit on it).
+__device__ __forceinline__ unsigned long long match_any8(uint32_t d, unsigned long long among) {
+    uint32_t dlo = 0, dhi = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const uint32_t sb = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);  // bit b as 0 / ~0
+        const unsigned long long m = __ballot(sb != 0);
+        dlo |= sb ^ (uint32_t)m;
+        dhi |= sb ^ (uint32_t)(m >> 32);
+    }
+    return among & ~(((unsigned long long)dhi << 32) | dlo);
+}
+
+// XCD-aware tile of block b in a grid of g blocks (cdna_hip_programming.md T1):
+// blocks are dealt round-robin over the 8 XCDs, so block b runs on XCD b % 8;
+// this bijection gives each XCD a contiguous range of tiles instead. Tiles whose
+// outputs share cache lines (adjacent digit runs of a radix scatter) then meet in
+// one L2 and leave it as whole lines. Speed only: any bijection is correct.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t g) {
+    const uint32_t q = g >> 3, r = g & 7u, x = b & 7u;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 }  // namespace mqi
 
 #define HIPCHK(expr)                                                                         \

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1,
     __shared__ uint32_t h[kRadix];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kSortTile;
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1,
         }
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // LAST: 0 = packed words to out, 1 = split into kout (flipped keys) / vout,
@@ -194,9 +195,10 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
-    gofs[tid] = goff[(uint64_t)tid * ntiles + blockIdx.x];
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kSortTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
@@ -207,13 +209,7 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
         const bool valid = i < n;
         el[k] = valid ? sort_word<FIRST>(c1, p1, in, i) : 0ull;
         const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
-        u64 peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const bool bit = (d >> b) & 1u;
-            const u64 m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
+        const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
         const uint32_t cur = wcnt[wave][d];
         __builtin_amdgcn_wave_barrier();
@@ -399,7 +395,8 @@ __global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
     __shared__ uint32_t h[kRadix];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kSortTile;
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
@@ -409,7 +406,7 @@ __global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
         }
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // Stable scatter (k_sortw_scatter's ballot ranking), staged through LDS so that each
@@ -428,9 +425,10 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
     for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
-    gofs[tid] = goff[(uint64_t)tid * ntiles + blockIdx.x];
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)blockIdx.x * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kSortTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
@@ -441,13 +439,7 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
         const bool valid = i < n;
         el[k] = valid ? win_elem<FROM_COLS>(c1, p1, in, i) : 0ull;
         const uint32_t d = (win_id((uint32_t)el[k], t) >> shift) & 0xFF;
-        u64 peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const bool bit = (d >> b) & 1u;
-            const u64 m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
+        const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
         const uint32_t cur = wcnt[wave][d];
         __builtin_amdgcn_wave_barrier();

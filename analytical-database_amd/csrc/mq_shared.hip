@@ -403,13 +403,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                 const bool valid = i < tot;
                 const uint32_t me = valid ? pl[i] : 0u;
                 const uint32_t mq = me >> 16;  // < q <= kMaxQ = 256: 8 bits
-                unsigned long long peers = __ballot(valid);
-#pragma unroll
-                for (int bt = 0; bt < 8; bt++) {
-                    const bool bit = (mq >> bt) & 1u;
-                    const unsigned long long m = __ballot(bit);
-                    peers &= bit ? m : ~m;
-                }
+                const unsigned long long peers = match_any8(mq, __ballot(valid));
                 const uint32_t rank = (uint32_t)__popcll(peers & ltmask);
                 const bool last = (peers & ~ltmask & ~(1ull << lane)) == 0;
                 unsigned long long base = 0;
