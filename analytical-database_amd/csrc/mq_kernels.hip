@@ -1063,6 +1063,27 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
 }
 
 // ---------------------------------------------------------------------------
+// hashset.c lookup (hashset.c:35-45): one probe per lane along the reference's
+// linear sequence from key % size; 0 marks an empty slot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kTPB) void k_hashset_lookup(const int32_t* __restrict__ table, int32_t size,
+                                                         const int32_t* __restrict__ probe, uint64_t n,
+                                                         uint8_t* __restrict__ found) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const int32_t key = probe[i];
+        int32_t idx = key % size;  // hash() of multimap.c:60-63
+        if (idx < 0) idx += size;  // the reference indexes out of bounds here
+        int32_t v = table[idx];
+        for (int32_t step = 1; v != 0 && v != key && step < size; step++) {
+            idx = idx + 1 == size ? 0 : idx + 1;
+            v = table[idx];
+        }
+        found[i] = (v != 0 && v == key) ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // fetch (query.c:223-243): out[i] = col[pos[i]], 4 positions per lane.
 // ---------------------------------------------------------------------------
 template <bool VEC>
@@ -1894,6 +1915,43 @@ int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes
                        rpb, static_cast<uint32_t*>(d_ws));
     LAUNCHCHK("k_stream_read");
     return MQ_OK;
+}
+
+int mq_hashset_lookup(const int32_t* d_table, int32_t size, const int32_t* d_probe, uint64_t n,
+                      uint8_t* d_found, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (size <= 0) return set_err(MQ_EINVAL, "mq_hashset_lookup: size %d", size);
+    if (n == 0) return MQ_OK;
+    if (!d_table || !d_probe || !d_found) return set_err(MQ_EINVAL, "mq_hashset_lookup: NULL pointer");
+    hipLaunchKernelGGL(k_hashset_lookup, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream, d_table,
+                       size, d_probe, n, d_found);
+    LAUNCHCHK("k_hashset_lookup");
+    return MQ_OK;
+}
+
+// get_hashset_elements (hashset.c:48-65): the nonzero slots in slot order, i.e. the
+// ordered compaction of the table with itself as payload under v != 0, which is
+// the unsigned range (uint32)(v - 1) <= 0xFFFFFFFE.
+int mq_hashset_elements(const int32_t* d_table, uint64_t size, int32_t* d_out, uint64_t* d_count,
+                        void* d_ws, size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!d_count || (size && (!d_table || !d_out || !d_ws)))
+        return set_err(MQ_EINVAL, "mq_hashset_elements: NULL pointer");
+    if (size >= (1ull << 31)) return set_err(MQ_EINVAL, "mq_hashset_elements: size beyond int32 positions");
+    hipStream_t st = (hipStream_t)stream;
+    if (size == 0) {
+        HIPCHK(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+        return MQ_OK;
+    }
+    if (ws_bytes < mq_scan_workspace_bytes(size)) return set_err(MQ_EINVAL, "mq_hashset_elements: workspace too small");
+    Pred p;
+    p.lo = 1u;
+    p.wm1 = 0xFFFFFFFEu;
+    return run_select_stage(d_table, d_table, size, p, d_out, d_count, d_ws, st, s);
 }
 
 int mq_combine_partials(const void* d_ws, uint32_t nblocks, mq_agg* d_out, void* stream) {

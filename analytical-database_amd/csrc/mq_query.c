@@ -777,6 +777,90 @@ char* print(Result** results, int result_num, Status* ret_status) {
 
 /* The server's own capacity helpers (db_manager.c:430 save_data, :736 start_data),
  * resolved from the executable that links libmq; NULL when none does. */
+/* ---- J4: hashset.c (src/hashset.c:11-65) ----
+ * The reference's linear-probing int32 set, kept as its own host table so that
+ * code written against hashset.h behaves the same; defined behaviour where the
+ * reference has none (include/mq_query.h). get_hashset_elements lists large
+ * tables on the GPU (mq_hashset_elements: ordered compaction of the nonzero
+ * slots, in slot order). */
+__attribute__((weak)) int hash(int key, int size) { return key % size; }  /* multimap.c:60-63 */
+
+static int hs_home(int key, int size) {
+    int idx = key % size;
+    return idx < 0 ? idx + size : idx;  /* the reference reads keys[negative] here */
+}
+
+hashset* create_hashset(int size) {
+    hashset* set = (hashset*)malloc(sizeof(hashset));
+    set->keys = (int*)calloc(size > 0 ? (size_t)size : 1, sizeof(int));  /* reference: malloc */
+    set->size = size;
+    return set;
+}
+
+void free_hashset(hashset* set) {
+    if (!set) return;
+    free(set->keys);
+    free(set);
+}
+
+void insert_hashset(hashset* set, int key) {
+    if (!set || set->size <= 0) return;
+    int idx = hs_home(key, set->size);
+    for (int step = 0; set->keys[idx] != 0 && set->keys[idx] != key; step++) {
+        if (step + 1 >= set->size) return;  /* full without the key: the reference spins */
+        idx = idx + 1 == set->size ? 0 : idx + 1;
+    }
+    set->keys[idx] = key;
+}
+
+bool lookup_hashset(hashset* set, int key) {
+    if (!set || set->size <= 0) return false;
+    int idx = hs_home(key, set->size);
+    for (int step = 0; set->keys[idx] != 0 && set->keys[idx] != key; step++) {
+        if (step + 1 >= set->size) return false;
+        idx = idx + 1 == set->size ? 0 : idx + 1;
+    }
+    return set->keys[idx] != 0;
+}
+
+static size_t hashset_gpu_min(void) {
+    const char* e = getenv("MQ_HASHSET_GPU_MIN");
+    return e ? (size_t)strtoull(e, NULL, 10) : (size_t)32768;
+}
+
+Result* get_hashset_elements(hashset* set) {
+    const size_t size = set && set->size > 0 ? (size_t)set->size : 0;
+    if (size >= hashset_gpu_min() && ready(NULL) == 0) {
+        Status st = {OK, NULL};
+        void* d_tab = NULL;
+        int rc = mq_malloc(&d_tab, 2 * size * sizeof(int32_t));  /* table, then elements */
+        if (!rc && !(rc = ensure_ws(size, &st)) && !(rc = h2d(d_tab, set->keys, size * sizeof(int32_t)))) {
+            int32_t* d_out = (int32_t*)d_tab + size;
+            uint64_t k = 0;
+            if (!(rc = mq_hashset_elements((const int32_t*)d_tab, size, d_out, (uint64_t*)g_small, g_ws,
+                                           g_ws_bytes, g_stream)) &&
+                !(rc = read_count(&k, &st))) {
+                int32_t* host = (int32_t*)malloc((k ? k : 1) * sizeof(int32_t));
+                if (!(rc = k ? d2h(host, d_out, k * sizeof(int32_t)) : 0)) {
+                    mq_free(d_tab);
+                    return new_result(INT, k, host);
+                }
+                free(host);
+            }
+        }
+        if (d_tab) mq_free(d_tab);
+        fail(NULL, "get_hashset_elements on the GPU", rc ? rc : MQ_EHIP);
+        return NULL;
+    }
+    size_t count = 0;
+    for (size_t i = 0; i < size; i++) count += set->keys[i] != 0;
+    int32_t* elements = (int32_t*)malloc((count ? count : 1) * sizeof(int32_t));  /* reference: 16 B */
+    count = 0;
+    for (size_t i = 0; i < size; i++)
+        if (set->keys[i] != 0) elements[count++] = set->keys[i];
+    return new_result(INT, count, elements);
+}
+
 extern void save_data(Table* table, Column* column, Status* ret_status) __attribute__((weak));
 extern void start_data(Db* db, Table* table, Column* column, Status* ret_status)
     __attribute__((weak));

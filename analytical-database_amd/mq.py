@@ -130,6 +130,8 @@ _SIGS = {
     "mq_csv_count_rows": (_int, [_vp, _u64, _int, C.POINTER(_u64), _vp, _sz, _vp]),
     "mq_csv_parse_int32": (_int, [_vp, _u64, _int, _vp, _u64, _vp, _vp, _sz, _vp]),
     "mq_stream_read": (_int, [_vp, _u64, _vp, _sz, C.POINTER(C.c_uint64), _vp]),
+    "mq_hashset_lookup": (_int, [_vp, _i32, _vp, _u64, _vp, _vp]),
+    "mq_hashset_elements": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _vp]),
     "mq_random_read": (_int, [_vp, _int, _u64, _vp, _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,

@@ -106,6 +106,22 @@ int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes
  * without the key compare or the output. d_ws: >= 8 bytes. */
 int mq_random_read(const uint64_t* d_table, int slots_log2, uint64_t n_reads, void* d_ws, void* stream);
 
+/* ---- J4 hashset.c (src/hashset.c:11-65) on the device ----
+ * The set is the reference's own table: `size` int32 slots, 0 = empty, a key's
+ * linear probe starting at hash(key, size) = key % size (multimap.c:60-63; a
+ * negative key, an out-of-bounds index in the reference, starts at the wrapped
+ * remainder here).
+ * mq_hashset_lookup: d_found[i] = lookup_hashset(set, d_probe[i]) (hashset.c:35-45)
+ *   for n probes; a full table without the key answers 0 after one lap (the
+ *   reference loops forever).
+ * mq_hashset_elements: the nonzero slots in slot order (get_hashset_elements,
+ *   hashset.c:48-65) into d_out (capacity size); *d_count (device) receives their
+ *   number. d_ws: mq_scan_workspace_bytes(size) bytes. */
+int mq_hashset_lookup(const int32_t* d_table, int32_t size, const int32_t* d_probe, uint64_t n,
+                      uint8_t* d_found, void* stream);
+int mq_hashset_elements(const int32_t* d_table, uint64_t size, int32_t* d_out, uint64_t* d_count,
+                        void* d_ws, size_t ws_bytes, void* stream);
+
 /* Config-3 fused: aggregate of d_val[i] over rows i where d_sel[i] is in range. */
 int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,
                         int32_t low, int has_high, int32_t high, mq_agg* d_out, void* d_ws,

@@ -143,6 +143,29 @@ Result* select_column_sorted_index(Column* column, int low, int high,
 /* index.c:180-185 — exported weak so the reference's index.o definition wins. */
 bool should_use_index(Column* column, int low, int high);
 
+/* ---- J4: hashset.h (src/include/hashset.h:7-24) ----
+ * hashset.c is not linked into the reference server and has no caller
+ * (src/Makefile:62); libmq exports its API so that code
+ * written against hashset.h links, with the reference's semantics: `size` int32
+ * slots, 0 = empty (0 is never a member), linear probing from hash(key, size).
+ * Defined where the reference leaves undefined behaviour: the slots start zeroed
+ * (create_hashset mallocs them uninitialised, hashset.c:13), a negative key's probe
+ * starts at the wrapped remainder (the reference indexes out of bounds), a full
+ * table stops after one lap (it loops forever), and get_hashset_elements returns a
+ * buffer sized for its elements (hashset.c:49 allocates 16 bytes). Its element
+ * listing runs on the GPU for tables of >= 32768 slots (MQ_HASHSET_GPU_MIN);
+ * mq_hashset_lookup (mq_device.h) is the batched device lookup. */
+typedef struct hashset {                                              /* hashset.h:7-10 */
+    int* keys;
+    int size;
+} hashset;
+int hash(int key, int size);                       /* multimap.c:60-63, exported weak */
+hashset* create_hashset(int size);                 /* hashset.c:11-16 */
+void free_hashset(hashset* set);                   /* hashset.c:19-22 */
+void insert_hashset(hashset* set, int key);        /* hashset.c:25-32 */
+bool lookup_hashset(hashset* set, int key);        /* hashset.c:35-45 */
+Result* get_hashset_elements(hashset* set);        /* hashset.c:48-65 */
+
 /* ---- the load path (db_manager.h:254) ----
  * load_db (db_manager.c:240-322 with insert_row :164-199): same header check
  * (db name, table name), same rows, values, min/max and table_length growth, with

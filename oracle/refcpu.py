@@ -256,3 +256,49 @@ def histogram(col: np.ndarray, mn: int, bin_size: int) -> np.ndarray:
     out = np.zeros(101, dtype=np.uint64)
     lib().rc_histogram(_a(col), len(col), mn, bin_size, _a(out))
     return out
+
+
+# ---------------------------------------------------------------------------
+# J4 hashset.c restatement (pure Python: small sets only)
+# ---------------------------------------------------------------------------
+def _hs_home(key: int, size: int) -> int:
+    """hash(key, size) = key % size (multimap.c:60-63, C remainder: truncates toward
+    zero). The reference indexes keys[negative] for a negative key; the restatement
+    (like libmq) starts such a probe at the wrapped remainder."""
+    r = abs(key) % size
+    r = -r if key < 0 else r
+    return r + size if r < 0 else r
+
+
+def hashset_table(keys, size: int) -> np.ndarray:
+    """The slots after insert_hashset of keys in order (hashset.c:25-32): linear
+    probing from the home slot while the slot is nonzero and not the key; 0 marks
+    an empty slot, so inserting 0 changes nothing. A full table without the key
+    stops after one lap (the reference loops forever)."""
+    t = [0] * size
+    for k in (int(x) for x in keys):
+        i = _hs_home(k, size)
+        for step in range(size):
+            if t[i] == 0 or t[i] == k:
+                t[i] = k
+                break
+            i = i + 1 if i + 1 < size else 0
+    return np.array(t, dtype=np.int32)
+
+
+def hashset_lookup(table: np.ndarray, key: int) -> bool:
+    """lookup_hashset (hashset.c:35-45): probe as insert does; found iff the slot it
+    stops at is nonzero (so 0 is never a member)."""
+    size = len(table)
+    i = _hs_home(int(key), size)
+    for _ in range(size):
+        v = int(table[i])
+        if v == 0 or v == key:
+            return v != 0
+        i = i + 1 if i + 1 < size else 0
+    return False
+
+
+def hashset_elements(table: np.ndarray) -> np.ndarray:
+    """get_hashset_elements (hashset.c:48-65): the nonzero slots in slot order."""
+    return table[table != 0]
