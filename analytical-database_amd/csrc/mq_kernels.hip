@@ -1763,6 +1763,21 @@ int mq_stream_sync(void* stream) {
     return MQ_OK;
 }
 
+int mq_pool_malloc(void** dptr, size_t bytes) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!dptr) return set_err(MQ_EINVAL, "mq_pool_malloc: NULL out pointer");
+    *dptr = pool_alloc(bytes);
+    if (!*dptr) return set_err(MQ_ENOMEM, "mq_pool_malloc(%zu) failed", bytes);
+    return MQ_OK;
+}
+
+int mq_pool_free(void* dptr) {
+    pool_free(dptr);
+    return MQ_OK;
+}
+
 void mq_trim(void) {
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(g_pool_mu);

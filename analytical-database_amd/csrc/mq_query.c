@@ -164,7 +164,7 @@ static int ready(Status* st) {
 
 static int grow(void** buf, size_t* have, size_t need) {
     if (*have >= need && *buf) return 0;
-    if (*buf) mq_free(*buf);
+    if (*buf) mq_pool_free(*buf);
     *buf = NULL;
     *have = 0;
     size_t want = need + need / 8 + 4096;
@@ -197,7 +197,7 @@ static ColEntry* col_find(const Column* c) {
 }
 
 static void col_drop(ColEntry* e) {
-    if (e->owned && e->dev) mq_free(e->dev);
+    if (e->owned && e->dev) mq_pool_free(e->dev);
     *e = g_cols[--g_ncols];
 }
 
@@ -211,10 +211,10 @@ static int column_device(Column* c, const int32_t** d, Status* st) {
     if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
     size_t bytes = c->row_count * sizeof(int32_t);
     void* dev = NULL;
-    int rc = mq_malloc(&dev, bytes);
+    int rc = mq_pool_malloc(&dev, bytes);
     if (rc) return fail(st, "column allocation", rc);
     if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
-        mq_free(dev);
+        mq_pool_free(dev);
         return fail(st, "column upload", rc);
     }
     g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1};
@@ -225,7 +225,7 @@ static int column_device(Column* c, const int32_t** d, Status* st) {
 /* ---- result shadows ---- */
 
 static void shadow_drop(int i) {
-    if (g_shadows[i].dev) mq_free(g_shadows[i].dev);
+    if (g_shadows[i].dev) mq_pool_free(g_shadows[i].dev);
     g_shadow_bytes -= g_shadows[i].bytes;
     g_shadows[i] = g_shadows[--g_nshadows];
 }
@@ -278,15 +278,29 @@ static int result_device(const Result* r, const int32_t** d, Status* st) {
         return 0;
     }
     void* dev = NULL;
-    int rc = mq_malloc(&dev, n * sizeof(int32_t));
+    int rc = mq_pool_malloc(&dev, n * sizeof(int32_t));
     if (rc) return fail(st, "result allocation", rc);
     if (n && (rc = h2d(dev, h, n * sizeof(int32_t)))) {
-        mq_free(dev);
+        mq_pool_free(dev);
         return fail(st, "result upload", rc);
     }
     shadow_put(h, n, dev);
     *d = (const int32_t*)dev;
     return 0;
+}
+
+/* A result payload: plain malloc (the caller free()s it, client_context.c:31-90).
+ * Large ones are advised onto transparent huge pages first: the D2H that fills a
+ * fresh buffer otherwise takes one page fault per 4 KB (tools/d2h_paths: 40 MB in
+ * 2.0 ms plain, 1.7 ms advised). */
+static void* payload_alloc(size_t bytes) {
+    void* p = malloc(bytes ? bytes : 1);
+    if (p && bytes >= ((size_t)8 << 20)) {
+        const uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095;
+        const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)4095;
+        if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
+    }
+    return p;
 }
 
 static Result* new_result(DataType t, size_t n, void* payload) {
@@ -300,7 +314,7 @@ static Result* new_result(DataType t, size_t n, void* payload) {
 /* Host Result from n int32 on the device (d_src, staging memory): D2H into a
  * malloc'd payload and keep an HBM shadow of it. */
 static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
-    int32_t* host = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
     int rc;
     if (n && (rc = d2h(host, d_src, n * sizeof(int32_t)))) {
         free(host);
@@ -308,13 +322,13 @@ static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
         return NULL;
     }
     void* dev = NULL;
-    if ((rc = mq_malloc(&dev, n * sizeof(int32_t)))) {
+    if ((rc = mq_pool_malloc(&dev, n * sizeof(int32_t)))) {
         free(host);
         fail(st, "shadow allocation", rc);
         return NULL;
     }
     if (n && (rc = mq_memcpy_d2d(dev, d_src, n * sizeof(int32_t), g_stream))) {
-        mq_free(dev);
+        mq_pool_free(dev);
         free(host);
         fail(st, "shadow copy", rc);
         return NULL;
@@ -386,15 +400,15 @@ Result* select_column_sorted_index(Column* column, int low, int high, Status* re
     for (int i = 0; i < g_nidx; i++)
         if (g_idx[i].index == ix) e = &g_idx[i];
     if (e && (e->values != ix->values || e->positions != ix->positions || e->rows != n)) {
-        mq_free(e->d_values);
-        mq_free(e->d_positions);
+        mq_pool_free(e->d_values);
+        mq_pool_free(e->d_positions);
         *e = g_idx[--g_nidx];
         e = NULL;
     }
     if (!e) {
         if (g_nidx == MAX_INDEXES) {
-            mq_free(g_idx[0].d_values);
-            mq_free(g_idx[0].d_positions);
+            mq_pool_free(g_idx[0].d_values);
+            mq_pool_free(g_idx[0].d_positions);
             g_idx[0] = g_idx[--g_nidx];
         }
         IndexEntry ne = {ix, ix->values, ix->positions, n, NULL, NULL};
@@ -403,8 +417,8 @@ Result* select_column_sorted_index(Column* column, int low, int high, Status* re
             (rc = mq_malloc(&ne.d_positions, n * sizeof(uint64_t))) ||
             (n && (rc = h2d(ne.d_values, ix->values, n * sizeof(int32_t)))) ||
             (n && (rc = h2d(ne.d_positions, ix->positions, n * sizeof(uint64_t))))) {
-            mq_free(ne.d_values);
-            mq_free(ne.d_positions);
+            mq_pool_free(ne.d_values);
+            mq_pool_free(ne.d_positions);
             fail(ret_status, "index upload", rc);
             return NULL;
         }
@@ -603,10 +617,10 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
         }
         int rc = grow(&g_ws, &g_ws_bytes, mq_shared_select_workspace_bytes(n, q));
         if (!rc) rc = mq_shared_select_count(dcol, n, lows, highs, q, k, g_ws, g_ws_bytes, g_stream);
-        for (int j = 0; !rc && j < q; j++) rc = mq_malloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
+        for (int j = 0; !rc && j < q; j++) rc = mq_pool_malloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
         if (!rc) rc = mq_shared_select_write(g_ws, (int32_t* const*)dev, g_stream);
         for (int j = 0; !rc && j < q; j++) {
-            int32_t* host = (int32_t*)malloc((k[j] ? k[j] : 1) * sizeof(int32_t));
+            int32_t* host = (int32_t*)payload_alloc((size_t)k[j] * sizeof(int32_t));
             if (k[j] && (rc = d2h(host, dev[j], (size_t)k[j] * sizeof(int32_t)))) {
                 free(host);
                 break;
@@ -616,7 +630,7 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
             out[q0 + j] = new_result(INT, (size_t)k[j], host);
             done = q0 + j + 1;
         }
-        for (int j = 0; j < q; j++) mq_free(dev[j]);
+        for (int j = 0; j < q; j++) mq_pool_free(dev[j]);
         if (rc) {
             fail(ret_status, "shared_select", rc);
             for (int j = 0; j < done; j++) {
@@ -639,13 +653,13 @@ static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, con
     int rc = mq_join_build(d1, dp1, n1, &jn, g_stream);
     if (!rc) rc = mq_join_probe(jn, d2, n2, &m, g_stream);
     if (!rc && m) {
-        if (!(rc = mq_malloc(&o1, m * sizeof(int32_t))) && !(rc = mq_malloc(&o2, m * sizeof(int32_t))))
+        if (!(rc = mq_pool_malloc(&o1, m * sizeof(int32_t))) && !(rc = mq_pool_malloc(&o2, m * sizeof(int32_t))))
             rc = mq_join_write(jn, dp2, (int32_t*)o1, (int32_t*)o2, g_stream);
     }
     mq_join_free(jn);
     if (rc) {
-        mq_free(o1);
-        mq_free(o2);
+        mq_pool_free(o1);
+        mq_pool_free(o2);
         fail(st, "hash_join", rc);
         return NULL;
     }
@@ -653,8 +667,8 @@ static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, con
     out[0] = int_result_from_device(swap ? o2 : o1, (size_t)m, st);
     out[1] = int_result_from_device(swap ? o1 : o2, (size_t)m, st);
     mq_stream_sync(g_stream);
-    mq_free(o1);
-    mq_free(o2);
+    mq_pool_free(o1);
+    mq_pool_free(o2);
     if (!out[0] || !out[1]) {
         st->code = ERROR;
         return NULL;
@@ -716,14 +730,14 @@ static int print_gpu(const Result* r, char* dst, size_t* len, Status* st) {
     const size_t need_out = (size_t)n * 12, need_ws = mq_format_workspace_bytes(n);
     int rc;
     if (g_print_out_cap < need_out) {
-        mq_free(g_print_out);
+        mq_pool_free(g_print_out);
         g_print_out = NULL;
         g_print_out_cap = 0;
         if ((rc = mq_malloc(&g_print_out, need_out))) return fail(st, "print: device buffer", rc);
         g_print_out_cap = need_out;
     }
     if (g_print_ws_cap < need_ws) {
-        mq_free(g_print_ws);
+        mq_pool_free(g_print_ws);
         g_print_ws = NULL;
         g_print_ws_cap = 0;
         if ((rc = mq_malloc(&g_print_ws, need_ws))) return fail(st, "print: workspace", rc);
@@ -842,13 +856,13 @@ Result* get_hashset_elements(hashset* set) {
                 !(rc = read_count(&k, &st))) {
                 int32_t* host = (int32_t*)malloc((k ? k : 1) * sizeof(int32_t));
                 if (!(rc = k ? d2h(host, d_out, k * sizeof(int32_t)) : 0)) {
-                    mq_free(d_tab);
+                    mq_pool_free(d_tab);
                     return new_result(INT, k, host);
                 }
                 free(host);
             }
         }
-        if (d_tab) mq_free(d_tab);
+        if (d_tab) mq_pool_free(d_tab);
         fail(NULL, "get_hashset_elements on the GPU", rc ? rc : MQ_EHIP);
         return NULL;
     }
@@ -1024,10 +1038,10 @@ void load_db(Db* db, const char* path, Status* ret_status) {
     table->row_count = total;
 out:
     for (int j = 0; j < ncols && j < 1024; j++)
-        if (dcol[j]) mq_free(dcol[j]);
-    if (d_text) mq_free(d_text);
-    if (d_ws) mq_free(d_ws);
-    if (d_mm) mq_free(d_mm);
+        if (dcol[j]) mq_pool_free(dcol[j]);
+    if (d_text) mq_pool_free(d_text);
+    if (d_ws) mq_pool_free(d_ws);
+    if (d_mm) mq_pool_free(d_mm);
     munmap((void*)text, n);
 }
 
@@ -1046,14 +1060,14 @@ _Static_assert(sizeof(MqHistogram) == 1208, "Histogram size");
 static void idx_put(ColumnIndex* ix, size_t n, void* d_values, void* d_positions) {
     for (int i = 0; i < g_nidx; i++)
         if (g_idx[i].index == ix) {
-            mq_free(g_idx[i].d_values);
-            mq_free(g_idx[i].d_positions);
+            mq_pool_free(g_idx[i].d_values);
+            mq_pool_free(g_idx[i].d_positions);
             g_idx[i] = g_idx[--g_nidx];
             break;
         }
     if (g_nidx == MAX_INDEXES) {
-        mq_free(g_idx[0].d_values);
-        mq_free(g_idx[0].d_positions);
+        mq_pool_free(g_idx[0].d_values);
+        mq_pool_free(g_idx[0].d_positions);
         g_idx[0] = g_idx[--g_nidx];
     }
     g_idx[g_nidx++] = (IndexEntry){ix, ix->values, ix->positions, n, d_values, d_positions};
@@ -1090,7 +1104,7 @@ static int index_one(Table* t, Column* c, Status* st) {
             if ((rc = mq_malloc(&dnew, (n ? n : 1) * 4))) goto bad;
             if ((rc = mq_gather_u64(dsrc, (const uint64_t*)dp, n, dnew, g_stream)) ||
                 (n && (rc = d2h(o->data, dnew, n * 4)))) {
-                mq_free(dnew);
+                mq_pool_free(dnew);
                 goto bad;
             }
             col_put(o, dnew); /* the reordered rows stay resident */
@@ -1130,15 +1144,15 @@ static int index_one(Table* t, Column* c, Status* st) {
     ix->positions = hp;
     c->index = ix;
     idx_put(ix, n, dv, dp); /* resident for select_column_sorted_index */
-    mq_free(dh);
+    mq_pool_free(dh);
     return 0;
 bad:
     free(ix);
     free(hv);
     free(hp);
-    mq_free(dv);
-    mq_free(dp);
-    mq_free(dh);
+    mq_pool_free(dv);
+    mq_pool_free(dp);
+    mq_pool_free(dh);
     fail(st, "build_index", rc);
     return rc;
 }
@@ -1188,15 +1202,15 @@ const void* mq_result_device_ptr(const Result* result) {
 
 void mq_release_all(void) {
     mq_trim();
-    mq_free(g_print_out);
-    mq_free(g_print_ws);
+    mq_pool_free(g_print_out);
+    mq_pool_free(g_print_ws);
     g_print_out = g_print_ws = NULL;
     g_print_out_cap = g_print_ws_cap = 0;
     while (g_ncols) col_drop(&g_cols[g_ncols - 1]);
     while (g_nshadows) shadow_drop(g_nshadows - 1);
     while (g_nidx) {
-        mq_free(g_idx[g_nidx - 1].d_values);
-        mq_free(g_idx[g_nidx - 1].d_positions);
+        mq_pool_free(g_idx[g_nidx - 1].d_values);
+        mq_pool_free(g_idx[g_nidx - 1].d_positions);
         g_nidx--;
     }
 }

@@ -427,7 +427,65 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
     out["load_csv_config3_table"] = load_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["index_build"] = index_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
+    out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
     return out
+
+
+def api_leg(lib, mq, n, lo, hi, gold) -> dict:
+    """Config 3 through the drop-in C API as the reference server calls it
+    (server.c:137-247): host Columns (malloc'd like the mmap'd column files),
+    select_column(col0) -> fetch_column(col1, positions) -> average, Result*
+    handed from call to call. Reports the PCIe-inclusive times: the one-off H2D
+    of each 4 GB column (column residency), then the chain on resident columns,
+    whose results come back to host memory as the reference's API requires."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refcpu  # input generator only (the §8(c) column, on the host)
+    from refapi import make_column, _libc
+    c0 = refcpu.gen_uniform(n, 42, nthreads=16)
+    c1 = refcpu.gen_uniform(n, 43, nthreads=16)
+    col0, col1 = make_column(c0, b"col0"), make_column(c1, b"col1")
+    t0 = time.perf_counter()
+    mq.check(lib.mq_column_upload(C.byref(col0)), "upload col0")
+    mq.check(lib.mq_column_upload(C.byref(col1)), "upload col1")
+    t_up = time.perf_counter() - t0
+    lo_c, hi_c = C.c_int(lo), C.c_int(hi)
+    times = {"select_column": [], "fetch_column": [], "average": []}
+    avg = None
+    k = 0
+    for rep in range(4):
+        st = mq.Status(0, None)
+        lib.mq_transfer_seconds(1)
+        t0 = time.perf_counter()
+        rp = lib.select_column(C.byref(col0), C.byref(lo_c), C.byref(hi_c), C.byref(st))
+        t1 = time.perf_counter()
+        rf = lib.fetch_column(C.byref(col1), rp, C.byref(st))
+        t2 = time.perf_counter()
+        ra = lib.average(rf, C.byref(st))
+        t3 = time.perf_counter()
+        assert st.code == mq.OK
+        xfer = lib.mq_transfer_seconds(0)
+        k = rp.contents.num_tuples
+        avg = C.cast(ra.contents.payload, C.POINTER(C.c_double))[0]
+        for r in (rp, rf, ra):
+            _libc.free(r.contents.payload)
+            _libc.free(r)
+        if rep:
+            times["select_column"].append(t1 - t0)
+            times["fetch_column"].append(t2 - t1)
+            times["average"].append(t3 - t2)
+    med = {f"ms_{name}": 1e3 * statistics.median(v) for name, v in times.items()}
+    chain_s = sum(med.values()) / 1e3
+    want = next((r for r in gold["config3"] if r["n"] == n and r["low"] == lo and r["high"] == hi), None)
+    res = {"rows": n, "k": k, "avg": avg, "ms_upload_two_columns": 1e3 * t_up,
+           "upload_gbs": 8.0 * n / t_up / 1e9, **med, "ms_chain": 1e3 * chain_s,
+           "rows_per_s_chain": n / chain_s, "ms_transfer_last_chain": 1e3 * xfer,
+           "note": "PCIe-inclusive: each operator returns malloc'd host payloads (client_context.c "
+                   "frees them); the chain runs on HBM-resident columns after the one-off upload"}
+    if want is not None:
+        res["parity"] = (k, avg) == (want["k"], want["avg"])
+    return res
 
 
 def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:

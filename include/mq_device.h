@@ -58,6 +58,12 @@ void* mq_default_stream(void);
 /* Release the device scratch libmq keeps cached between calls (join tables and
  * partition buffers, probe arrays); the next call allocates afresh. */
 void mq_trim(void);
+/* The same caching allocator for callers (the query layer keeps result shadows
+ * and column copies in it): a freed block may be handed out again at once, so
+ * free only what no queued work still uses. mq_pool_free also accepts pointers
+ * from mq_malloc (it frees those at once). */
+int mq_pool_malloc(void** dptr, size_t bytes);
+int mq_pool_free(void* dptr);
 
 /* Workspace (device bytes) needed by the scan entry points for n rows. */
 size_t mq_scan_workspace_bytes(uint64_t n);
