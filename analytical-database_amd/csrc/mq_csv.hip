@@ -637,7 +637,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
     __shared__ long long s_w[kWaves];
     __shared__ uint32_t s_u[kWaves];
     extern __shared__ int s_mm[];  // 2 * ncols: min, max
-    const uint64_t c = blockIdx.x, cs = c * kChunk;
+    const uint64_t c = xcd_tile(blockIdx.x, gridDim.x), cs = c * kChunk;  // XCD-contiguous chunks: halo reads and shared column lines meet in one L2
     const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
     const int tid = threadIdx.x, lane = tid & 63;
     const bool lmode = __builtin_amdgcn_readfirstlane(flags[F_LONG]) != 0;
