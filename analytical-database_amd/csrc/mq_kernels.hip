@@ -1483,8 +1483,10 @@ int blocks_per_cu(const void* fn) {
     };
     static Entry cache[64];
     static int ncache = 0;
+    static std::mutex mu;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(mu);
     for (int i = 0; i < ncache; i++)
         if (cache[i].dev == dev && cache[i].fn == fn) return cache[i].occ;
     int occ = 0;
