@@ -546,10 +546,11 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
 
 // kProbeILP probes per thread per step: the keys are loaded coalesced, then all
 // their home buckets (4 slots, 32 B, two 16-byte loads) are requested before any
-// is examined, so a wave keeps 64 x kProbeILP random reads in flight (one at a
-// time measured 8.4 ms at 2^28). Only a full bucket without the key continues
-// along the window, slot by slot.
-constexpr int kProbeILP = 8;
+// is examined. Only a full bucket without the key continues along the window,
+// slot by slot. With whole-bucket loads 2 probes per thread beat 8 (8.25 vs
+// 8.8 ms at 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8
+// had beaten 1 (7.9 vs 8.4 ms).
+constexpr int kProbeILP = 2;
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,

@@ -4,6 +4,7 @@ a host sync), median of reps; M checked against the golden."""
 import ctypes as C
 import json
 import statistics
+import os
 import sys
 import time
 
@@ -11,7 +12,7 @@ sys.path[:0] = ["tests", "oracle"]
 import torch  # noqa: E402
 from refapi import mq  # noqa: E402
 
-L = mq.load()
+L = mq.load(os.environ['MQ_LIB']) if os.environ.get('MQ_LIB') else mq.load()
 mq.check(L.mq_init(0))
 logn = int(sys.argv[1]) if len(sys.argv) > 1 else 28
 n = 1 << logn
