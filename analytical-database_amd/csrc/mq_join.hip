@@ -167,14 +167,18 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1,
     __syncthreads();
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
     const uint64_t base = (uint64_t)tile * kSortTile;
+    // all of the lane's items are loaded before any is counted (indices clamped,
+    // no branch), so the loads share one round trip instead of one each
+    uint32_t key[kSortItems];
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
-        if (i < n) {
-            const uint32_t key = FIRST ? ((uint32_t)c1[i] ^ 0x80000000u) : (uint32_t)in[i];
-            atomicAdd(&h[(key >> shift) & 0xFF], 1u);
-        }
+        const uint64_t ic = i < n ? i : n - 1;
+        key[k] = FIRST ? ((uint32_t)c1[ic] ^ 0x80000000u) : (uint32_t)in[ic];
     }
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++)
+        if (base + (uint64_t)k * kTPB + threadIdx.x < n) atomicAdd(&h[(key[k] >> shift) & 0xFF], 1u);
     __syncthreads();
     hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
@@ -203,11 +207,17 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
     uint32_t dr[kSortItems];
+    // all items loaded first (indices clamped, no branch): one round trip, not one
+    // per item (the ranking's ballots kept the compiler from hoisting the loads)
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        el[k] = sort_word<FIRST>(c1, p1, in, i < n ? i : n - 1);
+    }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool valid = i < n;
-        el[k] = valid ? sort_word<FIRST>(c1, p1, in, i) : 0ull;
         const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
@@ -397,14 +407,16 @@ __global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
     __syncthreads();
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
     const uint64_t base = (uint64_t)tile * kSortTile;
+    uint32_t key[kSortItems];  // loaded before any is counted, as in k_sortw_hist
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
-        if (i < n) {
-            const uint32_t key = FROM_COLS ? (uint32_t)c1[i] : (uint32_t)in[i];
-            atomicAdd(&h[(win_id(key, t) >> shift) & 0xFF], 1u);
-        }
+        const uint64_t ic = i < n ? i : n - 1;
+        key[k] = FROM_COLS ? (uint32_t)c1[ic] : (uint32_t)in[ic];
     }
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++)
+        if (base + (uint64_t)k * kTPB + threadIdx.x < n) atomicAdd(&h[(win_id(key[k], t) >> shift) & 0xFF], 1u);
     __syncthreads();
     hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
@@ -433,11 +445,17 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
     uint32_t dr[kSortItems];
+    // all items loaded first (indices clamped, no branch): one round trip, not one
+    // per item (the ranking's ballots kept the compiler from hoisting the loads)
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        el[k] = win_elem<FROM_COLS>(c1, p1, in, i < n ? i : n - 1);
+    }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool valid = i < n;
-        el[k] = valid ? win_elem<FROM_COLS>(c1, p1, in, i) : 0ull;
         const uint32_t d = (win_id((uint32_t)el[k], t) >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
