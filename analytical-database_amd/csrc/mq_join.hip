@@ -538,8 +538,19 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
     if (e - b > W - W / 4) {  // over 3/4 full: probes would run long (adversarial keys)
         if (threadIdx.x == 0) *general = 1;
     } else {
-        for (uint32_t i = b + threadIdx.x; i < e; i += kWinTPB) {
-            const u64 v = in[i];
+        // at most 3/4 of W words: every thread's (<= W / kWinTPB) words are loaded
+        // before any is inserted (one round trip, not one per word)
+        constexpr int kPer = (1 << kWinLog) / kWinTPB;
+        u64 vs[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t i = b + threadIdx.x + (uint32_t)k * kWinTPB;
+            vs[k] = i < e ? in[i] : kEmpty;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (b + threadIdx.x + (uint32_t)k * kWinTPB >= e) break;
+            const u64 v = vs[k];
             if (v == kEmpty) {
                 *general = 1;
                 continue;
