@@ -1087,26 +1087,47 @@ __global__ __launch_bounds__(kTPB) void k_hashset_lookup(const int32_t* __restri
 // fetch (query.c:223-243): out[i] = col[pos[i]], 4 positions per lane.
 // ---------------------------------------------------------------------------
 template <bool VEC>
+__device__ __forceinline__ void store4(int* __restrict__ p, int4 v) {
+    if constexpr (VEC) {
+        *reinterpret_cast<int4*>(p) = v;
+    } else {
+        p[0] = v.x;
+        p[1] = v.y;
+        p[2] = v.z;
+        p[3] = v.w;
+    }
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_fetch(const int* __restrict__ col,
                                                 const int* __restrict__ pos, uint64_t k,
                                                 int* __restrict__ out) {
+    // kFetchU groups of 4 positions per lane per step: all position loads, then all
+    // 4 x kFetchU gathers, are in flight before any result is used (one group at a
+    // time left the lane with two serial round trips per 4 gathers). The main loop
+    // runs whole steps only: no guard inside, so the compiler cannot sink the loads
+    // back to their stores.
+    constexpr int kFetchU = 4;
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     const uint64_t k4 = k / 4;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < k4; i += stride) {
-        const int4 p = load4<VEC>(pos + i * 4);
-        int4 o;
-        o.x = col[p.x];
-        o.y = col[p.y];
-        o.z = col[p.z];
-        o.w = col[p.w];
-        if constexpr (VEC) {
-            *reinterpret_cast<int4*>(out + i * 4) = o;
-        } else {
-            out[i * 4 + 0] = o.x;
-            out[i * 4 + 1] = o.y;
-            out[i * 4 + 2] = o.z;
-            out[i * 4 + 3] = o.w;
+    uint64_t i0 = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+    for (; i0 + (uint64_t)(kFetchU - 1) * stride < k4; i0 += stride * kFetchU) {
+        int4 p[kFetchU], o[kFetchU];
+#pragma unroll
+        for (int u = 0; u < kFetchU; u++) p[u] = load4<VEC>(pos + (i0 + (uint64_t)u * stride) * 4);
+#pragma unroll
+        for (int u = 0; u < kFetchU; u++) {
+            o[u].x = col[p[u].x];
+            o[u].y = col[p[u].y];
+            o[u].z = col[p[u].z];
+            o[u].w = col[p[u].w];
         }
+#pragma unroll
+        for (int u = 0; u < kFetchU; u++) store4<VEC>(out + (i0 + (uint64_t)u * stride) * 4, o[u]);
+    }
+    for (; i0 < k4; i0 += stride) {  // the last partial step, one group at a time
+        const int4 p = load4<VEC>(pos + i0 * 4);
+        store4<VEC>(out + i0 * 4, make_int4(col[p.x], col[p.y], col[p.z], col[p.w]));
     }
     if (blockIdx.x == 0 && threadIdx.x < (k & 3)) {
         const uint64_t i = k4 * 4 + threadIdx.x;
