@@ -247,6 +247,17 @@ __device__ __forceinline__ int ei_of(int32_t v, const EiMeta& M, const uint32_t*
     return lo;
 }
 
+// The bucket table into LDS: all of a thread's 16 entries are loaded before any
+// is stored (a load/store loop paid 16 round trips per block before its scan).
+__device__ __forceinline__ void stage_buckets(const uint32_t* __restrict__ g, uint32_t* s, int tid) {
+    constexpr int kPer = kBuckets / kTPB;
+    uint32_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) v[k] = g[tid + k * kTPB];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) s[tid + k * kTPB] = v[k];
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ssi_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q,
@@ -256,7 +267,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_count(const int* __restrict__ col,
     __shared__ uint32_t s_qoff[kEiMax];
     __shared__ uint32_t hist[kWaves][kEiMax];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < kBuckets; i += kTPB) s_bkt[i] = T.bucket[i];
+    stage_buckets(T.bucket, s_bkt, tid);
     for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
     for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
     for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
@@ -327,7 +338,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
     __shared__ uint32_t pairs[kWaves][kPairCap];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int i = tid; i < kBuckets; i += kTPB) s_bkt[i] = T.bucket[i];
+    stage_buckets(T.bucket, s_bkt, tid);
     for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
     for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
     for (int i = tid; i < q; i += kTPB) {
