@@ -55,11 +55,15 @@ template <typename Tin>
 __global__ __launch_bounds__(kTPB) void k_tile_sum(const Tin* in, uint64_t n, u64* sums) {
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
     u64 acc = 0;
+    Tin v[kScanItems];  // all loads in flight first (clamped index, no branch)
 #pragma unroll
     for (int k = 0; k < kScanItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
-        if (i < n) acc += (u64)in[i];
+        v[k] = in[i < n ? i : n - 1];
     }
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++)
+        if (base + (uint64_t)k * kTPB + threadIdx.x < n) acc += (u64)v[k];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     __shared__ u64 ws[kTPB / 64];
@@ -76,10 +80,16 @@ __global__ __launch_bounds__(kTPB) void k_tile_scan(const Tin* in, u64* out, uin
     __shared__ u64 ws[kTPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    {
+        Tin x[kScanItems];  // all loads in flight first (clamped index, no branch)
 #pragma unroll
-    for (int k = 0; k < kScanItems; k++) {
-        const uint64_t i = base + (uint64_t)k * kTPB + tid;
-        tile[k * kTPB + tid] = i < n ? (u64)in[i] : 0ull;
+        for (int k = 0; k < kScanItems; k++) {
+            const uint64_t i = base + (uint64_t)k * kTPB + tid;
+            x[k] = in[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < kScanItems; k++)
+            tile[k * kTPB + tid] = base + (uint64_t)k * kTPB + tid < n ? (u64)x[k] : 0ull;
     }
     __syncthreads();
     u64 v[kScanItems];
