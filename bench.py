@@ -99,7 +99,17 @@ def cpu_baseline(rows: int) -> dict:
                       f"fetch -> sum, {'oracle/_ref/libref.so (reference query.c, gcc -O2)' if kind == 'reference' else 'oracle/refcpu.c -O2'}, "
                       f"median of 3 = {t1:.3f} s",
             "variants": variants,
-            "nproc": os.cpu_count()}
+            "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main() -> None:
