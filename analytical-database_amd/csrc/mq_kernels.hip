@@ -1028,21 +1028,39 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         const unsigned long long ol = o + (incl - c);
         const uint64_t row0 = T * 256;
         if (tot > 1024) {
-            // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e)
-            for (int j = 0; j < 64; j++) {
-                if (__shfl(c, j, 64) == 0) continue;
-                const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
-                                         x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
-                const unsigned long long oj = __shfl(ol, j, 64);
-                const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
-                const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
-                                                        __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
-                int* q = out + oj + pre;
-                unsigned int k = 0;
-                if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 0] : (int)(rj + 0);
-                if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 1] : (int)(rj + 1);
-                if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 2] : (int)(rj + 2);
-                if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 3] : (int)(rj + 3);
+            // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e).
+            // select_result: the payload rows of 4 tiles are loaded (indices clamped)
+            // before any of them is written; gathering at each write made every
+            // tile wait for its own round trip (10-50 % selectivity ran at twice the
+            // positions-only time)
+            constexpr int kPf = 4;  // tiles per payload batch (registers: launch bounds 8 waves)
+            for (int j0 = 0; j0 < 64; j0 += kPf) {
+                int pv[kPf][4];
+                if constexpr (PAYLOAD) {
+#pragma unroll
+                    for (int jj = 0; jj < kPf; jj++) {
+                        const uint64_t rj = __shfl(row0, j0 + jj, 64) + 4 * (uint64_t)lane;
+#pragma unroll
+                        for (int e = 0; e < 4; e++) pv[jj][e] = payload[rj + e < n ? rj + e : n - 1];
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < kPf; jj++) {
+                    const int j = j0 + jj;
+                    if (__shfl(c, j, 64) == 0) continue;
+                    const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
+                                             x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
+                    const unsigned long long oj = __shfl(ol, j, 64);
+                    const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
+                    const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
+                                                            __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
+                    int* q = out + oj + pre;
+                    unsigned int k = 0;
+                    if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][0] : (int)(rj + 0);
+                    if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][1] : (int)(rj + 1);
+                    if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][2] : (int)(rj + 2);
+                    if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][3] : (int)(rj + 3);
+                }
             }
         } else if (c) {
             // sparse: each lane emits its own tile's rows in order
