@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
 //          the tile) gives its slot after the query's running offset. Tiles with
 //          many pairs (dense queries) take the per-query ballot loop instead.
 // ---------------------------------------------------------------------------
-constexpr int kEiMinQ = 24;
+constexpr int kEiMinQ = 12;  // measured crossover (count + write, 1e9 rows): Q=8 ballots 2.65 vs 3.25 ms, Q=12 3.63 vs 3.48, Q=16 4.64 vs 3.62
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
@@ -594,7 +594,8 @@ int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int3
     }
     char* w = static_cast<char*>(d_ws);
     const bool vec = aligned16(d_col);
-    const bool ei = qk >= kEiMinQ && getenv("MQ_SS_IMPL") == nullptr;  // MQ_SS_IMPL=ballot: A/B
+    const char* emin = getenv("MQ_SS_EI_MIN");  // A/B of the threshold
+    const bool ei = qk >= (emin ? atoi(emin) : kEiMinQ) && getenv("MQ_SS_IMPL") == nullptr;  // MQ_SS_IMPL=ballot: A/B
     const void* fn = ei ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
                         : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
     uint32_t g = 1;
