@@ -595,25 +595,31 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                                                           uint32_t* __restrict__ pstart,
                                                           uint32_t* __restrict__ plen) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB * kProbeILP;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x; j0 < n2; j0 += stride) {
+    uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x;
+    // the next step's keys are loaded while this step's buckets are in flight;
+    // indices are clamped (no branch) so nothing serialises the loads
+    uint32_t knext[kProbeILP];
+#pragma unroll
+    for (int u = 0; u < kProbeILP; u++) {
+        const uint64_t j = j0 + (uint64_t)u * kTPB;
+        knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
+    }
+    for (; j0 < n2; j0 += stride) {
         uint32_t key[kProbeILP];
         uint64_t h[kProbeILP];
         ulonglong2 b0[kProbeILP], b1[kProbeILP];  // the home bucket, slots 0-1 and 2-3
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
-            const uint64_t j = j0 + (uint64_t)u * kTPB;
-            key[u] = j < n2 ? (uint32_t)pkeys[j] : 0u;
+            key[u] = knext[u];
+            h[u] = ht_home(key[u], t.mask);
+            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(words + h[u]);
+            b0[u] = q[0];
+            b1[u] = q[1];
         }
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
-            h[u] = ht_home(key[u], t.mask);
-            if (j0 + (uint64_t)u * kTPB < n2) {
-                const ulonglong2* q = reinterpret_cast<const ulonglong2*>(words + h[u]);
-                b0[u] = q[0];
-                b1[u] = q[1];
-            } else {
-                b0[u] = b1[u] = make_ulonglong2(kEmpty, kEmpty);
-            }
+            const uint64_t j = j0 + stride + (uint64_t)u * kTPB;
+            knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
         }
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
