@@ -50,6 +50,30 @@ __global__ __launch_bounds__(256) void k_read(const unsigned long long* __restri
     if (acc == 0x123456789ull) out[0] = acc;  // keep the loads
 }
 
+// the join probe's pattern: a 32-byte bucket as two 16-byte loads (MODE 2) or one
+// 16-byte load (MODE 1) per read, from a key loaded from memory first (DEP)
+template <int MODE, bool DEP>
+__global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __restrict__ t, uint64_t mask, uint64_t p,
+                                                const unsigned* __restrict__ keys, unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 2;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * 256 * 2 + threadIdx.x; j0 < p; j0 += stride) {
+        ulonglong2 a[2], b[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint64_t j = j0 + (uint64_t)u * 256;
+            const unsigned k = DEP ? keys[j < p ? j : p - 1] : (unsigned)j;
+            const uint64_t h = (uint64_t)mix(k) & mask & ~3ull;
+            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t + h);
+            a[u] = q[0];
+            b[u] = MODE == 2 ? q[1] : make_ulonglong2(0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) acc ^= a[u].x ^ a[u].y ^ b[u].x ^ b[u].y;
+    }
+    if (acc == 0x123456789ull) out[0] = acc;
+}
+
 template <int ILP, bool RANDOM>
 float run(const unsigned long long* t, uint64_t mask, uint64_t p, unsigned long long* o, int grid) {
     hipEvent_t a, b;
@@ -79,7 +103,37 @@ int main(int argc, char** argv) {
     hipDeviceProp_t pr;
     CK(hipGetDeviceProperties(&pr, 0));
     const int cus = pr.multiProcessorCount;
-    for (int grid_mul : {8, 16, 32}) {
+    {
+        unsigned* keys;
+        CK(hipMalloc(&keys, P * 4));
+        {
+            std::vector<unsigned> hk(P);
+            for (uint64_t i = 0; i < P; i++) hk[i] = (unsigned)(i * 2654435761u);
+            CK(hipMemcpy(keys, hk.data(), P * 4, hipMemcpyHostToDevice));
+        }
+        const int grid = cus * 8;
+        auto tb = [&](auto kern) {
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            std::vector<float> ms;
+            for (int r = 0; r < 7; r++) {
+                CK(hipEventRecord(a));
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, t, S - 1, P, keys, o);
+                CK(hipEventRecord(b));
+                CK(hipEventSynchronize(b));
+                float x;
+                CK(hipEventElapsedTime(&x, a, b));
+                if (r >= 2) ms.push_back(x);
+            }
+            std::sort(ms.begin(), ms.end());
+            return ms[ms.size() / 2];
+        };
+        printf("{\"bucket_1x16\": %.3f, \"bucket_2x16\": %.3f, \"bucket_2x16_key_loaded\": %.3f}\n",
+               tb(k_bucket<1, false>), tb(k_bucket<2, false>), tb(k_bucket<2, true>));
+        CK(hipFree(keys));
+    }
+    for (int grid_mul : {8}) {
         const int grid = cus * grid_mul;
         const float r1 = run<1, true>(t, S - 1, P, o, grid), r4 = run<4, true>(t, S - 1, P, o, grid),
                     r8 = run<8, true>(t, S - 1, P, o, grid), r16 = run<16, true>(t, S - 1, P, o, grid),
