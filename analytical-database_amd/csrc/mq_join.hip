@@ -593,7 +593,7 @@ constexpr int kProbeILP = 2;
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
-                                                          uint32_t* __restrict__ plen) {
+                                                          u64* __restrict__ hits) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB * kProbeILP;
     uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x;
     // the next step's keys are loaded while this step's buckets are in flight;
@@ -624,9 +624,8 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
-            if (j >= n2) continue;
             const u64 sl[kBucket] = {b0[u].x, b0[u].y, b1[u].x, b1[u].y};
-            bool hit = false, done = false;
+            bool hit = false, done = j >= n2;
             uint32_t payload = 0;
 #pragma unroll
             for (uint32_t i = 0; i < kBucket; i++) {
@@ -649,9 +648,39 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                     hh = win_next(hh, t);
                 }
             }
-            pstart[j] = payload;  // unique path: the build position itself
-            plen[j] = hit ? 1u : 0u;
+            // a wave's 64 lanes hold 64 consecutive rows: their hits are one word
+            const u64 m = __ballot(hit);
+            if (j < n2) {
+                if (hit) pstart[j] = payload;  // the build position itself
+                if ((threadIdx.x & 63) == 0) hits[j >> 6] = m;
+            }
         }
+    }
+}
+
+// Unique path, after the probe: matches per 64-row hit word (scanned into the
+// words' output offsets), then each matching row j writes its pair at its word's
+// offset + the matches below it in the word. Output in ascending j, as J1.
+__global__ __launch_bounds__(kTPB) void k_hits_count(const u64* __restrict__ hits, uint64_t nw,
+                                                     uint32_t* __restrict__ cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t w = (uint64_t)blockIdx.x * kTPB + threadIdx.x; w < nw; w += stride)
+        cnt[w] = (uint32_t)__popcll(hits[w]);
+}
+
+__global__ __launch_bounds__(kTPB) void k_join_write_hits(const u64* __restrict__ hits,
+                                                          const u64* __restrict__ woffs,
+                                                          const uint32_t* __restrict__ pstart,
+                                                          const int* __restrict__ p2, uint64_t n2,
+                                                          int* __restrict__ out1, int* __restrict__ out2) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
+        const u64 m = hits[j >> 6];
+        const uint32_t b = (uint32_t)(j & 63);
+        if (!((m >> b) & 1)) continue;
+        const u64 o = woffs[j >> 6] + (u64)__popcll(m & ((1ull << b) - 1));
+        out1[o] = (int)pstart[j];
+        out2[o] = p2[j];
     }
 }
 
@@ -732,11 +761,6 @@ __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict_
         const u64 o = offs[j];
         const uint32_t s = pstart[j];
         const int pp = p2[j];
-        if (!bpos) {  // unique-key table: pstart holds the build position (L == 1)
-            out1[o] = (int)s;
-            out2[o] = pp;
-            continue;
-        }
         for (uint32_t t = 0; t < L; t++) {
             out1[o + t] = bpos[s + t];
             out2[o + t] = pp;
@@ -1043,24 +1067,35 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     j->m = 0;
     *h_m = 0;
     if (n2 == 0 || j->n1 == 0) return MQ_OK;
+    const uint64_t nwords = (n2 + 63) / 64;
     j->pstart = (uint32_t*)pool_alloc(n2 * 4);
-    j->plen = (uint32_t*)pool_alloc(n2 * 4);
-    j->offs = (u64*)pool_alloc(n2 * 8);
-    j->scan_scratch = (u64*)pool_alloc(scan_scratch_elems(n2) * 8);
+    j->plen = (uint32_t*)pool_alloc(j->unique ? nwords * 12 : n2 * 4);
+    j->offs = (u64*)pool_alloc((j->unique ? nwords : n2) * 8);
+    j->scan_scratch = (u64*)pool_alloc(scan_scratch_elems(j->unique ? nwords : n2) * 8);
     if (!j->pstart || !j->plen || !j->offs || !j->scan_scratch)
         return set_err(MQ_ENOMEM, "mq_join_probe: buffers for %llu rows", (unsigned long long)n2);
-    if (j->unique)
+    // unique path: plen holds one 64-bit hit word per 64 rows, then those words'
+    // popcounts; offs the words' output offsets. Otherwise both are per row.
+    const uint64_t nw = (n2 + 63) / 64;
+    const uint64_t nscan = j->unique ? nw : n2;
+    uint32_t* const cnt = j->unique ? j->plen + 2 * nw : j->plen;
+    if (j->unique) {
+        u64* const hits = reinterpret_cast<u64*>(j->plen);
         hipLaunchKernelGGL(k_ht_probe_unique, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)&k_ht_probe_unique)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, j->plen);
-    else
+                           j->words, j->win, j->pstart, hits);
+        LAUNCHCHK("k_ht_probe_unique");
+        hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
+        LAUNCHCHK("k_hits_count");
+    } else {
         hipLaunchKernelGGL(k_ht_probe, dim3(stream_grid(s, n2)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->start, j->len, j->mask, j->pstart, j->plen);
-    LAUNCHCHK("k_ht_probe");
-    if ((rc = scan_exclusive<uint32_t>(j->plen, j->offs, n2, j->scan_scratch, st))) return rc;
+        LAUNCHCHK("k_ht_probe");
+    }
+    if ((rc = scan_exclusive<uint32_t>(cnt, j->offs, nscan, j->scan_scratch, st))) return rc;
     u64 last_off = 0;
     uint32_t last_len = 0;
-    HIPCHK(hipMemcpyAsync(&last_off, j->offs + (n2 - 1), 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&last_len, j->plen + (n2 - 1), 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last_off, j->offs + (nscan - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&last_len, cnt + (nscan - 1), 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     j->m = last_off + last_len;
     *h_m = j->m;
@@ -1074,6 +1109,12 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (!j) return set_err(MQ_EINVAL, "mq_join_write: NULL handle");
     if (j->m == 0) return MQ_OK;
     if (!d_p2 || !d_out1 || !d_out2) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
+    if (j->unique) {
+        hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
+                           reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
+        LAUNCHCHK("k_join_write_hits");
+        return MQ_OK;
+    }
     hipLaunchKernelGGL(k_join_write, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                        j->pstart, j->plen, j->offs, d_p2, j->bpos, j->n2, d_out1, d_out2);
     LAUNCHCHK("k_join_write");
