@@ -525,7 +525,7 @@ def _dev_join(lib, c1, p1, c2, p2):
 
 
 @pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
-                                  "unique_partitioned", "dups_partitioned"])
+                                  "unique_partitioned", "dups_partitioned", "ragged_hits"])
 def test_hash_join_vs_oracle(lib, refcpu, case):
     rng = np.random.default_rng(hash(case) % 1000)
     if case == "unique":
@@ -547,6 +547,9 @@ def test_hash_join_vs_oracle(lib, refcpu, case):
     elif case == "marker":  # unique keys, one build row {key -1, position -1} = the
         c1 = (rng.permutation(3000) - 1500).astype(np.int32)  # packed table's empty word
         c2 = rng.integers(-1600, 1600, 5000, dtype=np.int32)
+    elif case == "ragged_hits":  # unique keys, probe rows 64k+1 with hits at the word edges
+        c1 = rng.permutation(1000).astype(np.int32)
+        c2 = np.concatenate([np.arange(129), rng.integers(500, 2000, 64 * 7 + 1), [999]]).astype(np.int32)
     elif case in ("unique_partitioned", "dups_partitioned"):
         # > 2^22 build rows: the window-partitioned insert. Keys from the spread
         # config-5 generator: the oracle restates the reference's `key % size`
