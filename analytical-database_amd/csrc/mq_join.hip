@@ -517,17 +517,21 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
     }
 }
 
-// wstart[w] = first index of window w in the partitioned words (wstart[nw] = n).
+// wstart[w] = first index of window w in the partitioned words (wstart[nw] = n):
+// the words are sorted by window id, so one binary search per window boundary
+// (nw + 1 threads, ~28 dependent reads whose upper levels sit in L2) instead of a
+// pass over all n words (0.48 ms at 2^28).
 __global__ __launch_bounds__(kTPB) void k_win_bounds(const u64* __restrict__ in, uint64_t n, Win t,
                                                      uint32_t nw, uint32_t* __restrict__ wstart) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        const uint32_t w = win_id((uint32_t)in[i], t);
-        const uint32_t wp = i ? win_id((uint32_t)in[i - 1], t) + 1 : 0u;
-        for (uint32_t x = wp; x <= w; x++) wstart[x] = (uint32_t)i;
-        if (i == n - 1)
-            for (uint32_t x = w + 1; x <= nw; x++) wstart[x] = (uint32_t)n;
+    const uint32_t x = blockIdx.x * kTPB + threadIdx.x;
+    if (x > nw) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (win_id((uint32_t)in[mid], t) < x) lo = mid + 1;
+        else hi = mid;
     }
+    wstart[x] = (uint32_t)lo;
 }
 
 // One block per window: insert the window's words into an LDS table with LDS CAS,
@@ -885,7 +889,7 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
         src = dst;
         dst = (dst == a) ? b : a;
     }
-    hipLaunchKernelGGL(k_win_bounds, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, src, n, t, nw, wstart);
+    hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
     hipLaunchKernelGGL(k_win_build, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, t, general);
     if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window build"));
     // the temporaries are released only after the build has run
