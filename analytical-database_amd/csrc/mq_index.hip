@@ -33,11 +33,32 @@ using namespace mqi;
 constexpr int kTPB = 256;
 constexpr int kBins = 100;  // BIN_NUM (cs165_api.h:46)
 
+// kGatherU rows per lane per step: their positions are loaded, then all their
+// random reads are in flight before any is stored (a plain grid-stride loop waits
+// out two dependent HBM round trips per row). Full steps carry no guards; the one
+// partial step at the end does.
+constexpr int kGatherU = 8;
 __global__ __launch_bounds__(kTPB) void k_gather_u64(const int32_t* __restrict__ col,
                                                       const unsigned long long* __restrict__ pos,
                                                       uint64_t n, int32_t* __restrict__ out) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] = col[pos[i]];
+    const uint64_t step = (uint64_t)gridDim.x * kTPB * kGatherU;
+    uint64_t i0 = (uint64_t)blockIdx.x * kTPB * kGatherU + threadIdx.x;
+    for (; i0 + (uint64_t)(kGatherU - 1) * kTPB < n; i0 += step) {
+        unsigned long long p[kGatherU];
+        int32_t v[kGatherU];
+#pragma unroll
+        for (int u = 0; u < kGatherU; u++) p[u] = pos[i0 + (uint64_t)u * kTPB];
+#pragma unroll
+        for (int u = 0; u < kGatherU; u++) v[u] = col[p[u]];
+#pragma unroll
+        for (int u = 0; u < kGatherU; u++) out[i0 + (uint64_t)u * kTPB] = v[u];
+    }
+    // i0 + step > n here, so this partial step is the last one
+#pragma unroll
+    for (int u = 0; u < kGatherU; u++) {
+        const uint64_t i = i0 + (uint64_t)u * kTPB;
+        if (i < n) out[i] = col[pos[i]];
+    }
 }
 
 // build_histogram (index.c:63-84): bin of a row = (data - min) / bin_size, an int
@@ -82,7 +103,7 @@ int mq_gather_u64(const int32_t* d_col, const uint64_t* d_positions, uint64_t n,
     if (rc) return rc;
     if (n && (!d_col || !d_positions || !d_out)) return set_err(MQ_EINVAL, "mq_gather_u64: NULL pointer");
     if (n == 0) return MQ_OK;
-    hipLaunchKernelGGL(k_gather_u64, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream, d_col,
+    hipLaunchKernelGGL(k_gather_u64, dim3(stream_grid(s, (n + kGatherU - 1) / kGatherU)), dim3(kTPB), 0, (hipStream_t)stream, d_col,
                        reinterpret_cast<const unsigned long long*>(d_positions), n, d_out);
     LAUNCHCHK("k_gather_u64");
     return MQ_OK;

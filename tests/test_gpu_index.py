@@ -47,10 +47,12 @@ def test_index_build_vs_oracle(lib, refcpu, n, lo, hi):
 def test_gather_and_histogram_vs_oracle(lib, refcpu):
     rng = np.random.default_rng(9)
     col = rng.integers(-10**6, 10**6, 300_000).astype(np.int32)
-    pos = rng.integers(0, len(col), 200_000).astype(np.uint64)
-    dc, dp, out = Dev.of(col), Dev.of(pos), Dev(len(pos) * 4)
-    mq.check(lib.mq_gather_u64(dc.ptr, dp.ptr, len(pos), out.ptr, None))
-    assert np.array_equal(out.get(np.int32, len(pos)), col[pos.astype(np.int64)])
+    dc = Dev.of(col)
+    for m in (1, 7, 2047, 2049, 200_013):  # full steps of 8 x 256 rows and the ragged last one
+        pos = rng.integers(0, len(col), m).astype(np.uint64)
+        dp, out = Dev.of(pos), Dev(len(pos) * 4)
+        mq.check(lib.mq_gather_u64(dc.ptr, dp.ptr, len(pos), out.ptr, None))
+        assert np.array_equal(out.get(np.int32, len(pos)), col[pos.astype(np.int64)]), m
     for mn, bs in ((int(col.min()), (int(col.max()) - int(col.min())) // 99), (0, 7), (-10, -3)):
         h = Dev(101 * 8)
         mq.check(lib.mq_histogram(dc.ptr, len(col), mn, bs, h.ptr, None))
