@@ -424,7 +424,8 @@ __global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
         const uint64_t ic = i < n ? i : n - 1;
-        key[k] = FROM_COLS ? (uint32_t)c1[ic] : (uint32_t)in[ic];
+        key[k] = FROM_COLS ? (uint32_t)__builtin_nontemporal_load(c1 + ic)
+                           : (uint32_t)__builtin_nontemporal_load(in + ic);
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++)
