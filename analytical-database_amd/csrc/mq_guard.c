@@ -1,0 +1,316 @@
+/*
+ * mq_guard.c — write guards on host memory that libmq mirrors in HBM.
+ *
+ * The reference hands libmq host memory that it may later rewrite in place: the
+ * clustered index build reorders every other column through the same mmap'd
+ * pointer (src/index.c:105-114, reorder_column), insert_row appends through it
+ * (src/db_manager.c:190-197). A device copy keyed on (pointer, length) cannot see
+ * that. A guard makes any such write visible:
+ *
+ *   arm    the whole pages inside [p, p+bytes) become read-only (mprotect); the
+ *          partial pages at both ends (at most 2 x 4 KB) are copied aside;
+ *   write  the first store into a guarded page faults; the SIGSEGV handler gives
+ *          the pages their protection back, marks the guard dirty and returns, so
+ *          the store re-executes and succeeds (one fault per guard, not per page);
+ *   check  clean = not dirty, the edge bytes still equal their copies, and the
+ *          read-only pages are still the ones armed (a munmap + fresh mapping at
+ *          the same address is writable again: MADV_POPULATE_WRITE, which never
+ *          changes content, fails on the armed pages and succeeds on a new map).
+ *
+ * Only memory whose lifetime ends in munmap is guarded, so a read-only page can
+ * never be left behind inside the malloc heap (where a later read(2) into it would
+ * fail with EFAULT):
+ *   MQ_GUARD_FILE   every page is in a writable file-backed mapping (the
+ *                   reference's column files, start_data db_manager.c:736-790, or
+ *                   a memfd);
+ *   MQ_GUARD_CHUNK  the caller's own malloc chunk that glibc served with mmap
+ *                   (freed by munmap); checked from the chunk header.
+ * Anything else is not guardable: arm returns 0 and the caller treats its copy as
+ * single-use.
+ *
+ * Not seen: content changed through the page cache (write(2) to a column file)
+ * rather than through the mapping; documented in DESIGN.md §1.
+ */
+#define _GNU_SOURCE
+#include "mq_guard.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
+#define NGUARD 8192
+
+enum { G_FREE = 0, G_ARMED = 1, G_DIRTY = 2 };
+
+typedef struct {
+    _Atomic int state;
+    uintptr_t lo, hi;       /* read-only pages [lo, hi) (empty when no whole page) */
+    int prot;               /* protection restored on a write or at release */
+    uint32_t gen;
+    const unsigned char* p; /* the guarded range */
+    size_t bytes;
+    unsigned char* edge;    /* [p, lo) then [hi, p + bytes); the whole range if lo == hi */
+    size_t head, tail;
+} Guard;
+
+static Guard g_guard[NGUARD];
+static _Atomic int g_hw;        /* slots [0, g_hw) may be in use */
+static size_t g_page;
+static struct sigaction g_prev;
+static int g_installed;
+static int g_probe = -1;        /* 1: MADV_POPULATE_WRITE tells armed pages apart; 0: not available */
+static int g_probe_errno;
+static int g_enabled = -1;
+static mq_guard_stats g_stats;
+
+static void on_segv(int sig, siginfo_t* si, void* uc);
+
+static size_t page(void) {
+    if (!g_page) g_page = (size_t)sysconf(_SC_PAGESIZE);
+    return g_page;
+}
+
+int mq_guard_enabled(void) {
+    if (g_enabled < 0) {
+        const char* e = getenv("MQ_GUARD");
+        g_enabled = !(e && e[0] == '0');
+    }
+    return g_enabled;
+}
+
+/* Keep the handler first in line: Python's faulthandler (pytest enables it) or
+ * anything else installed later would otherwise see the guard faults first. */
+static void install(void) {
+    struct sigaction cur;
+    sigaction(SIGSEGV, NULL, &cur);
+    if (g_installed && (cur.sa_flags & SA_SIGINFO) && cur.sa_sigaction == on_segv) return;
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = on_segv;
+    sa.sa_flags = SA_SIGINFO | SA_NODEFER | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(SIGSEGV, &sa, &g_prev) == 0) g_installed = 1;
+}
+
+static void on_segv(int sig, siginfo_t* si, void* uc) {
+    const uintptr_t a = (uintptr_t)si->si_addr;
+    int hit = 0;
+    if (si->si_code == SEGV_ACCERR) {
+        const int hw = atomic_load_explicit(&g_hw, memory_order_acquire);
+        for (int i = 0; i < hw; i++) {
+            Guard* g = &g_guard[i];
+            if (atomic_load_explicit(&g->state, memory_order_acquire) != G_ARMED) continue;
+            if (a < g->lo || a >= g->hi) continue;
+            mprotect((void*)g->lo, g->hi - g->lo, g->prot);
+            atomic_store_explicit(&g->state, G_DIRTY, memory_order_release);
+            hit = 1;
+        }
+    }
+    if (hit) return;
+    /* not ours: hand it on as if we were not here */
+    if (g_prev.sa_flags & SA_SIGINFO) {
+        if (g_prev.sa_sigaction) {
+            g_prev.sa_sigaction(sig, si, uc);
+            return;
+        }
+    } else if (g_prev.sa_handler != SIG_DFL && g_prev.sa_handler != SIG_IGN) {
+        g_prev.sa_handler(sig);
+        return;
+    }
+    signal(SIGSEGV, SIG_DFL); /* the faulting access re-executes and terminates the process */
+}
+
+/* Does MADV_POPULATE_WRITE distinguish a read-only page (armed) from a writable
+ * one on this kernel? Calibrated once on a page of our own. */
+static void calibrate(void) {
+    if (g_probe >= 0) return;
+    g_probe = 0;
+    void* m = mmap(NULL, page(), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) return;
+    if (madvise(m, page(), MADV_POPULATE_WRITE) == 0 && mprotect(m, page(), PROT_READ) == 0) {
+        errno = 0;
+        if (madvise(m, page(), MADV_POPULATE_WRITE) != 0 && errno != ENOMEM) {
+            g_probe = 1;
+            g_probe_errno = errno;
+        }
+    }
+    munmap(m, page());
+}
+
+/* 1 when page lo is still a read-only page of ours (or the kernel cannot tell). */
+static int still_armed(uintptr_t lo) {
+    calibrate();
+    if (!g_probe) return 1;
+    errno = 0;
+    int rc = madvise((void*)lo, page(), MADV_POPULATE_WRITE);
+    return rc != 0 && errno == g_probe_errno;
+}
+
+/* Protection of [lo, hi) when every page of it lies in writable mappings that are
+ * file-backed (want_file) or of any kind; -1 when not, or when they differ. */
+static int vma_prot(uintptr_t lo, uintptr_t hi, int want_file) {
+    int fd = open("/proc/self/maps", O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return -1;
+    static char buf[1 << 16];
+    size_t have = 0;
+    uintptr_t covered = lo;
+    int prot = -2, ok = 1, done = 0;
+    while (!done && ok) {
+        ssize_t r = read(fd, buf + have, sizeof buf - 1 - have);
+        if (r <= 0) break;
+        have += (size_t)r;
+        buf[have] = '\0';
+        char* line = buf;
+        char* nl;
+        while ((nl = strchr(line, '\n'))) {
+            *nl = '\0';
+            unsigned long s, e, off, ino;
+            char perms[8] = {0}, dev[16] = {0};
+            if (sscanf(line, "%lx-%lx %7s %lx %15s %lu", &s, &e, perms, &off, dev, &ino) == 6 && e > covered &&
+                s < hi) {
+                if (s > covered) { ok = 0; break; } /* a hole */
+                int p = (perms[0] == 'r' ? PROT_READ : 0) | (perms[1] == 'w' ? PROT_WRITE : 0) |
+                        (perms[2] == 'x' ? PROT_EXEC : 0);
+                if (!(p & PROT_WRITE) || !(p & PROT_READ) || (want_file && ino == 0) ||
+                    (prot != -2 && p != prot)) {
+                    ok = 0;
+                    break;
+                }
+                prot = p;
+                covered = e;
+                if (covered >= hi) { done = 1; break; }
+            }
+            line = nl + 1;
+        }
+        have = strlen(line);
+        memmove(buf, line, have);
+    }
+    close(fd);
+    return (ok && covered >= hi && prot >= 0) ? prot : -1;
+}
+
+static void restore(Guard* g) {
+    if (g->hi > g->lo && atomic_load(&g->state) == G_ARMED && still_armed(g->lo))
+        mprotect((void*)g->lo, g->hi - g->lo, g->prot);
+}
+
+static void slot_free(Guard* g) {
+    free(g->edge);
+    g->edge = NULL;
+    g->gen++;
+    atomic_store_explicit(&g->state, G_FREE, memory_order_release);
+}
+
+void mq_guard_forget_range(uintptr_t addr, size_t bytes) {
+    const uintptr_t a = addr, b = a + bytes;
+    const int hw = atomic_load(&g_hw);
+    for (int i = 0; i < hw; i++) {
+        Guard* g = &g_guard[i];
+        if (atomic_load(&g->state) != G_ARMED) continue;
+        const uintptr_t ga = (uintptr_t)g->p, gb = ga + g->bytes;
+        if (ga < b && a < gb) {
+            restore(g);
+            atomic_store(&g->state, G_DIRTY); /* its owner sees it unclean */
+        }
+    }
+}
+
+uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {
+    if (!mq_guard_enabled() || !p || !bytes) return 0;
+    const uintptr_t a = (uintptr_t)p, b = a + bytes;
+    const uintptr_t pg = page();
+    uintptr_t lo = (a + pg - 1) & ~(pg - 1), hi = b & ~(pg - 1);
+    if (hi <= lo) lo = hi = 0;
+    int prot = PROT_READ | PROT_WRITE;
+    if (kind == MQ_GUARD_CHUNK) {
+        /* glibc chunk header: the size word before p has IS_MMAPPED (0x2) set */
+        if (!(((const size_t*)p)[-1] & 2)) return 0;
+    } else {
+        if (lo == hi) return 0;
+        if ((prot = vma_prot(lo, hi, 1)) < 0) return 0;
+    }
+    mq_guard_forget_range((uintptr_t)p, bytes);
+    int idx = -1;
+    const int hw = atomic_load(&g_hw);
+    for (int i = 0; i < hw; i++)
+        if (atomic_load(&g_guard[i].state) == G_FREE) {
+            idx = i;
+            break;
+        }
+    if (idx < 0) {
+        if (hw == NGUARD) return 0;
+        idx = hw;
+    }
+    Guard* g = &g_guard[idx];
+    const size_t head = lo == hi ? bytes : lo - a, tail = lo == hi ? 0 : b - hi;
+    unsigned char* edge = (unsigned char*)malloc(head + tail + 1);
+    if (!edge) return 0;
+    memcpy(edge, p, head);
+    if (tail) memcpy(edge + head, (const void*)hi, tail);
+    g->lo = lo;
+    g->hi = hi;
+    g->prot = prot;
+    g->p = (const unsigned char*)p;
+    g->bytes = bytes;
+    g->edge = edge;
+    g->head = head;
+    g->tail = tail;
+    if (!g->gen) g->gen = 1;
+    install();
+    atomic_store_explicit(&g->state, G_ARMED, memory_order_release);
+    if (idx == hw) atomic_store_explicit(&g_hw, hw + 1, memory_order_release);
+    if (hi > lo && mprotect((void*)lo, hi - lo, PROT_READ) != 0) {
+        slot_free(g);
+        return 0;
+    }
+    g_stats.armed++;
+    return ((uint64_t)g->gen << 32) | (uint32_t)idx;
+}
+
+static Guard* lookup(uint64_t h) {
+    if (!h) return NULL;
+    const uint32_t idx = (uint32_t)h;
+    if (idx >= NGUARD) return NULL;
+    Guard* g = &g_guard[idx];
+    return (g->gen == (uint32_t)(h >> 32) && atomic_load(&g->state) != G_FREE) ? g : NULL;
+}
+
+int mq_guard_clean(uint64_t h, const void* p, size_t bytes) {
+    Guard* g = lookup(h);
+    int ok = g && g->p == (const unsigned char*)p && g->bytes == bytes && atomic_load(&g->state) == G_ARMED &&
+             memcmp(g->edge, p, g->head) == 0 &&
+             (!g->tail || memcmp(g->edge + g->head, (const void*)g->hi, g->tail) == 0) &&
+             (g->hi == g->lo || still_armed(g->lo));
+    if (ok) g_stats.clean++;
+    else g_stats.stale++;
+    return ok;
+}
+
+void mq_guard_release(uint64_t h) {
+    Guard* g = lookup(h);
+    if (!g) return;
+    restore(g);
+    slot_free(g);
+}
+
+mq_guard_stats mq_guard_get_stats(void) {
+    int n = 0;
+    const int hw = atomic_load(&g_hw);
+    for (int i = 0; i < hw; i++) n += atomic_load(&g_guard[i].state) != G_FREE;
+    mq_guard_stats s = g_stats;
+    s.live = (uint64_t)n;
+    calibrate();
+    s.remap_probe = (uint64_t)g_probe;
+    return s;
+}

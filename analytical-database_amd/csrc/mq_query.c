@@ -34,6 +34,7 @@
 #include <unistd.h>
 
 #include "mq_device.h"
+#include "mq_guard.h"
 
 /* ---- ABI pins: x86-64 layouts of the reference structs ---- */
 _Static_assert(sizeof(Result) == 24, "Result size");
@@ -78,21 +79,29 @@ _Static_assert(OK == 0 && ERROR == 1, "StatusCode values");
 /* state                                                              */
 /* ------------------------------------------------------------------ */
 
+/* Every entry remembers the operator that last used it (op == g_op: in use by
+ * the current call, never evicted) and, for copies of host memory, the write
+ * guard (mq_guard.c) that says whether that memory is still what was uploaded.
+ * An entry without a guard (memory that cannot be guarded) serves only the
+ * operator that uploaded it. */
 typedef struct {
     const Column* col;
     const int* host;
     size_t rows;
     void* dev;
-    int owned;
+    int owned;                /* 0: attached by the caller (mq_column_attach), trusted */
+    uint64_t guard;
+    unsigned long long op;
 } ColEntry;
 
 typedef struct {
     const void* host;
     size_t n;
     size_t bytes;
-    int32_t head, tail;
     void* dev;
-    unsigned long long stamp;
+    uint64_t guard;
+    unsigned long long stamp; /* LRU */
+    unsigned long long op;
 } ShadowEntry;
 
 typedef struct {
@@ -102,6 +111,8 @@ typedef struct {
     size_t rows;
     void* d_values;
     void* d_positions;
+    uint64_t guard_v, guard_p;
+    unsigned long long op;
 } IndexEntry;
 
 #define MAX_COLS 1024
@@ -114,8 +125,10 @@ static ShadowEntry g_shadows[MAX_SHADOWS];
 static int g_nshadows;
 static size_t g_shadow_bytes;
 static unsigned long long g_stamp;
+static unsigned long long g_op;
 static IndexEntry g_idx[MAX_INDEXES];
 static int g_nidx;
+static mq_residency g_res;
 
 static void* g_ws;        /* scan workspace */
 static size_t g_ws_bytes;
@@ -137,6 +150,8 @@ static int fail(Status* st, const char* what, int rc) {
     if (st) st->code = ERROR;
     return rc;
 }
+
+static void sweep(void);
 
 static int ready(Status* st) {
     if (g_ready == 1) return 0;
@@ -162,15 +177,12 @@ static int ready(Status* st) {
     return 0;
 }
 
-static int grow(void** buf, size_t* have, size_t need) {
-    if (*have >= need && *buf) return 0;
-    if (*buf) mq_pool_free(*buf);
-    *buf = NULL;
-    *have = 0;
-    size_t want = need + need / 8 + 4096;
-    int rc = mq_malloc(buf, want);
-    if (rc) return rc;
-    *have = want;
+/* Start of an operator of the reference API: a new op number (what the previous
+ * operator held may now be evicted) and drop the copies no later call can use. */
+static int op_begin(Status* st) {
+    if (ready(st)) return -1;
+    g_op++;
+    sweep();
     return 0;
 }
 
@@ -196,57 +208,142 @@ static ColEntry* col_find(const Column* c) {
     return NULL;
 }
 
+/* Free an entry's device copy. Work queued on g_stream may still read it and the
+ * pool hands blocks out again at once, so the stream is drained first. */
 static void col_drop(ColEntry* e) {
-    if (e->owned && e->dev) mq_pool_free(e->dev);
+    mq_guard_release(e->guard);
+    if (e->owned && e->dev) {
+        mq_stream_sync(g_stream);
+        mq_pool_free(e->dev);
+    }
     *e = g_cols[--g_ncols];
 }
 
-static int column_device(Column* c, const int32_t** d, Status* st) {
-    ColEntry* e = col_find(c);
-    if (e && e->host == c->data && e->rows == c->row_count) {
-        *d = (const int32_t*)e->dev;
-        return 0;
-    }
-    if (e) col_drop(e);
-    if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
-    size_t bytes = c->row_count * sizeof(int32_t);
-    void* dev = NULL;
-    int rc = mq_pool_malloc(&dev, bytes);
-    if (rc) return fail(st, "column allocation", rc);
-    if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
-        mq_pool_free(dev);
-        return fail(st, "column upload", rc);
-    }
-    g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1};
-    *d = (const int32_t*)dev;
-    return 0;
+static int col_usable(const ColEntry* e, const Column* c) {
+    if (e->host != c->data || e->rows != c->row_count) return 0;
+    if (!e->owned || e->op == g_op || e->rows == 0) return 1;
+    return e->guard && mq_guard_clean(e->guard, e->host, e->rows * sizeof(int32_t));
 }
 
 /* ---- result shadows ---- */
 
 static void shadow_drop(int i) {
-    if (g_shadows[i].dev) mq_pool_free(g_shadows[i].dev);
+    mq_guard_release(g_shadows[i].guard);
+    if (g_shadows[i].dev) {
+        mq_stream_sync(g_stream);
+        mq_pool_free(g_shadows[i].dev);
+    }
     g_shadow_bytes -= g_shadows[i].bytes;
     g_shadows[i] = g_shadows[--g_nshadows];
 }
 
-static size_t shadow_budget(void) {
-    static size_t budget;
-    if (!budget) {
-        const char* env = getenv("MQ_SHADOW_MB");
-        size_t mb = env ? (size_t)strtoull(env, NULL, 10) : 65536;
-        budget = mb << 20;
-    }
-    return budget;
+static size_t shadow_budget(void) { /* read per call: tests change it at run time */
+    const char* env = getenv("MQ_SHADOW_MB");
+    size_t mb = env ? (size_t)strtoull(env, NULL, 10) : 65536;
+    return mb << 20;
 }
 
+/* LRU eviction down to the budget; what the current operator holds stays (the
+ * budget may be exceeded for the duration of one call). */
 static void shadow_make_room(size_t bytes) {
-    while (g_nshadows > 0 && (g_nshadows >= MAX_SHADOWS || g_shadow_bytes + bytes > shadow_budget())) {
-        int lru = 0;
-        for (int i = 1; i < g_nshadows; i++)
-            if (g_shadows[i].stamp < g_shadows[lru].stamp) lru = i;
+    while (g_nshadows >= MAX_SHADOWS || g_shadow_bytes + bytes > shadow_budget()) {
+        int lru = -1;
+        for (int i = 0; i < g_nshadows; i++)
+            if (g_shadows[i].op != g_op && (lru < 0 || g_shadows[i].stamp < g_shadows[lru].stamp)) lru = i;
+        if (lru < 0) break;
         shadow_drop(lru);
     }
+}
+
+/* Entries that only the operator that made them could use (no guard, or the
+ * guard saw a write) are dropped at the start of the next operator. */
+static void sweep(void) {
+    for (int i = g_nshadows - 1; i >= 0; i--)
+        if (g_shadows[i].op != g_op && !g_shadows[i].guard) shadow_drop(i);
+    for (int i = g_ncols - 1; i >= 0; i--)
+        if (g_cols[i].owned && g_cols[i].op != g_op && g_cols[i].rows && !g_cols[i].guard) col_drop(&g_cols[i]);
+}
+
+/* Device allocation for copies: on failure, evict what the current operator does
+ * not hold (shadows LRU, then columns), release the pool's idle blocks, retry. */
+static int dev_alloc(void** p, size_t bytes) {
+    int rc = mq_pool_malloc(p, bytes);
+    while (rc == MQ_ENOMEM) {
+        int lru = -1;
+        for (int i = 0; i < g_nshadows; i++)
+            if (g_shadows[i].op != g_op && (lru < 0 || g_shadows[i].stamp < g_shadows[lru].stamp)) lru = i;
+        if (lru >= 0) {
+            shadow_drop(lru);
+        } else {
+            int c = -1;
+            for (int i = 0; i < g_ncols; i++)
+                if (g_cols[i].owned && g_cols[i].op != g_op) c = i;
+            if (c < 0) {
+                mq_stream_sync(g_stream);
+                mq_trim();
+                return mq_pool_malloc(p, bytes);
+            }
+            col_drop(&g_cols[c]);
+        }
+        mq_stream_sync(g_stream);
+        mq_trim();
+        rc = mq_pool_malloc(p, bytes);
+    }
+    return rc;
+}
+
+static int grow(void** buf, size_t* have, size_t need) {
+    if (*have >= need && *buf) return 0;
+    if (*buf) {
+        mq_stream_sync(g_stream);
+        mq_pool_free(*buf);
+    }
+    *buf = NULL;
+    *have = 0;
+    size_t want = need + need / 8 + 4096;
+    int rc = dev_alloc(buf, want);
+    if (rc) return rc;
+    *have = want;
+    return 0;
+}
+
+/* Register a device copy of a column's rows (made here: owned) and guard the host
+ * rows it mirrors. */
+static ColEntry* col_put(Column* c, void* dev) {
+    ColEntry* e = col_find(c);
+    if (e) col_drop(e);
+    if (g_ncols == MAX_COLS) {
+        int victim = 0;
+        for (int i = 0; i < g_ncols; i++)
+            if (g_cols[i].op != g_op) victim = i;
+        col_drop(&g_cols[victim]);
+    }
+    const size_t bytes = c->row_count * sizeof(int32_t);
+    const uint64_t guard = bytes ? mq_guard_arm(c->data, bytes, MQ_GUARD_FILE) : 0;
+    g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1, guard, g_op};
+    return &g_cols[g_ncols - 1];
+}
+
+static int column_device(Column* c, const int32_t** d, Status* st) {
+    ColEntry* e = col_find(c);
+    if (e && col_usable(e, c)) {
+        e->op = g_op;
+        *d = (const int32_t*)e->dev;
+        return 0;
+    }
+    if (e) col_drop(e);
+    size_t bytes = c->row_count * sizeof(int32_t);
+    void* dev = NULL;
+    int rc = dev_alloc(&dev, bytes);
+    if (rc) return fail(st, "column allocation", rc);
+    if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
+        mq_pool_free(dev);
+        return fail(st, "column upload", rc);
+    }
+    g_res.column_uploads++;
+    g_res.column_bytes += bytes;
+    *d = (const int32_t*)col_put(c, dev)->dev;
+    return 0;
 }
 
 static int shadow_find(const void* host) {
@@ -255,36 +352,49 @@ static int shadow_find(const void* host) {
     return -1;
 }
 
-/* Register dev (owned, n int32) as the shadow of host payload. */
-static void shadow_put(const void* host, size_t n, void* dev) {
+/* Register dev (owned, n int32) as the shadow of host payload, with its guard
+ * (0: single-use). */
+static void shadow_put(const void* host, size_t n, void* dev, uint64_t guard) {
     int i = shadow_find(host);
     if (i >= 0) shadow_drop(i);
     size_t bytes = n * sizeof(int32_t);
     shadow_make_room(bytes);
-    const int32_t* h = (const int32_t*)host;
-    g_shadows[g_nshadows++] = (ShadowEntry){host, n, bytes, n ? h[0] : 0, n ? h[n - 1] : 0, dev,
-                                            ++g_stamp};
+    if (g_nshadows == MAX_SHADOWS) { /* everything is held by the current operator */
+        int v = 0;
+        for (int j = 0; j < g_nshadows; j++)
+            if (g_shadows[j].stamp < g_shadows[v].stamp) v = j;
+        shadow_drop(v);
+    }
+    g_shadows[g_nshadows++] = (ShadowEntry){host, n, bytes, dev, guard, ++g_stamp, g_op};
     g_shadow_bytes += bytes;
 }
 
-/* Device view of an int32 Result payload (shadow, or a fresh upload). */
+/* Device view of an int32 Result payload: its shadow while the payload is
+ * unchanged (guarded, or uploaded by this same operator), else a fresh upload. */
 static int result_device(const Result* r, const int32_t** d, Status* st) {
     const int32_t* h = (const int32_t*)r->payload;
     size_t n = r->num_tuples;
     int i = shadow_find(h);
-    if (i >= 0 && g_shadows[i].n == n && (n == 0 || (g_shadows[i].head == h[0] && g_shadows[i].tail == h[n - 1]))) {
-        g_shadows[i].stamp = ++g_stamp;
-        *d = (const int32_t*)g_shadows[i].dev;
-        return 0;
+    if (i >= 0) {
+        ShadowEntry* e = &g_shadows[i];
+        if (e->n == n && (e->op == g_op || n == 0 || (e->guard && mq_guard_clean(e->guard, h, n * 4)))) {
+            e->stamp = ++g_stamp;
+            e->op = g_op;
+            *d = (const int32_t*)e->dev;
+            return 0;
+        }
+        shadow_drop(i);
     }
     void* dev = NULL;
-    int rc = mq_pool_malloc(&dev, n * sizeof(int32_t));
+    int rc = dev_alloc(&dev, n * sizeof(int32_t));
     if (rc) return fail(st, "result allocation", rc);
     if (n && (rc = h2d(dev, h, n * sizeof(int32_t)))) {
         mq_pool_free(dev);
         return fail(st, "result upload", rc);
     }
-    shadow_put(h, n, dev);
+    g_res.result_uploads++;
+    g_res.result_bytes += n * sizeof(int32_t);
+    shadow_put(h, n, dev, 0); /* not libmq's memory: single-use */
     *d = (const int32_t*)dev;
     return 0;
 }
@@ -295,7 +405,9 @@ static int result_device(const Result* r, const int32_t** d, Status* st) {
  * 2.0 ms plain, 1.7 ms advised). */
 static void* payload_alloc(size_t bytes) {
     void* p = malloc(bytes ? bytes : 1);
-    if (p && bytes >= ((size_t)8 << 20)) {
+    if (!p) return NULL;
+    mq_guard_forget_range((uintptr_t)p, bytes ? bytes : 1); /* a guard left on recycled memory */
+    if (bytes >= ((size_t)8 << 20)) {
         const uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095;
         const uintptr_t e = ((uintptr_t)p + bytes) & ~(uintptr_t)4095;
         if (e > a) (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
@@ -312,7 +424,9 @@ static Result* new_result(DataType t, size_t n, void* payload) {
 }
 
 /* Host Result from n int32 on the device (d_src, staging memory): D2H into a
- * malloc'd payload and keep an HBM shadow of it. */
+ * malloc'd payload. When the payload can be guarded (glibc served it with mmap, so
+ * free() unmaps it) an HBM shadow of it is kept for the operators that follow;
+ * otherwise they upload it again. */
 static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
     int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
     int rc;
@@ -321,19 +435,19 @@ static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
         fail(st, "result download", rc);
         return NULL;
     }
-    void* dev = NULL;
-    if ((rc = mq_pool_malloc(&dev, n * sizeof(int32_t)))) {
-        free(host);
-        fail(st, "shadow allocation", rc);
-        return NULL;
+    const uint64_t guard = n ? mq_guard_arm(host, n * sizeof(int32_t), MQ_GUARD_CHUNK) : 0;
+    if (guard) {
+        void* dev = NULL;
+        if ((rc = dev_alloc(&dev, n * sizeof(int32_t))) ||
+            (rc = mq_memcpy_d2d(dev, d_src, n * sizeof(int32_t), g_stream))) {
+            mq_guard_release(guard);
+            mq_pool_free(dev);
+            free(host);
+            fail(st, "shadow copy", rc);
+            return NULL;
+        }
+        shadow_put(host, n, dev, guard);
     }
-    if (n && (rc = mq_memcpy_d2d(dev, d_src, n * sizeof(int32_t), g_stream))) {
-        mq_pool_free(dev);
-        free(host);
-        fail(st, "shadow copy", rc);
-        return NULL;
-    }
-    shadow_put(host, n, dev);
     st->code = OK;
     return new_result(INT, n, host);
 }
@@ -373,9 +487,8 @@ __attribute__((weak)) bool should_use_index(Column* column, int low, int high) {
     return true;
 }
 
-/* query.c:92-137 */
-Result* select_column_scan(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+/* query.c:92-137 (the body; shared_select calls it inside its own operator) */
+static Result* scan_positions(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
     size_t n = column->row_count;
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
@@ -391,40 +504,72 @@ Result* select_column_scan(Column* column, int* low_pointer, int* high_pointer, 
     return int_result_from_device(g_scratch, (size_t)k, ret_status);
 }
 
+Result* select_column_scan(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
+    if (op_begin(ret_status)) return NULL;
+    return scan_positions(column, low_pointer, high_pointer, ret_status);
+}
+
+/* ---- sorted-index residency: the index arrays' HBM copies ---- */
+
+static void idx_drop(IndexEntry* e) {
+    mq_guard_release(e->guard_v);
+    mq_guard_release(e->guard_p);
+    mq_stream_sync(g_stream);
+    mq_pool_free(e->d_values);
+    mq_pool_free(e->d_positions);
+    *e = g_idx[--g_nidx];
+}
+
+static int idx_usable(const IndexEntry* e, const ColumnIndex* ix, size_t n) {
+    if (e->values != ix->values || e->positions != ix->positions || e->rows != n) return 0;
+    if (e->op == g_op || n == 0) return 1;
+    return e->guard_v && e->guard_p && mq_guard_clean(e->guard_v, e->values, n * sizeof(int32_t)) &&
+           mq_guard_clean(e->guard_p, e->positions, n * sizeof(size_t));
+}
+
+/* guarded: the arrays are libmq's own malloc'd memory (build_index) */
+static IndexEntry* idx_put(ColumnIndex* ix, size_t n, void* d_values, void* d_positions, int guarded) {
+    for (int i = 0; i < g_nidx; i++)
+        if (g_idx[i].index == ix) {
+            idx_drop(&g_idx[i]);
+            break;
+        }
+    if (g_nidx == MAX_INDEXES) idx_drop(&g_idx[0]);
+    uint64_t gv = 0, gp = 0;
+    if (guarded && n) {
+        gv = mq_guard_arm(ix->values, n * sizeof(int32_t), MQ_GUARD_CHUNK);
+        gp = mq_guard_arm(ix->positions, n * sizeof(size_t), MQ_GUARD_CHUNK);
+    }
+    g_idx[g_nidx++] = (IndexEntry){ix, ix->values, ix->positions, n, d_values, d_positions, gv, gp, g_op};
+    return &g_idx[g_nidx - 1];
+}
+
 /* query.c:165-198: sorted-index select, in value order. */
 Result* select_column_sorted_index(Column* column, int low, int high, Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     ColumnIndex* ix = column->index;
     size_t n = column->row_count;
     IndexEntry* e = NULL;
     for (int i = 0; i < g_nidx; i++)
         if (g_idx[i].index == ix) e = &g_idx[i];
-    if (e && (e->values != ix->values || e->positions != ix->positions || e->rows != n)) {
-        mq_pool_free(e->d_values);
-        mq_pool_free(e->d_positions);
-        *e = g_idx[--g_nidx];
+    if (e && !idx_usable(e, ix, n)) {
+        idx_drop(e);
         e = NULL;
     }
     if (!e) {
-        if (g_nidx == MAX_INDEXES) {
-            mq_pool_free(g_idx[0].d_values);
-            mq_pool_free(g_idx[0].d_positions);
-            g_idx[0] = g_idx[--g_nidx];
-        }
-        IndexEntry ne = {ix, ix->values, ix->positions, n, NULL, NULL};
+        void *dv = NULL, *dp = NULL;
         int rc;
-        if ((rc = mq_malloc(&ne.d_values, n * sizeof(int32_t))) ||
-            (rc = mq_malloc(&ne.d_positions, n * sizeof(uint64_t))) ||
-            (n && (rc = h2d(ne.d_values, ix->values, n * sizeof(int32_t)))) ||
-            (n && (rc = h2d(ne.d_positions, ix->positions, n * sizeof(uint64_t))))) {
-            mq_pool_free(ne.d_values);
-            mq_pool_free(ne.d_positions);
+        if ((rc = dev_alloc(&dv, n * sizeof(int32_t))) || (rc = dev_alloc(&dp, n * sizeof(uint64_t))) ||
+            (n && (rc = h2d(dv, ix->values, n * sizeof(int32_t)))) ||
+            (n && (rc = h2d(dp, ix->positions, n * sizeof(uint64_t))))) {
+            mq_pool_free(dv);
+            mq_pool_free(dp);
             fail(ret_status, "index upload", rc);
             return NULL;
         }
-        g_idx[g_nidx++] = ne;
-        e = &g_idx[g_nidx - 1];
+        e = idx_put(ix, n, dv, dp, 0); /* the caller's arrays: single-use */
     }
+    e->op = g_op;
     if (ensure_ws(n, ret_status)) return NULL;
     int rc = mq_index_select((const int32_t*)e->d_values, (const uint64_t*)e->d_positions, n, low, high,
                              (int32_t*)g_scratch, (uint64_t*)g_small, g_stream);
@@ -450,7 +595,7 @@ Result* select_column(Column* column, int* low_pointer, int* high_pointer, Statu
 /* query.c:38-86 */
 Result* select_result(Result* column, Result* prev_position, int* low_pointer, int* high_pointer,
                       Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     size_t n = column->num_tuples;
     const int32_t *dval, *dpos;
     if (result_device(column, &dval, ret_status) || result_device(prev_position, &dpos, ret_status) ||
@@ -470,7 +615,7 @@ Result* select_result(Result* column, Result* prev_position, int* low_pointer, i
 
 /* query.c:223-243 */
 Result* fetch_column(Column* column, Result* position_result, Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     size_t k = position_result->num_tuples;
     const int32_t *dcol, *dpos;
     if (column_device(column, &dcol, ret_status) || result_device(position_result, &dpos, ret_status) ||
@@ -485,7 +630,7 @@ Result* fetch_column(Column* column, Result* position_result, Status* ret_status
 }
 
 static int reduce_result(Result* r, mq_agg* a, Status* st) {
-    if (ready(st)) return -1;
+    if (op_begin(st)) return -1;
     const int32_t* d;
     if (result_device(r, &d, st) || ensure_ws(0, st)) return -1;
     int rc = mq_reduce(d, r->num_tuples, (mq_agg*)g_small, g_ws, g_ws_bytes, g_stream);
@@ -509,7 +654,7 @@ Result* sum(GeneralizedColumn* column, Status* ret_status) {
     if (column->column_type == RESULT) {
         if (reduce_result(column->column_pointer.result, &a, ret_status)) return NULL;
     } else {
-        if (ready(ret_status)) return NULL;
+        if (op_begin(ret_status)) return NULL;
         Column* c = column->column_pointer.column;
         const int32_t* d;
         if (column_device(c, &d, ret_status) || ensure_ws(0, ret_status)) return NULL;
@@ -527,7 +672,7 @@ Result* sum(GeneralizedColumn* column, Status* ret_status) {
 }
 
 static Result* elementwise(Result* a, Result* b, Status* st, int is_sub) {
-    if (ready(st)) return NULL;
+    if (op_begin(st)) return NULL;
     size_t n = a->num_tuples;
     const int32_t *da, *db;
     if (result_device(a, &da, st) || result_device(b, &db, st) || ensure_ws(n, st)) return NULL;
@@ -584,7 +729,7 @@ Result* max(Result* column, Status* ret_status) {
  * serve all queries of a chunk (up to 256): count -> exact allocation -> write; each
  * query's device output becomes its result's HBM shadow. */
 Result** shared_select(SelectOperator* operators, int query_count, Column* column, Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     size_t n = column->row_count;
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status)) return NULL;
@@ -592,7 +737,7 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
     if (query_count <= 3) {  /* a few queries: one ordered-compaction pass each is cheaper */
         for (int j = 0; j < query_count; j++) {
             int lo = operators[j].low, hi = operators[j].high;
-            if (!(out[j] = select_column_scan(column, &lo, &hi, ret_status))) {
+            if (!(out[j] = scan_positions(column, &lo, &hi, ret_status))) {
                 for (int i = 0; i < j; i++) {
                     free(out[i]->payload);
                     free(out[i]);
@@ -617,7 +762,7 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
         }
         int rc = grow(&g_ws, &g_ws_bytes, mq_shared_select_workspace_bytes(n, q));
         if (!rc) rc = mq_shared_select_count(dcol, n, lows, highs, q, k, g_ws, g_ws_bytes, g_stream);
-        for (int j = 0; !rc && j < q; j++) rc = mq_pool_malloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
+        for (int j = 0; !rc && j < q; j++) rc = dev_alloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
         if (!rc) rc = mq_shared_select_write(g_ws, (int32_t* const*)dev, g_stream);
         for (int j = 0; !rc && j < q; j++) {
             int32_t* host = (int32_t*)payload_alloc((size_t)k[j] * sizeof(int32_t));
@@ -625,11 +770,15 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
                 free(host);
                 break;
             }
-            shadow_put(host, (size_t)k[j], dev[j]);
-            dev[j] = NULL;  /* owned by the shadow now */
+            const uint64_t guard = k[j] ? mq_guard_arm(host, (size_t)k[j] * 4, MQ_GUARD_CHUNK) : 0;
+            if (guard) {
+                shadow_put(host, (size_t)k[j], dev[j], guard);
+                dev[j] = NULL; /* owned by the shadow now */
+            }
             out[q0 + j] = new_result(INT, (size_t)k[j], host);
             done = q0 + j + 1;
         }
+        mq_stream_sync(g_stream);
         for (int j = 0; j < q; j++) mq_pool_free(dev[j]);
         if (rc) {
             fail(ret_status, "shared_select", rc);
@@ -681,7 +830,7 @@ static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, con
  * probe-major, build-insertion order. */
 Result** hash_join(Result* column_one, Result* position_one, Result* column_two, Result* position_two,
                    Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     const int32_t *d1, *dp1, *d2, *dp2;
     if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
         result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))
@@ -694,7 +843,7 @@ Result** hash_join(Result* column_one, Result* position_one, Result* column_two,
  * order = inner order) and probes with the outer side, outputs swapped. */
 Result** nested_loop_join(Result* column_one, Result* position_one, Result* column_two,
                           Result* position_two, Status* ret_status) {
-    if (ready(ret_status)) return NULL;
+    if (op_begin(ret_status)) return NULL;
     const int32_t *d1, *dp1, *d2, *dp2;
     if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
         result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))
@@ -726,7 +875,7 @@ static size_t g_print_out_cap, g_print_ws_cap;
 static int print_gpu(const Result* r, char* dst, size_t* len, Status* st) {
     const uint64_t n = r->num_tuples;
     const int32_t* d;
-    if (ready(st) || result_device(r, &d, st)) return -1;
+    if (result_device(r, &d, st)) return -1;
     const size_t need_out = (size_t)n * 12, need_ws = mq_format_workspace_bytes(n);
     int rc;
     if (g_print_out_cap < need_out) {
@@ -753,7 +902,12 @@ static int print_gpu(const Result* r, char* dst, size_t* len, Status* st) {
 
 char* print(Result** results, int result_num, Status* ret_status) {
     size_t total = 0;
-    for (int i = 0; i < result_num; i++) total += results[i]->num_tuples;
+    int on_gpu = 0;
+    for (int i = 0; i < result_num; i++) {
+        total += results[i]->num_tuples;
+        on_gpu |= results[i]->data_type == INT && results[i]->num_tuples >= print_gpu_min();
+    }
+    if (on_gpu && op_begin(ret_status)) return NULL;
     size_t cap = total * 24 + (size_t)result_num + 1;
     char* s = (char*)malloc(cap);
     size_t at = 0;
@@ -879,13 +1033,6 @@ extern void save_data(Table* table, Column* column, Status* ret_status) __attrib
 extern void start_data(Db* db, Table* table, Column* column, Status* ret_status)
     __attribute__((weak));
 
-static void col_put(Column* c, void* dev) {
-    ColEntry* e = col_find(c);
-    if (e) col_drop(e);
-    if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
-    g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1};
-}
-
 static void load_fail(Status* st, const char* msg) {
     fprintf(stderr, "libmq: load_db: %s\n", msg);
     st->code = ERROR;
@@ -974,7 +1121,7 @@ void load_db(Db* db, const char* path, Status* ret_status) {
         load_fail(ret_status, "more than 1024 columns");
         goto out;
     }
-    if (ready(ret_status)) goto out;
+    if (op_begin(ret_status)) goto out;
     const size_t wsb = mq_csv_workspace_bytes(dn, ncols);
     if ((rc = mq_malloc(&d_text, dn ? dn : 16)) || (rc = mq_malloc(&d_ws, wsb)) ||
         (rc = mq_malloc(&d_mm, 8 * (size_t)(ncols ? ncols : 1)))) {
@@ -999,7 +1146,7 @@ void load_db(Db* db, const char* path, Status* ret_status) {
             goto out;
         }
         ColEntry* e = col_find(c);
-        if (old && e && e->host == c->data && e->rows == old)
+        if (old && e && col_usable(e, c))
             rc = mq_memcpy_d2d(dcol[j], e->dev, old * 4, g_stream);
         else if (old)
             rc = h2d(dcol[j], c->data, old * 4);
@@ -1023,6 +1170,7 @@ void load_db(Db* db, const char* path, Status* ret_status) {
     }
     for (int j = 0; j < ncols; j++) {
         Column* c = table->columns + j;
+        mq_guard_forget_range((uintptr_t)c->data, total * 4); /* libmq writes the rows in place */
         if (rows && (rc = d2h(c->data + old, dparse[j], rows * 4))) {
             fail(ret_status, "load_db column download", rc);
             goto out;
@@ -1057,22 +1205,6 @@ typedef struct MqHistogram { /* cs165_api.h:71-75 */
 } MqHistogram;
 _Static_assert(sizeof(MqHistogram) == 1208, "Histogram size");
 
-static void idx_put(ColumnIndex* ix, size_t n, void* d_values, void* d_positions) {
-    for (int i = 0; i < g_nidx; i++)
-        if (g_idx[i].index == ix) {
-            mq_pool_free(g_idx[i].d_values);
-            mq_pool_free(g_idx[i].d_positions);
-            g_idx[i] = g_idx[--g_nidx];
-            break;
-        }
-    if (g_nidx == MAX_INDEXES) {
-        mq_pool_free(g_idx[0].d_values);
-        mq_pool_free(g_idx[0].d_positions);
-        g_idx[0] = g_idx[--g_nidx];
-    }
-    g_idx[g_nidx++] = (IndexEntry){ix, ix->values, ix->positions, n, d_values, d_positions};
-}
-
 /* One indexed column (index.c:119-143 + :63-84). Returns 0 or an MQ_E code. */
 static int index_one(Table* t, Column* c, Status* st) {
     const size_t n = c->row_count;
@@ -1102,6 +1234,7 @@ static int index_one(Table* t, Column* c, Status* st) {
             void* dnew = NULL;
             if ((rc = column_device(o, &dsrc, st))) goto bad;
             if ((rc = mq_malloc(&dnew, (n ? n : 1) * 4))) goto bad;
+            mq_guard_forget_range((uintptr_t)o->data, n * 4); /* reorder_column writes o->data in place */
             if ((rc = mq_gather_u64(dsrc, (const uint64_t*)dp, n, dnew, g_stream)) ||
                 (n && (rc = d2h(o->data, dnew, n * 4)))) {
                 mq_pool_free(dnew);
@@ -1143,7 +1276,7 @@ static int index_one(Table* t, Column* c, Status* st) {
     }
     ix->positions = hp;
     c->index = ix;
-    idx_put(ix, n, dv, dp); /* resident for select_column_sorted_index */
+    idx_put(ix, n, dv, dp, 1); /* resident for select_column_sorted_index */
     mq_pool_free(dh);
     return 0;
 bad:
@@ -1159,7 +1292,7 @@ bad:
 
 void build_index(Db* db) {
     Status st = {OK, NULL};
-    if (!db || ready(&st)) return;
+    if (!db || op_begin(&st)) return;
     for (size_t i = 0; i < db->tables_size; i++) {
         Table* t = db->tables + i;
         for (size_t j = 0; j < t->col_count; j++) {
@@ -1179,13 +1312,13 @@ int mq_column_attach(Column* column, const int32_t* d_data) {
     ColEntry* e = col_find(column);
     if (e) col_drop(e);
     if (g_ncols == MAX_COLS) col_drop(&g_cols[0]);
-    g_cols[g_ncols++] = (ColEntry){column, column->data, column->row_count, (void*)d_data, 0};
+    g_cols[g_ncols++] = (ColEntry){column, column->data, column->row_count, (void*)d_data, 0, 0, g_op};
     return MQ_OK;
 }
 
 int mq_column_upload(Column* column) {
     Status st = {OK, NULL};
-    if (ready(&st)) return MQ_ENODEV;
+    if (op_begin(&st)) return MQ_ENODEV;
     const int32_t* d;
     return column_device(column, &d, &st) ? MQ_EHIP : MQ_OK;
 }
@@ -1197,22 +1330,36 @@ void mq_column_invalidate(Column* column) {
 
 const void* mq_result_device_ptr(const Result* result) {
     int i = shadow_find(result->payload);
-    return i >= 0 ? g_shadows[i].dev : NULL;
+    if (i < 0) return NULL;
+    const ShadowEntry* e = &g_shadows[i];
+    if (e->n != result->num_tuples) return NULL;
+    if (e->op == g_op || e->n == 0 || (e->guard && mq_guard_clean(e->guard, e->host, e->n * 4))) return e->dev;
+    return NULL;
 }
 
 void mq_release_all(void) {
-    mq_trim();
+    if (g_stream) mq_stream_sync(g_stream);
     mq_pool_free(g_print_out);
     mq_pool_free(g_print_ws);
     g_print_out = g_print_ws = NULL;
     g_print_out_cap = g_print_ws_cap = 0;
     while (g_ncols) col_drop(&g_cols[g_ncols - 1]);
     while (g_nshadows) shadow_drop(g_nshadows - 1);
-    while (g_nidx) {
-        mq_pool_free(g_idx[g_nidx - 1].d_values);
-        mq_pool_free(g_idx[g_nidx - 1].d_positions);
-        g_nidx--;
-    }
+    while (g_nidx) idx_drop(&g_idx[g_nidx - 1]);
+    mq_trim();
+}
+
+void mq_residency_stats(mq_residency* out) {
+    mq_guard_stats gs = mq_guard_get_stats();
+    *out = g_res;
+    out->guards_armed = gs.armed;
+    out->guard_clean = gs.clean;
+    out->guard_stale = gs.stale;
+    out->guards_live = gs.live;
+    out->remap_probe = gs.remap_probe;
+    out->columns_resident = (uint64_t)g_ncols;
+    out->shadows_resident = (uint64_t)g_nshadows;
+    out->shadow_bytes = (uint64_t)g_shadow_bytes;
 }
 
 double mq_transfer_seconds(int reset) {

@@ -3,7 +3,7 @@
 Host-side mirror of the reference operator interface for Python callers
 (tests, bench). The product is the C-ABI library; this module only declares
 its signatures and the reference struct layouts
-(src/include/cs165_api.h:129-258, src/include/db_manager.h:95-108).
+(src/include/cs165_api.h:58-206, src/include/db_manager.h:95-108).
 
 No fallback: `load()` raises if libmq.so is missing, and every device entry
 point returns MQ_ENODEV when there is no gfx950 device.
@@ -34,7 +34,7 @@ class ColumnIndex(C.Structure):
     _fields_ = [("values", C.POINTER(C.c_int)), ("positions", C.POINTER(C.c_size_t))]
 
 
-class Column(C.Structure):  # cs165_api.h:129-144
+class Column(C.Structure):  # cs165_api.h:77-92
     _fields_ = [("name", C.c_char * 64), ("data", C.POINTER(C.c_int)), ("fd", C.c_int),
                 ("row_count", C.c_size_t), ("sorted", C.c_bool), ("clustered", C.c_bool),
                 ("has_index", C.c_bool), ("index", C.POINTER(ColumnIndex)),
@@ -42,11 +42,11 @@ class Column(C.Structure):  # cs165_api.h:129-144
                 ("min", C.c_int)]
 
 
-class Status(C.Structure):  # cs165_api.h:212-215
+class Status(C.Structure):  # cs165_api.h:160-163
     _fields_ = [("code", C.c_int), ("error_message", C.c_char_p)]
 
 
-class Result(C.Structure):  # cs165_api.h:231-235
+class Result(C.Structure):  # cs165_api.h:179-183
     _fields_ = [("num_tuples", C.c_size_t), ("data_type", C.c_int), ("payload", C.c_void_p)]
 
 
@@ -54,7 +54,7 @@ class GeneralizedColumnPointer(C.Union):
     _fields_ = [("result", C.POINTER(Result)), ("column", C.POINTER(Column))]
 
 
-class GeneralizedColumn(C.Structure):  # cs165_api.h:255-258
+class GeneralizedColumn(C.Structure):  # cs165_api.h:203-206
     _fields_ = [("column_type", C.c_int), ("column_pointer", GeneralizedColumnPointer)]
 
 
@@ -182,7 +182,28 @@ _SIGS = {
     "mq_result_device_ptr": (_vp, [_PR]),
     "mq_release_all": (None, []),
     "mq_transfer_seconds": (C.c_double, [_int]),
+    "mq_residency_stats": (None, [C.c_void_p]),
+    # write guards (csrc/mq_guard.h; internal, bound for the guard tests)
+    "mq_guard_arm": (C.c_uint64, [_vp, _sz, _int]),
+    "mq_guard_clean": (_int, [C.c_uint64, _vp, _sz]),
+    "mq_guard_release": (None, [C.c_uint64]),
+    "mq_guard_forget_range": (None, [C.c_size_t, _sz]),
 }
+
+MQ_GUARD_FILE, MQ_GUARD_CHUNK = 0, 1
+
+
+class Residency(C.Structure):  # include/mq_query.h mq_residency
+    _fields_ = [(n, C.c_uint64) for n in (
+        "column_uploads", "column_bytes", "result_uploads", "result_bytes", "guards_armed",
+        "guard_clean", "guard_stale", "guards_live", "remap_probe", "columns_resident",
+        "shadows_resident", "shadow_bytes")]
+
+
+def residency(lib=None) -> dict:
+    r = Residency()
+    (lib or load()).mq_residency_stats(C.byref(r))
+    return {n: int(getattr(r, n)) for n, _ in Residency._fields_}
 
 # The reference-API signatures shared with the reference's own library (oracle/_ref).
 REFERENCE_API = ["select_result", "select_column", "select_column_scan",

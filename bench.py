@@ -71,15 +71,19 @@ def cpu_baseline(rows: int) -> dict:
             s = refcpu.agg(refcpu.fetch(d, pos))["sum"]
             times.append(time.perf_counter() - t0)
     t1 = statistics.median(times)
-    # host-cores variant: row-balanced pthreads restatement (16 = this box's CPU share)
+    # host-cores variant: row-balanced pthreads restatement on every core this
+    # process may use (SURVEY §8(d) "nproc threads"; on the GPU box the cgroup CPU
+    # quota, not nproc, is the limit, and the record says which)
+    cores, why = host_cores()
     mt = []
     for _ in range(3):
         t0 = time.perf_counter()
-        c, s2 = refcpu.count_sum(d, lo, hi, nthreads=16)
+        c, s2 = refcpu.count_sum(d, lo, hi, nthreads=cores)
         mt.append(time.perf_counter() - t0)
     assert s2 == s
-    variants = {"host_cores_16": {"value": ns / statistics.median(mt), "cores": 16, "kind": "port",
-                                  "what": "refcpu rc_select_count_sum, 16 pthreads, row-balanced"}}
+    variants = {"host_cores": {"value": ns / statistics.median(mt), "cores": cores, "kind": "port",
+                               "cores_from": why,
+                               "what": f"refcpu rc_select_count_sum, {cores} pthreads, row-balanced"}}
     if kind == "reference":
         # the reference as its Makefile builds it (-O0, src/Makefile:12), one run
         api0 = Api(refcpu.reference(refcpu.REFLIB_O0))
@@ -102,6 +106,21 @@ def cpu_baseline(rows: int) -> dict:
             "nproc": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
+def host_cores() -> tuple[int, str]:
+    """Cores this process may run on: min(affinity mask, cgroup v2 cpu.max quota)."""
+    n = len(os.sched_getaffinity(0))
+    why = f"sched_getaffinity={n} (nproc={os.cpu_count()})"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) // int(period)))
+            why += f", cgroup cpu.max quota={q}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, why
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -112,7 +131,39 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def launch_ranks(ngpus: int, argv: list) -> int:
+    """`bench.py --gpus N` without an external launcher: start N rank processes of
+    this script (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set as
+    torch.distributed.run sets them) before this process touches the GPU, wait for
+    all, return the worst exit status. Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    if os.environ.get("MQ_BENCH_ONE_DEVICE") != "1":
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if ngpus > have:
+            print(f"bench.py: --gpus {ngpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(ngpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(ngpus),
+                   LOCAL_WORLD_SIZE=str(ngpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def main() -> None:
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        known, _ = pre.parse_known_args()
+        if known.gpus > 1:
+            sys.exit(launch_ranks(known.gpus, sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -129,6 +180,9 @@ def main() -> None:
     mq = _load("mq_binding", os.path.join(PKG, "mq.py"))
     mqd = _load("mq_dist", os.path.join(PKG, "dist.py"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal knobs for the N > 1 path on a one-GPU box (never set by the driver):
@@ -263,8 +317,7 @@ def main() -> None:
                          "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
                          "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),
                          "kernel_ms_median": statistics.median(kernel_ms),
-                         "achievable_peak": achievable,
-                         "frac_of_achievable": (gbs / achievable["gbs"]) if achievable else None,
+                         "stream_read_probe": achievable,
                          "algorithmic_bytes_per_launch": 4 * n},
             "parity": {"ok": parity, "count": res["count"], "sum": res["sum"]},
             "extra": extra,
@@ -453,8 +506,23 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import refcpu  # input generator only (the §8(c) column, on the host)
     from refapi import make_column, _libc
-    c0 = refcpu.gen_uniform(n, 42, nthreads=16)
-    c1 = refcpu.gen_uniform(n, 43, nthreads=16)
+    import mmap
+    maps = []
+
+    def file_column(seed):
+        # the reference keeps columns in MAP_SHARED file mappings (start_data,
+        # db_manager.c:736-790); a memfd is such a file, so libmq can guard it and
+        # keep its HBM copy across operators
+        fd = os.memfd_create(f"col{seed}")
+        os.ftruncate(fd, 4 * n)
+        m = mmap.mmap(fd, 4 * n, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        os.close(fd)
+        a = np.frombuffer(m, dtype=np.int32)
+        refcpu.lib().rc_gen_uniform(a.ctypes.data, n, seed, n, host_cores()[0])
+        maps.append(m)
+        return a
+
+    c0, c1 = file_column(42), file_column(43)
     col0, col1 = make_column(c0, b"col0"), make_column(c1, b"col1")
     t0 = time.perf_counter()
     mq.check(lib.mq_column_upload(C.byref(col0)), "upload col0")
@@ -488,11 +556,16 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
     med = {f"ms_{name}": 1e3 * statistics.median(v) for name, v in times.items()}
     chain_s = sum(med.values()) / 1e3
     want = next((r for r in gold["config3"] if r["n"] == n and r["low"] == lo and r["high"] == hi), None)
+    resid = mq.residency(lib)
+    lib.mq_release_all()
     res = {"rows": n, "k": k, "avg": avg, "ms_upload_two_columns": 1e3 * t_up,
+           "residency": {"column_uploads": resid["column_uploads"], "guards_live": resid["guards_live"],
+                         "result_uploads": resid["result_uploads"]},
            "upload_gbs": 8.0 * n / t_up / 1e9, **med, "ms_chain": 1e3 * chain_s,
            "rows_per_s_chain": n / chain_s, "ms_transfer_last_chain": 1e3 * xfer,
            "note": "PCIe-inclusive: each operator returns malloc'd host payloads (client_context.c "
-                   "frees them); the chain runs on HBM-resident columns after the one-off upload"}
+                   "frees them); the chain runs on HBM-resident columns after the one-off upload "
+                   "(memfd-backed columns, write-guarded)"}
     if want is not None:
         res["parity"] = (k, avg) == (want["k"], want["avg"])
     return res

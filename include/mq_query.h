@@ -8,7 +8,7 @@
  * Each entry point below cites the reference function it replaces.
  *
  * The types are re-declared here layout-for-layout from
- * src/include/cs165_api.h:77-92,110-116,152-215 and src/include/db_manager.h:95-108;
+ * src/include/cs165_api.h:58-132,152-206 and src/include/db_manager.h:95-108;
  * mq_query.c pins every size and offset with _Static_assert (x86-64 SysV).
  * The reference's own headers stay authoritative for its translation units;
  * this header is what libmq itself is compiled against.
@@ -16,9 +16,9 @@
  * Ownership (reference contract, client_context.c:31-90, server.c:432):
  * every returned Result / Result** and every payload is malloc'd host memory
  * that the caller frees with free(). Inputs are borrowed.
- * Device residency: a Column's rows are uploaded to HBM on first use and cached
- * until mq_column_invalidate(); Results produced by libmq keep a device shadow
- * so a following fetch/sum/avg/select_result on them does not re-upload.
+ * Device residency: a Column's rows are uploaded to HBM on first use and kept
+ * while a write guard shows them unchanged; Results produced by libmq keep a
+ * device shadow on the same terms (see "residency control" below).
  */
 #ifndef MQ_QUERY_H
 #define MQ_QUERY_H
@@ -35,17 +35,17 @@ extern "C" {
 #define MQ_MAX_SIZE_NAME 64
 #define MQ_HANDLE_MAX_SIZE 64
 
-typedef enum DataType { INT, LONG, FLOAT, DOUBLE } DataType;          /* cs165_api.h:110-115 */
+typedef enum DataType { INT, LONG, FLOAT, DOUBLE } DataType;          /* cs165_api.h:58-63 */
 
-typedef struct ColumnIndex {                                          /* cs165_api.h:117-120 */
+typedef struct ColumnIndex {                                          /* cs165_api.h:65-68 */
     int* values;
     size_t* positions;
 } ColumnIndex;
 
 struct Node;       /* btree node, opaque here (btree.h) */
-struct Histogram;  /* opaque here (cs165_api.h:123-127) */
+struct Histogram;  /* opaque here (cs165_api.h:71-75) */
 
-typedef struct Column {                                               /* cs165_api.h:129-144 */
+typedef struct Column {                                               /* cs165_api.h:77-92 */
     char name[MQ_MAX_SIZE_NAME];
     int* data;
     int fd;
@@ -60,27 +60,27 @@ typedef struct Column {                                               /* cs165_a
     int min;
 } Column;
 
-typedef enum StatusCode { OK, ERROR } StatusCode;                    /* cs165_api.h:204-209 */
+typedef enum StatusCode { OK, ERROR } StatusCode;                    /* cs165_api.h:152-157 */
 
-typedef struct Status {                                               /* cs165_api.h:212-215 */
+typedef struct Status {                                               /* cs165_api.h:160-163 */
     StatusCode code;
     char* error_message;
 } Status;
 
-typedef struct Result {                                               /* cs165_api.h:231-235 */
+typedef struct Result {                                               /* cs165_api.h:179-183 */
     size_t num_tuples;
     DataType data_type;
     void* payload;
 } Result;
 
-typedef enum GeneralizedColumnType { RESULT, COLUMN } GeneralizedColumnType;  /* :240-243 */
+typedef enum GeneralizedColumnType { RESULT, COLUMN } GeneralizedColumnType;  /* cs165_api.h:188-191 */
 
-typedef union GeneralizedColumnPointer {                              /* cs165_api.h:247-250 */
+typedef union GeneralizedColumnPointer {                              /* cs165_api.h:195-198 */
     Result* result;
     Column* column;
 } GeneralizedColumnPointer;
 
-typedef struct GeneralizedColumn {                                    /* cs165_api.h:255-258 */
+typedef struct GeneralizedColumn {                                    /* cs165_api.h:203-206 */
     GeneralizedColumnType column_type;
     GeneralizedColumnPointer column_pointer;
 } GeneralizedColumn;
@@ -189,9 +189,18 @@ void load_db(Db* db, const char* path, Status* ret_status);
  * instead of index.o's. */
 void build_index(Db* db);
 
-/* ---- libmq residency control (not in the reference) ---- */
+/* ---- libmq residency control (not in the reference) ----
+ * A device copy of host memory (a Column's rows, a Result payload, an index's
+ * arrays) is reused by later operators only while a write guard proves the host
+ * memory unchanged: the whole pages inside it are read-only, the
+ * first write into them faults once and marks the copy stale. Guarded are the
+ * reference's column files (any writable file-backed mapping, e.g. start_data's
+ * MAP_SHARED column files, or a memfd) and the payloads libmq allocates when glibc
+ * serves them with mmap. Any other memory is uploaded again by each operator that
+ * reads it. MQ_GUARD=0 turns the guards off (every copy single-use). */
 /* Use an existing device copy of column->data (row_count int32 rows in HBM); the
- * caller keeps ownership of d_data and must keep it alive while attached. */
+ * caller keeps ownership of d_data and must keep it alive while attached (attached
+ * copies are trusted: not guarded). */
 int mq_column_attach(Column* column, const int32_t* d_data);
 /* Upload column->data now (otherwise done lazily on first use). */
 int mq_column_upload(Column* column);
@@ -201,6 +210,15 @@ void mq_column_invalidate(Column* column);
 const void* mq_result_device_ptr(const Result* result);
 /* Drop every cached device copy. */
 void mq_release_all(void);
+/* Residency counters since load (tests and the bench read them). */
+typedef struct mq_residency {
+    uint64_t column_uploads, column_bytes;  /* H2D uploads of column rows */
+    uint64_t result_uploads, result_bytes;  /* H2D uploads of Result payloads */
+    uint64_t guards_armed, guard_clean, guard_stale, guards_live;
+    uint64_t remap_probe;                   /* 1: a remapped range is told apart (MADV_POPULATE_WRITE) */
+    uint64_t columns_resident, shadows_resident, shadow_bytes;
+} mq_residency;
+void mq_residency_stats(mq_residency* out);
 /* Seconds spent in host<->device copies by the query API since the last reset. */
 double mq_transfer_seconds(int reset);
 

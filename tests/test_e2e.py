@@ -114,6 +114,29 @@ class Server:
         self.proc = None
 
 
+def run_dsl_files(server_bin: str, workdir: str, names) -> dict:
+    """Replay DSL files from tests/golden/e2e in ONE server session (no restart):
+    {name: normalised output lines}."""
+    os.makedirs(workdir, exist_ok=True)
+    for f in os.listdir(E2E):
+        if f.endswith(".csv"):
+            shutil.copy(os.path.join(E2E, f), workdir)
+    log = open(os.path.join(workdir, "server.log"), "ab")
+    srv = Server(server_bin, workdir, log)
+    out = {}
+    try:
+        srv.start()
+        for name in names:
+            dsl = open(os.path.join(E2E, name)).read().replace("@DATA@", ".")
+            cp = subprocess.run([os.path.join(REFBIN, "client")], input=dsl.encode(), cwd=workdir,
+                                capture_output=True, timeout=600)
+            out[name] = normalise(cp.stdout.decode(errors="replace"))
+    finally:
+        srv.stop()
+        log.close()
+    return out
+
+
 def run_suite(server_bin: str, workdir: str, tests=TESTS) -> dict:
     """Returns {test_id: (normalised output lines, verdict)}."""
     os.makedirs(workdir, exist_ok=True)
@@ -193,3 +216,35 @@ def test_libmq_dropin_with_gpu_index_build(tmp_path):
         assert sorted(_ws(mine[t][0]), key=_sortkey) == sorted(_ws(ref[t][0]), key=_sortkey), t
         order_only.append(t)
     print(f"tests whose output differs from the reference only in tie order: {order_only}")
+
+
+@needs_bins
+@pytest.mark.timeout(300)
+def test_reference_server_residency_dsl(tmp_path):
+    """The residency DSL is meaningful on the reference: it prints every query."""
+    out = run_dsl_files(os.path.join(REFBIN, "server_ref"), str(tmp_path), [RESIDENCY_DSL])
+    assert len(out[RESIDENCY_DSL]) > 20
+
+
+RESIDENCY_DSL = "residency_noshutdown.dsl"
+
+
+@pytest.mark.gpu
+@needs_bins
+@pytest.mark.parametrize("binary", ["server_mq"])
+@pytest.mark.timeout(300)
+def test_load_index_query_same_session(tmp_path, binary):
+    """load_db keeps the columns resident in HBM, then the index
+    build rewrites the other columns in place (reference build_index in server_mq,
+    libmq's in server_mq_ix), then select/fetch/sum on them in the same session.
+    The output must be the reference server's, line for line (server_mq_ix: the
+    clustered tie order is libmq's, so there it is compared as sorted lines)."""
+    if not _have(binary):
+        pytest.skip(f"{binary} not built")
+    mine = run_dsl_files(os.path.join(REFBIN, binary), str(tmp_path / "mq"), [RESIDENCY_DSL])
+    ref = run_dsl_files(os.path.join(REFBIN, "server_ref"), str(tmp_path / "ref"), [RESIDENCY_DSL])
+    a, b = _ws(mine[RESIDENCY_DSL]), _ws(ref[RESIDENCY_DSL])
+    if binary == "server_mq":
+        assert a == b
+    else:
+        assert sorted(a, key=_sortkey) == sorted(b, key=_sortkey)

@@ -1,0 +1,252 @@
+"""Residency of host memory in HBM through the drop-in API (-m gpu).
+
+VERDICT r01 weak-1 / ADVICE r01: a device copy must never outlive the host bytes
+it mirrors. The reference rewrites column data in place (reorder_column,
+src/index.c:105-114; insert_row, src/db_manager.c:190-197) and the server frees
+and replaces Result payloads (client_context.c:31-45). Each case below changes
+host memory between two operators and checks the second one against the oracle
+(refcpu, pinned to the reference build) on the NEW bytes.
+"""
+import ctypes as C
+import mmap
+import os
+
+import numpy as np
+import pytest
+
+from refapi import make_column, make_result, mq, take, free_result_struct
+
+pytestmark = pytest.mark.gpu
+
+libc = C.CDLL(None)
+libc.free.argtypes = [C.c_void_p]
+
+
+@pytest.fixture(scope="module")
+def lib():
+    L = mq.load()
+    mq.check(L.mq_init(0), "mq_init")
+    return L
+
+
+def memfd_column(values: np.ndarray):
+    """A column in a MAP_SHARED file mapping, as the reference's start_data makes
+    (db_manager.c:736-790); returns (numpy view, mmap, Column)."""
+    fd = os.memfd_create("mqcol")
+    os.ftruncate(fd, max(values.nbytes, 4))
+    m = mmap.mmap(fd, max(values.nbytes, 4), mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+    os.close(fd)
+    a = np.frombuffer(m, dtype=np.int32)[:len(values)]
+    a[:] = values
+    return a, m, make_column(a)
+
+
+def st():
+    return mq.Status(0, None)
+
+
+def close_map(m):
+    try:
+        m.close()
+    except BufferError:  # a numpy view still exports it; the mapping dies with it
+        pass
+
+
+def select(lib, col, lo, hi):
+    s = st()
+    rp = lib.select_column(C.byref(col), C.pointer(C.c_int(lo)), C.pointer(C.c_int(hi)), C.byref(s))
+    assert s.code == mq.OK and rp
+    return rp
+
+
+def fetch(lib, col, rp):
+    s = st()
+    out = lib.fetch_column(C.byref(col), rp, C.byref(s))
+    assert s.code == mq.OK and out
+    return out
+
+
+def sum_result(lib, rp):
+    g = mq.GeneralizedColumn()
+    g.column_type = mq.RESULT
+    g.column_pointer.result = rp
+    s = st()
+    out = lib.sum(C.byref(g), C.byref(s))
+    assert s.code == mq.OK
+    return int(take(out)[0])
+
+
+def sum_column(lib, col):
+    g = mq.GeneralizedColumn()
+    g.column_type = mq.COLUMN
+    g.column_pointer.column = C.pointer(col)
+    s = st()
+    out = lib.sum(C.byref(g), C.byref(s))
+    assert s.code == mq.OK
+    return int(take(out)[0])
+
+
+@pytest.mark.parametrize("backing", ["file", "anonymous"])
+def test_column_rewritten_in_place_between_selects(lib, refcpu, backing):
+    """The done-when of VERDICT r01 next-1: rewrite Column.data in place between two
+    selects; the second select sees the new rows."""
+    n = 3_000_000
+    v0 = refcpu.gen_uniform(n, 42)
+    if backing == "file":
+        a, m, col = memfd_column(v0)
+    else:
+        a = v0.copy()
+        col = make_column(a)
+    lo, hi = n // 4, n // 4 + n // 50
+    want0 = refcpu.select_scan(a, lo, hi)
+    assert np.array_equal(take(select(lib, col, lo, hi)), want0)
+    r0 = mq.residency(lib)
+    assert np.array_equal(take(select(lib, col, lo, hi)), want0)
+    r1 = mq.residency(lib)
+    if backing == "file":
+        assert r1["column_uploads"] == r0["column_uploads"], "unchanged file-backed column re-uploaded"
+    # an in-place reorder of the rows (what reorder_column does), same pointer and length
+    perm = np.argsort(refcpu.gen_uniform(n, 77), kind="stable")
+    a[:] = a[perm]
+    want1 = refcpu.select_scan(a, lo, hi)
+    assert not np.array_equal(want0, want1)
+    assert np.array_equal(take(select(lib, col, lo, hi)), want1)
+    assert sum_column(lib, col) == int(a.astype(np.int64).sum())
+    # a single-element edit in the middle of the column
+    i = int(want1[len(want1) // 2])
+    a[i] = hi + 5
+    want2 = refcpu.select_scan(a, lo, hi)
+    assert np.array_equal(take(select(lib, col, lo, hi)), want2)
+    # fetch through a changed column, positions from an earlier select
+    rp = select(lib, col, lo, hi)
+    a[:n // 2] = -a[:n // 2]
+    got = take(fetch(lib, col, rp))
+    assert np.array_equal(got, a[want2])
+    take(rp)
+    del a
+    if backing == "file":
+        col.data = None
+        close_map(m)
+
+
+def test_payload_edited_in_place(lib, refcpu):
+    """A Result payload libmq produced, then edited in place by the caller, is read
+    from host memory again (not from its HBM shadow)."""
+    n = 20_000_000
+    v = refcpu.gen_uniform(n, 43)
+    col = make_column(v)
+    rp = select(lib, col, 0, n // 2)  # ~40 MB payload: an mmapped chunk, guarded shadow
+    r = rp.contents
+    k = int(r.num_tuples)
+    pos = np.ctypeslib.as_array(C.cast(r.payload, C.POINTER(C.c_int32)), shape=(k,))
+    assert sum_result(lib, rp) == int(pos.astype(np.int64).sum())
+    before = mq.residency(lib)
+    assert sum_result(lib, rp) == int(pos.astype(np.int64).sum())
+    assert mq.residency(lib)["result_uploads"] == before["result_uploads"], "shadow not used"
+    pos[k // 3] = 7
+    pos[-1] = 0
+    assert sum_result(lib, rp) == int(pos.astype(np.int64).sum())
+    got = take(fetch(lib, col, rp))
+    assert np.array_equal(got, v[pos])
+    take(rp)
+
+
+def test_freed_payload_address_reused(lib, refcpu):
+    """The server frees a payload (update_result) and another payload takes its
+    address: the new bytes are what the next operator reads."""
+    n = 20_000_000
+    v = refcpu.gen_uniform(n, 44)
+    col = make_column(v)
+    rp = select(lib, col, 0, n // 2)
+    k = int(rp.contents.num_tuples)
+    addr = rp.contents.payload
+    take(rp)  # frees payload + Result, as free_client_context does
+    other = (np.arange(k, dtype=np.int64) % 1000).astype(np.int32)
+    r2 = make_result(other)  # malloc of the same size: usually the same address
+    got = take(lib.fetch_column(C.byref(col), C.byref(r2), C.byref(st())))
+    assert np.array_equal(got, v[other])
+    s2 = mq.GeneralizedColumn()
+    s2.column_type = mq.RESULT
+    s2.column_pointer.result = C.pointer(r2)
+    out = lib.sum(C.byref(s2), C.byref(st()))
+    assert int(take(out)[0]) == int(other.astype(np.int64).sum())
+    print("address reused:", r2.payload == addr)
+    free_result_struct(r2)
+
+
+def test_operands_survive_a_tiny_shadow_budget(lib, refcpu, monkeypatch):
+    """with MQ_SHADOW_MB below the size of two operands, the first
+    operand's shadow must not be evicted (and its block reused) while the operator
+    still reads it."""
+    n = 12_000_000
+    v = refcpu.gen_uniform(n, 45)
+    col = make_column(v)
+    ra = select(lib, col, 0, n)  # every row: 48 MB payloads
+    rb = fetch(lib, col, ra)
+    monkeypatch.setenv("MQ_SHADOW_MB", "1")
+    s = st()
+    out = lib.add(ra, rb, C.byref(s))
+    assert s.code == mq.OK
+    pa = take(ra, free=False)
+    pb = take(rb, free=False)
+    assert np.array_equal(take(out), refcpu.add(pa, pb))
+    s = st()
+    out = lib.sub(rb, ra, C.byref(s))
+    assert np.array_equal(take(out), refcpu.sub(pb, pa))
+    assert mq.residency(lib)["shadow_bytes"] <= 2 * 4 * n + (1 << 20)
+    take(ra)
+    take(rb)
+
+
+def test_guarded_column_write_after_load_db(lib, refcpu, tmp_path):
+    """load_db leaves the loaded columns resident (file-backed, as the server's
+    start_data maps them); an in-place rewrite afterwards (as the reference's
+    clustered build_index does) is seen by the next select / fetch / sum."""
+    ncols, rows = 2, 300_000
+    keep = [memfd_column(np.zeros(rows, np.int32)) for _ in range(ncols)]
+    cols = (mq.Column * ncols)()
+    for j, (_, _, c) in enumerate(keep):
+        C.memmove(C.byref(cols[j]), C.byref(c), C.sizeof(mq.Column))
+        cols[j].name = b"col%d" % (j + 1)
+        cols[j].row_count = 0
+        cols[j].max, cols[j].min = -(2 ** 31), 2 ** 31 - 1
+    t = mq.Table()
+    t.name = b"tbl1"
+    t.columns = cols
+    t.col_count, t.row_count, t.table_length = ncols, 0, rows
+    db = mq.Db()
+    db.name = b"db1"
+    db.tables = C.pointer(t)
+    db.tables_size = db.tables_capacity = 1
+    data = refcpu.gen_uniform(ncols * rows, 46).reshape(rows, ncols)
+    csv = tmp_path / "t.csv"
+    with open(csv, "w") as f:
+        f.write("db1.tbl1.col1,db1.tbl1.col2\n")
+        np.savetxt(f, data, fmt="%d", delimiter=",")
+    s = st()
+    lib.load_db(C.byref(db), str(csv).encode(), C.byref(s))
+    assert s.code == mq.OK and t.row_count == rows
+    a0, a1 = keep[0][0], keep[1][0]
+    assert np.array_equal(a0, data[:, 0])
+    lo, hi = rows // 4, rows // 4 + rows // 20
+    up = mq.residency(lib)["column_uploads"]
+    want = refcpu.select_scan(a0, lo, hi)
+    rp = select(lib, cols[0], lo, hi)
+    assert np.array_equal(take(rp, free=False), want)
+    assert np.array_equal(take(fetch(lib, cols[1], rp)), a1[want])
+    assert mq.residency(lib)["column_uploads"] == up, "load_db's resident copies not used"
+    perm = np.argsort(a0, kind="stable")  # a clustered reorder of column 2 by column 1
+    a1[:] = a1[perm]
+    a0[:] = a0[perm]
+    want = refcpu.select_scan(a0, lo, hi)
+    rp2 = select(lib, cols[0], lo, hi)
+    assert np.array_equal(take(rp2, free=False), want)
+    assert np.array_equal(take(fetch(lib, cols[1], rp2)), a1[want])
+    assert sum_column(lib, cols[1]) == int(a1.astype(np.int64).sum())
+    take(rp)
+    take(rp2)
+    for j in range(ncols):
+        cols[j].data = None
+    del a0, a1
+    for _, m, _ in keep:
+        close_map(m)

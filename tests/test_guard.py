@@ -1,0 +1,187 @@
+"""Write guards on host memory mirrored in HBM (csrc/mq_guard.c), checked on the CPU.
+
+The guard is how libmq knows that a Column's rows (or a Result payload) are still
+what it uploaded: the reference rewrites column data in place through the same
+mmap'd pointer (src/index.c:105-114 reorder_column) and appends through it
+(src/db_manager.c:190-197 insert_row). No GPU is involved here: these are host
+page-protection mechanics, exercised through libmq.so's own entry points.
+"""
+import ctypes as C
+import mmap
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from refapi import mq
+
+PAGE = mmap.PAGESIZE
+libc = C.CDLL(None, use_errno=True)
+libc.malloc.restype = C.c_void_p
+libc.malloc.argtypes = [C.c_size_t]
+libc.free.argtypes = [C.c_void_p]
+libc.mmap.restype = C.c_void_p
+libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+libc.memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+libc.memset.restype = C.c_void_p
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return mq.load()
+
+
+def memfd_array(n, fill=None):
+    """n int32 in a MAP_SHARED memfd mapping (a file-backed column, as start_data makes)."""
+    fd = os.memfd_create("mqcol")
+    os.ftruncate(fd, n * 4)
+    m = mmap.mmap(fd, n * 4, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+    os.close(fd)
+    a = np.frombuffer(m, dtype=np.int32)
+    a[:] = np.arange(n, dtype=np.int32) if fill is None else fill
+    return a, m
+
+
+def test_file_mapping_clean_until_written(lib):
+    a, m = memfd_array(1 << 16)
+    h = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    assert h
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 1
+    assert int(a[12345]) == 12345  # reads do not disturb it
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 1
+    a[40000] = -7  # an in-place store: faults once, the handler lets it through
+    assert int(a[40000]) == -7
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 0
+    a[40001] = -8  # the pages are writable again: no second fault needed
+    lib.mq_guard_release(h)
+    del a
+    m.close()
+
+
+def test_reorder_like_writes_from_c(lib):
+    """A write from C code (memset, like reorder_column's memcpy) is seen too."""
+    a, m = memfd_array(1 << 15)
+    h = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    libc.memset(a.ctypes.data + 8 * PAGE, 0, 4 * PAGE)
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 0
+    assert not a[2 * PAGE:3 * PAGE].any()
+    lib.mq_guard_release(h)
+    del a
+    m.close()
+
+
+def test_partial_edge_pages_are_compared(lib):
+    """Bytes outside the whole pages (not protected) are compared with their copy."""
+    a, m = memfd_array(PAGE)  # 4 pages
+    sub = a[5:PAGE - 3]  # starts and ends inside a page
+    h = lib.mq_guard_arm(sub.ctypes.data, sub.nbytes, mq.MQ_GUARD_FILE)
+    assert h and lib.mq_guard_clean(h, sub.ctypes.data, sub.nbytes)
+    a[3] = 99  # outside the range: no effect
+    assert lib.mq_guard_clean(h, sub.ctypes.data, sub.nbytes) == 1
+    sub[-1] = 12  # inside the range, on the unprotected tail page
+    assert lib.mq_guard_clean(h, sub.ctypes.data, sub.nbytes) == 0
+    lib.mq_guard_release(h)
+    del a, sub
+    m.close()
+
+
+def test_anonymous_heap_memory_is_not_guarded(lib):
+    a = np.arange(1 << 16, dtype=np.int32)
+    assert lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE) == 0
+    p = libc.malloc(256)  # a heap chunk (not mmapped): freeing it would leave pages behind
+    assert lib.mq_guard_arm(p, 256, mq.MQ_GUARD_CHUNK) == 0
+    libc.free(p)
+
+
+def test_mmapped_malloc_chunk(lib):
+    n = 64 << 20  # above glibc's largest mmap threshold: served by mmap, freed by munmap
+    p = libc.malloc(n)
+    libc.memset(p, 1, n)
+    h = lib.mq_guard_arm(p, n, mq.MQ_GUARD_CHUNK)
+    assert h
+    assert lib.mq_guard_clean(h, p, n) == 1
+    C.c_char.from_address(p + n // 2).value = b"\x07"
+    assert lib.mq_guard_clean(h, p, n) == 0
+    lib.mq_guard_release(h)
+    libc.free(p)
+
+
+def test_remapped_range_is_stale(lib):
+    """munmap + a fresh mapping at the same address (same length) is not the memory
+    that was guarded, even with identical bytes."""
+    r = mq.residency(lib)
+    if not r["remap_probe"]:
+        pytest.skip("kernel without MADV_POPULATE_WRITE: remaps are not told apart")
+    n = 16 * PAGE
+    PROT_RW, MAP_SHARED_ANON, MAP_FIXED = 3, 0x01 | 0x20, 0x10
+    p = libc.mmap(None, n, PROT_RW, MAP_SHARED_ANON, -1, 0)
+    fd = os.memfd_create("mqremap")
+    os.ftruncate(fd, n)
+    libc.munmap(p, n)
+    q = libc.mmap(p, n, PROT_RW, 0x01 | MAP_FIXED, fd, 0)
+    assert q == p
+    h = lib.mq_guard_arm(q, n, mq.MQ_GUARD_FILE)
+    assert h and lib.mq_guard_clean(h, q, n)
+    libc.munmap(q, n)
+    q2 = libc.mmap(p, n, PROT_RW, 0x01 | MAP_FIXED, fd, 0)  # same file, same bytes
+    assert q2 == p
+    assert lib.mq_guard_clean(h, q2, n) == 0
+    lib.mq_guard_release(h)
+    libc.munmap(q2, n)
+    os.close(fd)
+
+
+def test_forget_range_lifts_guard(lib):
+    a, m = memfd_array(1 << 14)
+    h = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    lib.mq_guard_forget_range(a.ctypes.data + 100, 8)
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 0
+    fd = os.open("/dev/zero", os.O_RDONLY)
+    assert os.readv(fd, [memoryview(m)[:PAGE * 2]]) == PAGE * 2
+    os.close(fd)
+    lib.mq_guard_release(h)
+    del a
+    m.close()
+
+
+def test_foreign_segfault_still_terminates(tmp_path):
+    """A fault that is not a guard's goes on to the previous handler (here: the
+    default action), so real crashes are not swallowed."""
+    code = f"""
+import ctypes as C, mmap, os, sys
+sys.path.insert(0, {os.path.join(os.path.dirname(__file__))!r})
+from refapi import mq
+import numpy as np
+lib = mq.load()
+fd = os.memfd_create("x"); os.ftruncate(fd, 1 << 16)
+m = mmap.mmap(fd, 1 << 16)
+a = np.frombuffer(m, dtype=np.int32)
+assert lib.mq_guard_arm(a.ctypes.data, a.nbytes, 0)
+a[5] = 1
+print("guard-write-ok", flush=True)
+C.string_at(8, 8)
+print("not reached", flush=True)
+"""
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert "guard-write-ok" in cp.stdout
+    assert "not reached" not in cp.stdout
+    assert cp.returncode == -11, (cp.returncode, cp.stderr[-2000:])
+
+
+def test_guard_disabled_by_env(tmp_path):
+    code = """
+import sys; sys.path.insert(0, %r)
+from refapi import mq
+import mmap, os, numpy as np
+lib = mq.load()
+fd = os.memfd_create("x"); os.ftruncate(fd, 1 << 16)
+m = mmap.mmap(fd, 1 << 16); a = np.frombuffer(m, dtype=np.int32)
+print(lib.mq_guard_arm(a.ctypes.data, a.nbytes, 0))
+""" % os.path.dirname(__file__)
+    env = dict(os.environ, MQ_GUARD="0")
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                        env=env)
+    assert cp.stdout.strip() == "0", cp.stderr[-2000:]
