@@ -43,6 +43,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <time.h>
 #include <unistd.h>
 
 #ifndef MADV_POPULATE_WRITE
@@ -226,6 +227,11 @@ void mq_guard_forget_range(uintptr_t addr, size_t bytes) {
     }
 }
 
+int mq_guard_chunk_ok(const void* p) {
+    /* glibc chunk header: the size word before p has IS_MMAPPED (0x2) set */
+    return p && (((const size_t*)p)[-1] & 2) != 0;
+}
+
 uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {
     if (!mq_guard_enabled() || !p || !bytes) return 0;
     const uintptr_t a = (uintptr_t)p, b = a + bytes;
@@ -234,8 +240,7 @@ uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {
     if (hi <= lo) lo = hi = 0;
     int prot = PROT_READ | PROT_WRITE;
     if (kind == MQ_GUARD_CHUNK) {
-        /* glibc chunk header: the size word before p has IS_MMAPPED (0x2) set */
-        if (!(((const size_t*)p)[-1] & 2)) return 0;
+        if (!mq_guard_chunk_ok(p)) return 0;
     } else {
         if (lo == hi) return 0;
         if ((prot = vma_prot(lo, hi, 1)) < 0) return 0;
@@ -286,7 +291,16 @@ static Guard* lookup(uint64_t h) {
     return (g->gen == (uint32_t)(h >> 32) && atomic_load(&g->state) != G_FREE) ? g : NULL;
 }
 
+static double gnow(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 int mq_guard_clean(uint64_t h, const void* p, size_t bytes) {
+    static int tr = -1;
+    if (tr < 0) tr = getenv("MQ_TRACE") && getenv("MQ_TRACE")[0] == '1';
+    const double t0 = tr ? gnow() : 0;
     Guard* g = lookup(h);
     int ok = g && g->p == (const unsigned char*)p && g->bytes == bytes && atomic_load(&g->state) == G_ARMED &&
              memcmp(g->edge, p, g->head) == 0 &&
@@ -294,6 +308,7 @@ int mq_guard_clean(uint64_t h, const void* p, size_t bytes) {
              (g->hi == g->lo || still_armed(g->lo));
     if (ok) g_stats.clean++;
     else g_stats.stale++;
+    if (tr) fprintf(stderr, "mq-trace guard_clean(%zu B)       %9.3f ms\n", bytes, 1e3 * (gnow() - t0));
     return ok;
 }
 

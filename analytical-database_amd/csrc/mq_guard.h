@@ -13,6 +13,8 @@ enum { MQ_GUARD_FILE = 0, MQ_GUARD_CHUNK = 1 };
 
 /* 0 when MQ_GUARD=0 (then nothing is guarded and host copies are single-use). */
 int mq_guard_enabled(void);
+/* 1 when p starts a malloc chunk glibc served with mmap (MQ_GUARD_CHUNK can cover it). */
+int mq_guard_chunk_ok(const void* p);
 /* Guard [p, p+bytes); returns a handle, or 0 when the memory is not guardable. */
 uint64_t mq_guard_arm(const void* p, size_t bytes, int kind);
 /* 1 when nothing wrote into [p, p+bytes) since the guard was armed. */

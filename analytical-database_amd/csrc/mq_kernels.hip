@@ -831,7 +831,7 @@ struct StageState {
 // Rows are 32-bit here: positions are int32, so n < 2^31 (mq_select_positions).
 template <bool PAYLOAD, int BUF, bool FULL, int J>
 __device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint32_t t0, uint32_t E, uint32_t lo,
-                                           uint32_t wm1, int lane, int* buf,
+                                           uint32_t wm1, int32_t base, int lane, int* buf,
                                            const int* __restrict__ payload,
                                            unsigned long long* __restrict__ bm, int* __restrict__ spill,
                                            uint32_t r0, int& rlo, int& rhi) {
@@ -864,10 +864,10 @@ __device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint32_t t0, 
                 st.flushed = __builtin_amdgcn_readfirstlane(st.flushed + need);
             }
             uint32_t k = rank_lt(m3, rank_lt(m2, rank_lt(m1, rank_lt(m0, st.fill))));
-            if (p0) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 0] : (int)(row0 + 0);
-            if (p1) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 1] : (int)(row0 + 1);
-            if (p2) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 2] : (int)(row0 + 2);
-            if (p3) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 3] : (int)(row0 + 3);
+            if (p0) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 0] : (int)(row0 + 0) + base;
+            if (p1) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 1] : (int)(row0 + 1) + base;
+            if (p2) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 2] : (int)(row0 + 2) + base;
+            if (p3) buf[(k++) % (uint32_t)BUF] = PAYLOAD ? payload[row0 + 3] : (int)(row0 + 3) + base;
             st.fill = __builtin_amdgcn_readfirstlane(st.fill + c);
             return;
         }
@@ -900,6 +900,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lo = pred.lo, wm1 = pred.wm1;
+    const int32_t rbase = pred.base;
     const uint32_t b = blockIdx.x;
     uint64_t S = ((uint64_t)b * kWaves + (uint64_t)wave) * rw;
     if (S > n) S = n;
@@ -925,7 +926,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
 #pragma unroll
         for (int j = 0; j < kStTiles; j++) {
             switch (j) {  // J must be a constant for the writelane lane index
-#define MQ_ST(JJ) case JJ: stage_tile<PAYLOAD, BUF, true, JJ>(st, v[JJ], t + JJ * 256, E32, lo, wm1, lane, s_buf[wave], payload, bm, spill, r0, rlo, rhi); break;
+#define MQ_ST(JJ) case JJ: stage_tile<PAYLOAD, BUF, true, JJ>(st, v[JJ], t + JJ * 256, E32, lo, wm1, rbase, lane, s_buf[wave], payload, bm, spill, r0, rlo, rhi); break;
                 MQ_ST(0) MQ_ST(1) MQ_ST(2) MQ_ST(3) MQ_ST(4) MQ_ST(5) MQ_ST(6) MQ_ST(7)
 #undef MQ_ST
             }
@@ -943,7 +944,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         v.y = row + 1 < E32 ? col[row + 1] : 0;
         v.z = row + 2 < E32 ? col[row + 2] : 0;
         v.w = row + 3 < E32 ? col[row + 3] : 0;
-        stage_tile<PAYLOAD, BUF, false, -1>(st, v, t, E32, lo, wm1, lane, s_buf[wave], payload, bm, spill,
+        stage_tile<PAYLOAD, BUF, false, -1>(st, v, t, E32, lo, wm1, rbase, lane, s_buf[wave], payload, bm, spill,
                                             (t - S32) >> 8, rlo, rhi);
     }
     int* buf = s_buf[wave];
@@ -1056,10 +1057,10 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
                                                             __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
                     int* q = out + oj + pre;
                     unsigned int k = 0;
-                    if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][0] : (int)(rj + 0);
-                    if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][1] : (int)(rj + 1);
-                    if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][2] : (int)(rj + 2);
-                    if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][3] : (int)(rj + 3);
+                    if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][0] : (int)(rj + 0) + rbase;
+                    if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][1] : (int)(rj + 1) + rbase;
+                    if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][2] : (int)(rj + 2) + rbase;
+                    if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][3] : (int)(rj + 3) + rbase;
                 }
             }
         } else if (c) {
@@ -1070,10 +1071,10 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
                 const int l = __ffsll((long long)m) - 1;
                 m &= m - 1;
                 const uint64_t r = row0 + 4 * (uint64_t)l;
-                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0);
-                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1);
-                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2);
-                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3);
+                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0) + rbase;
+                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1) + rbase;
+                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2) + rbase;
+                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3) + rbase;
             }
         }
         o += tot;
@@ -1379,6 +1380,39 @@ __global__ __launch_bounds__(kTPB) void k_gen_join(int* __restrict__ out, uint64
     }
 }
 
+// Device-to-device copy (mq_memcpy_d2d): 16-byte words grid-stride, 4 in flight per
+// lane; the byte tail by the first threads. hipMemcpyAsync D2D measured 23 ms for
+// 40 MB on the API path (an engine copy behind the stream); this runs at HBM speed.
+__global__ __launch_bounds__(kTPB) void k_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                 uint64_t n16, unsigned char* __restrict__ dtail,
+                                                 const unsigned char* __restrict__ stail, uint32_t ntail) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+    const uint32_t t = blockIdx.x * kTPB + threadIdx.x;
+    if (t < ntail) dtail[t] = stail[t];
+}
+
+__global__ __launch_bounds__(kTPB) void k_copy1(unsigned char* __restrict__ dst, const unsigned char* __restrict__ src,
+                                                uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+// out[i] += base for the *count positions a non-staging select wrote (row shards)
+__global__ __launch_bounds__(kTPB) void k_add_base(int* __restrict__ out, const unsigned long long* __restrict__ count,
+                                                   int32_t base) {
+    const uint64_t n = *count, stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] += base;
+}
+
 __global__ __launch_bounds__(kTPB) void k_iota(int* __restrict__ out, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] = (int)i;
@@ -1510,6 +1544,7 @@ bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
     if (width <= 0) return false;
     p->lo = (uint32_t)lo;
     p->wm1 = (uint32_t)(width - 1);
+    p->base = 0;
     return true;
 }
 
@@ -1787,9 +1822,77 @@ int mq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
     return MQ_OK;
 }
 
+// D2H through pinned staging buffers: the DMA fills a ring of 4 x 8 MB pinned
+// buffers and the host copies each chunk out while the next ones are in flight.
+// A direct D2H into pageable memory makes the runtime register those pages with
+// the driver; write-protecting them afterwards (mq_guard_arm) then costs the next
+// kernel 17-30 ms (tools/guard_stall.hip). Staged, the destination is never
+// registered.
+namespace {
+constexpr int kStageBufs = 4;
+constexpr size_t kStageBytes = (size_t)8 << 20;
+struct Staging {
+    void* buf[kStageBufs];
+    hipEvent_t ev[kStageBufs];
+    bool ready;
+};
+thread_local Staging g_staging[kMaxDev];
+}  // namespace
+
+int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream) {
+    if (bytes == 0) return MQ_OK;
+    int d;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    Staging& S = g_staging[d];
+    if (!S.ready) {
+        for (int i = 0; i < kStageBufs; i++) {
+            HIPCHK(hipHostMalloc(&S.buf[i], kStageBytes, hipHostMallocDefault));
+            HIPCHK(hipEventCreateWithFlags(&S.ev[i], hipEventDisableTiming));
+        }
+        S.ready = true;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const size_t nchunks = (bytes + kStageBytes - 1) / kStageBytes;
+    auto issue = [&](size_t c) -> int {
+        const size_t off = c * kStageBytes, len = bytes - off < kStageBytes ? bytes - off : kStageBytes;
+        const int b = (int)(c % kStageBufs);
+        HIPCHK(hipMemcpyAsync(S.buf[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(S.ev[b], st));
+        return MQ_OK;
+    };
+    for (size_t c = 0; c < nchunks && c < (size_t)kStageBufs; c++)
+        if ((rc = issue(c))) return rc;
+    for (size_t c = 0; c < nchunks; c++) {
+        const int b = (int)(c % kStageBufs);
+        HIPCHK(hipEventSynchronize(S.ev[b]));
+        const size_t off = c * kStageBytes, len = bytes - off < kStageBytes ? bytes - off : kStageBytes;
+        memcpy(static_cast<char*>(dst) + off, S.buf[b], len);
+        if (c + kStageBufs < nchunks && (rc = issue(c + kStageBufs))) return rc;
+    }
+    return MQ_OK;
+}
+
 int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
     if (bytes == 0) return MQ_OK;
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!dst || !src) return set_err(MQ_EINVAL, "mq_memcpy_d2d: NULL pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
+        const uint64_t n16 = bytes / 16;
+        const uint32_t tail = (uint32_t)(bytes % 16);
+        const uint32_t g = stream_grid(s, n16 > tail ? n16 : tail);
+        hipLaunchKernelGGL(k_copy16, dim3(g), dim3(kTPB), 0, st, static_cast<uint4*>(dst),
+                           static_cast<const uint4*>(src), n16, static_cast<unsigned char*>(dst) + n16 * 16,
+                           static_cast<const unsigned char*>(src) + n16 * 16, tail);
+        LAUNCHCHK("k_copy16");
+    } else {
+        hipLaunchKernelGGL(k_copy1, dim3(stream_grid(s, bytes)), dim3(kTPB), 0, st, static_cast<unsigned char*>(dst),
+                           static_cast<const unsigned char*>(src), (uint64_t)bytes);
+        LAUNCHCHK("k_copy1");
+    }
     return MQ_OK;
 }
 
@@ -2007,6 +2110,7 @@ int mq_hashset_elements(const int32_t* d_table, uint64_t size, int32_t* d_out, u
     Pred p;
     p.lo = 1u;
     p.wm1 = 0xFFFFFFFEu;
+    p.base = 0;
     return run_select_stage(d_table, d_table, size, p, d_out, d_count, d_ws, st, s);
 }
 
@@ -2030,6 +2134,37 @@ int mq_reduce(const int32_t* d_vals, uint64_t n, mq_agg* d_out, void* d_ws, size
 int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int has_low,
                         int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
                         uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream) {
+    return mq_select_positions_at(d_col, d_payload, n, 0, has_low, low, has_high, high, d_pos_out, d_count,
+                                  d_ws, ws_bytes, stream);
+}
+
+namespace {
+int select_positions_impl(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int32_t row_base,
+                          int has_low, int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
+                          uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream);
+}
+
+int mq_select_positions_at(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int32_t row_base,
+                           int has_low, int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
+                           uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream) {
+    if (row_base < 0 || (uint64_t)row_base + n > (uint64_t)INT32_MAX)
+        return set_err(MQ_EINVAL, "mq_select_positions_at: rows [%d, %d + %llu) beyond int32 positions", row_base,
+                       row_base, (unsigned long long)n);
+    int rc = select_positions_impl(d_col, d_payload, n, d_payload ? 0 : row_base, has_low, low, has_high, high,
+                                   d_pos_out, d_count, d_ws, ws_bytes, stream);
+    if (rc || d_payload || row_base == 0 || positions_impl() == kPosStage || n == 0) return rc;
+    DevState* s;
+    if ((rc = ensure_ready(&s))) return rc;
+    hipLaunchKernelGGL(k_add_base, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream, d_pos_out,
+                       reinterpret_cast<const unsigned long long*>(d_count), row_base);
+    LAUNCHCHK("k_add_base");
+    return MQ_OK;
+}
+
+namespace {
+int select_positions_impl(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int32_t row_base,
+                          int has_low, int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
+                          uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream) {
     DevState* s;
     int rc = ensure_ready(&s);
     if (rc) return rc;
@@ -2049,6 +2184,7 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
     if (!d_ws || ws_bytes < mq_scan_workspace_bytes(n))
         return set_err(MQ_EINVAL, "mq_select_positions: workspace too small (%zu < %zu)", ws_bytes,
                        mq_scan_workspace_bytes(n));
+    p.base = row_base;  // k_select_stage adds it as it writes; the others via k_add_base
     const PosImpl impl = positions_impl();
     if (impl == kPosStage)
         return run_select_stage(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, st, s);
@@ -2080,6 +2216,7 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
     LAUNCHCHK("k_compact");
     return MQ_OK;
 }
+}  // namespace
 
 int mq_index_select(const int32_t* d_values, const uint64_t* d_positions, uint64_t n, int32_t low,
                     int32_t high, int32_t* d_pos_out, uint64_t* d_count, void* stream) {
@@ -2105,6 +2242,30 @@ int mq_index_select(const int32_t* d_values, const uint64_t* d_positions, uint64
     hipLaunchKernelGGL(k_index_copy, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, d_positions,
                        run_buf[d], d_pos_out);
     LAUNCHCHK("k_index_copy");
+    return MQ_OK;
+}
+
+int mq_fetch_at(const int32_t* d_col, int32_t row_base, const int32_t* d_pos, uint64_t k, int32_t* d_out,
+                void* stream) {
+    if (row_base < 0) return set_err(MQ_EINVAL, "mq_fetch_at: negative row base");
+    // k_fetch reads col[pos]; positions of this shard lie in [row_base, row_base + rows),
+    // so the column pointer is taken row_base rows back (never dereferenced there)
+    return mq_fetch(d_col - row_base, d_pos, k, d_out, stream);
+}
+
+int mq_stream_create(void** stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!stream) return set_err(MQ_EINVAL, "mq_stream_create: NULL out pointer");
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    *stream = st;
+    return MQ_OK;
+}
+
+int mq_stream_destroy(void* stream) {
+    if (stream) HIPCHK(hipStreamDestroy((hipStream_t)stream));
     return MQ_OK;
 }
 

@@ -25,6 +25,7 @@
 
 #include <fcntl.h>
 #include <limits.h>
+#include <malloc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -115,6 +116,10 @@ typedef struct {
     unsigned long long op;
 } IndexEntry;
 
+/* Payloads from this size on keep an HBM shadow (ready() lowers glibc's mmap
+ * threshold to it, so they are mmapped chunks, which a guard can cover). */
+#define SHADOW_MIN_BYTES ((size_t)1 << 20)
+
 #define MAX_COLS 1024
 #define MAX_SHADOWS 4096
 #define MAX_INDEXES 256
@@ -145,6 +150,20 @@ static double now_s(void) {
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* MQ_TRACE=1: host-side phase times of the API path on stderr (diagnostics). */
+static int trace_on(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MQ_TRACE");
+        v = e && e[0] == '1';
+    }
+    return v;
+}
+#define TRACE(label, t0)                                                                    \
+    do {                                                                                    \
+        if (trace_on()) fprintf(stderr, "mq-trace %-24s %9.3f ms\n", label, 1e3 * (now_s() - (t0))); \
+    } while (0)
+
 static int fail(Status* st, const char* what, int rc) {
     fprintf(stderr, "libmq: %s failed (%d): %s\n", what, rc, mq_last_error());
     if (st) st->code = ERROR;
@@ -163,6 +182,11 @@ static int ready(Status* st) {
         g_ready = -1;
         return fail(st, "device init", rc);
     }
+    /* Result payloads of >= 1 MB come from mmap (and go back to it on free), which
+     * is what lets a write guard cover them; glibc's dynamic threshold would
+     * otherwise rise to the last freed size (up to 32 MB) and serve them from the
+     * heap. Affects only where large blocks of this process come from. */
+    mallopt(M_MMAP_THRESHOLD, (int)SHADOW_MIN_BYTES);
     g_stream = mq_default_stream();
     if (!g_stream) {
         g_ready = -1;
@@ -180,9 +204,11 @@ static int ready(Status* st) {
 /* Start of an operator of the reference API: a new op number (what the previous
  * operator held may now be evicted) and drop the copies no later call can use. */
 static int op_begin(Status* st) {
+    const double t0 = now_s();
     if (ready(st)) return -1;
     g_op++;
     sweep();
+    TRACE("op_begin", t0);
     return 0;
 }
 
@@ -196,6 +222,15 @@ static int h2d(void* d, const void* h, size_t bytes) {
 static int d2h(void* h, const void* d, size_t bytes) {
     double t0 = now_s();
     int rc = mq_memcpy_d2h(h, d, bytes, g_stream);
+    g_xfer_s += now_s() - t0;
+    return rc;
+}
+
+/* D2H into memory that will be write-guarded: through pinned staging, so the
+ * guard's mprotect does not stall the GPU (mq_memcpy_d2h_staged). */
+static int d2h_staged(void* h, const void* d, size_t bytes) {
+    double t0 = now_s();
+    int rc = mq_memcpy_d2h_staged(h, d, bytes, g_stream);
     g_xfer_s += now_s() - t0;
     return rc;
 }
@@ -260,6 +295,7 @@ static void shadow_make_room(size_t bytes) {
 static void sweep(void) {
     for (int i = g_nshadows - 1; i >= 0; i--)
         if (g_shadows[i].op != g_op && !g_shadows[i].guard) shadow_drop(i);
+    shadow_make_room(0); /* back within the budget the last operator may have exceeded */
     for (int i = g_ncols - 1; i >= 0; i--)
         if (g_cols[i].owned && g_cols[i].op != g_op && g_cols[i].rows && !g_cols[i].guard) col_drop(&g_cols[i]);
 }
@@ -325,10 +361,12 @@ static ColEntry* col_put(Column* c, void* dev) {
 }
 
 static int column_device(Column* c, const int32_t** d, Status* st) {
+    const double t0 = now_s();
     ColEntry* e = col_find(c);
     if (e && col_usable(e, c)) {
         e->op = g_op;
         *d = (const int32_t*)e->dev;
+        TRACE("column_device(hit)", t0);
         return 0;
     }
     if (e) col_drop(e);
@@ -343,6 +381,7 @@ static int column_device(Column* c, const int32_t** d, Status* st) {
     g_res.column_uploads++;
     g_res.column_bytes += bytes;
     *d = (const int32_t*)col_put(c, dev)->dev;
+    TRACE("column_device(upload)", t0);
     return 0;
 }
 
@@ -372,6 +411,7 @@ static void shadow_put(const void* host, size_t n, void* dev, uint64_t guard) {
 /* Device view of an int32 Result payload: its shadow while the payload is
  * unchanged (guarded, or uploaded by this same operator), else a fresh upload. */
 static int result_device(const Result* r, const int32_t** d, Status* st) {
+    const double t0 = now_s();
     const int32_t* h = (const int32_t*)r->payload;
     size_t n = r->num_tuples;
     int i = shadow_find(h);
@@ -381,6 +421,7 @@ static int result_device(const Result* r, const int32_t** d, Status* st) {
             e->stamp = ++g_stamp;
             e->op = g_op;
             *d = (const int32_t*)e->dev;
+            TRACE("result_device(hit)", t0);
             return 0;
         }
         shadow_drop(i);
@@ -428,14 +469,24 @@ static Result* new_result(DataType t, size_t n, void* payload) {
  * free() unmaps it) an HBM shadow of it is kept for the operators that follow;
  * otherwise they upload it again. */
 static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
-    int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
+    double t0 = now_s();
+    const size_t bytes = n * sizeof(int32_t);
+    int32_t* host = (int32_t*)payload_alloc(bytes);
+    TRACE("payload_alloc", t0);
+    /* small payloads are cheaper to upload again than to guard */
+    const int keep = bytes >= SHADOW_MIN_BYTES && mq_guard_enabled() && mq_guard_chunk_ok(host);
     int rc;
-    if (n && (rc = d2h(host, d_src, n * sizeof(int32_t)))) {
+    t0 = now_s();
+    if (n && (rc = keep ? d2h_staged(host, d_src, bytes) : d2h(host, d_src, bytes))) {
         free(host);
         fail(st, "result download", rc);
         return NULL;
     }
-    const uint64_t guard = n ? mq_guard_arm(host, n * sizeof(int32_t), MQ_GUARD_CHUNK) : 0;
+    TRACE("result d2h", t0);
+    t0 = now_s();
+    const uint64_t guard = keep ? mq_guard_arm(host, bytes, MQ_GUARD_CHUNK) : 0;
+    TRACE("guard_arm(payload)", t0);
+    t0 = now_s();
     if (guard) {
         void* dev = NULL;
         if ((rc = dev_alloc(&dev, n * sizeof(int32_t))) ||
@@ -446,8 +497,14 @@ static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
             fail(st, "shadow copy", rc);
             return NULL;
         }
+        if (trace_on()) {
+            mq_stream_sync(g_stream);
+            TRACE("shadow alloc+d2d", t0);
+            t0 = now_s();
+        }
         shadow_put(host, n, dev, guard);
     }
+    TRACE("shadow put", t0);
     st->code = OK;
     return new_result(INT, n, host);
 }
@@ -492,6 +549,7 @@ static Result* scan_positions(Column* column, int* low_pointer, int* high_pointe
     size_t n = column->row_count;
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
+    const double t0 = now_s();
     int rc = mq_select_positions(dcol, NULL, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
                                  high_pointer != NULL, high_pointer ? *high_pointer : 0,
                                  (int32_t*)g_scratch, (uint64_t*)g_small, g_ws, g_ws_bytes, g_stream);
@@ -501,6 +559,7 @@ static Result* scan_positions(Column* column, int* low_pointer, int* high_pointe
     }
     uint64_t k;
     if (read_count(&k, ret_status)) return NULL;
+    TRACE("select kernel+count", t0);
     return int_result_from_device(g_scratch, (size_t)k, ret_status);
 }
 
@@ -765,12 +824,14 @@ Result** shared_select(SelectOperator* operators, int query_count, Column* colum
         for (int j = 0; !rc && j < q; j++) rc = dev_alloc(&dev[j], (size_t)k[j] * sizeof(int32_t));
         if (!rc) rc = mq_shared_select_write(g_ws, (int32_t* const*)dev, g_stream);
         for (int j = 0; !rc && j < q; j++) {
-            int32_t* host = (int32_t*)payload_alloc((size_t)k[j] * sizeof(int32_t));
-            if (k[j] && (rc = d2h(host, dev[j], (size_t)k[j] * sizeof(int32_t)))) {
+            const size_t bytes = (size_t)k[j] * sizeof(int32_t);
+            int32_t* host = (int32_t*)payload_alloc(bytes);
+            const int keep = bytes >= SHADOW_MIN_BYTES && mq_guard_enabled() && mq_guard_chunk_ok(host);
+            if (k[j] && (rc = keep ? d2h_staged(host, dev[j], bytes) : d2h(host, dev[j], bytes))) {
                 free(host);
                 break;
             }
-            const uint64_t guard = k[j] ? mq_guard_arm(host, (size_t)k[j] * 4, MQ_GUARD_CHUNK) : 0;
+            const uint64_t guard = keep ? mq_guard_arm(host, bytes, MQ_GUARD_CHUNK) : 0;
             if (guard) {
                 shadow_put(host, (size_t)k[j], dev[j], guard);
                 dev[j] = NULL; /* owned by the shadow now */

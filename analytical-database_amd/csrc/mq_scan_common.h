@@ -32,6 +32,7 @@ static_assert(sizeof(Partial) == sizeof(mq_agg), "Partial must mirror mq_agg");
 struct Pred {
     uint32_t lo;
     uint32_t wm1;
+    int32_t base;  // added to emitted row positions (a row shard's first row; 0 otherwise)
 };
 
 template <bool VEC>

@@ -139,7 +139,7 @@ __device__ __forceinline__ gint* global_ptr(int* p) { return (gint*)p; }
 __device__ __forceinline__ void ss_emit(gint* __restrict__ out, unsigned long long& o, uint64_t row,
                                        unsigned long long m0, unsigned long long m1,
                                        unsigned long long m2, unsigned long long m3, int lane,
-                                       unsigned long long ltmask) {
+                                       unsigned long long ltmask, int32_t base) {
     const unsigned int tot = (unsigned int)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
     if (!tot) return;  // uniform
     const unsigned int pre = (unsigned int)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) +
@@ -147,10 +147,10 @@ __device__ __forceinline__ void ss_emit(gint* __restrict__ out, unsigned long lo
     const unsigned long long bit = 1ull << lane;
     gint* w = out + o + pre;
     unsigned int k = 0;
-    if (m0 & bit) w[k++] = (int)(row + 0);
-    if (m1 & bit) w[k++] = (int)(row + 1);
-    if (m2 & bit) w[k++] = (int)(row + 2);
-    if (m3 & bit) w[k++] = (int)(row + 3);
+    if (m0 & bit) w[k++] = (int)(row + 0) + base;
+    if (m1 & bit) w[k++] = (int)(row + 1) + base;
+    if (m2 & bit) w[k++] = (int)(row + 2) + base;
+    if (m3 & bit) w[k++] = (int)(row + 3) + base;
     o += tot;
 }
 
@@ -158,7 +158,7 @@ template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, uint64_t n,
                                                    uint64_t rpb, const Pred* __restrict__ preds,
                                                    int q, const unsigned long long* __restrict__ offs,
-                                                   uint64_t nwc, int* const* __restrict__ outs) {
+                                                   uint64_t nwc, int* const* __restrict__ outs, int32_t base) {
     __shared__ unsigned long long run[kWaves][kMaxQ];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -186,11 +186,11 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
                 const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
                 if (full) {
                     ss_emit(out, o, row, bal(v[u].x, p.lo, p.wm1), bal(v[u].y, p.lo, p.wm1),
-                            bal(v[u].z, p.lo, p.wm1), bal(v[u].w, p.lo, p.wm1), lane, ltmask);
+                            bal(v[u].z, p.lo, p.wm1), bal(v[u].w, p.lo, p.wm1), lane, ltmask, base);
                 } else {
                     const uint32_t b = match4(v[u], p, row, e);
                     ss_emit(out, o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
-                            __ballot(b & 8u), lane, ltmask);
+                            __ballot(b & 8u), lane, ltmask, base);
                 }
             }
             if (lane == 0) run[wave][j] = o;
@@ -330,7 +330,7 @@ template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, const Pred* __restrict__ preds,
                                                     int q, const unsigned long long* __restrict__ offs,
-                                                    uint64_t nwc, int* const* __restrict__ outs) {
+                                                    uint64_t nwc, int* const* __restrict__ outs, int32_t base) {
     __shared__ uint32_t s_bkt[kBuckets];
     __shared__ int32_t s_b[kEiMax];
     __shared__ uint32_t s_qoff[kEiMax];
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                     unsigned long long o = run[wave][j];
                     const uint32_t b = match4(v[u], p, row, e);
                     ss_emit(global_ptr(outs[j]), o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
-                            __ballot(b & 8u), lane, ltmask);
+                            __ballot(b & 8u), lane, ltmask, base);
                     if (lane == 0) run[wave][j] = o;
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -417,13 +417,13 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                 const unsigned long long peers = match_any8(mq, __ballot(valid));
                 const uint32_t rank = (uint32_t)__popcll(peers & ltmask);
                 const bool last = (peers & ~ltmask & ~(1ull << lane)) == 0;
-                unsigned long long base = 0;
+                unsigned long long at0 = 0;
                 if (valid) {
-                    base = run[wave][mq];
-                    global_ptr(outs[mq])[base + rank] = (int)(tile0 + (me & 0xFFFFu));
+                    at0 = run[wave][mq];
+                    global_ptr(outs[mq])[at0 + rank] = (int)(tile0 + (me & 0xFFFFu)) + base;
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (valid && last) run[wave][mq] = base + rank + 1;
+                if (valid && last) run[wave][mq] = at0 + rank + 1;
                 __builtin_amdgcn_wave_barrier();
             }
         }
@@ -491,6 +491,7 @@ struct SsState {
     const int32_t* col;
     bool ei;    // elementary-interval kernels (qk >= kEiMinQ)
     EiMeta meta;
+    int32_t base;  // first row number of this (row-shard) column
 };
 
 // Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
@@ -567,15 +568,16 @@ EiTables ei_tables(char* region) {
     return T;
 }
 
-int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int32_t* h_highs,
-             int q, uint64_t* d_totals, void* d_ws, size_t ws_bytes, hipStream_t st,
+int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* h_lows,
+             const int32_t* h_highs, int q, uint64_t* d_totals, void* d_ws, size_t ws_bytes, hipStream_t st,
              SsState* state) {
     DevState* s;
     int rc = ensure_ready(&s);
     if (rc) return rc;
     if (q < 1 || q > kMaxQ || !h_lows || !h_highs || !d_totals)
         return set_err(MQ_EINVAL, "shared_select: bad argument (q = %d, 1..%d)", q, kMaxQ);
-    if (n > (uint64_t)INT32_MAX) return set_err(MQ_EINVAL, "shared_select: n over 2^31");
+    if (row_base < 0 || (uint64_t)row_base + n > (uint64_t)INT32_MAX)
+        return set_err(MQ_EINVAL, "shared_select: rows beyond int32 positions");
     if (!d_ws || ws_bytes < mq_shared_select_workspace_bytes(n, q))
         return set_err(MQ_EINVAL, "shared_select: workspace too small");
     // Queries whose range is empty (high <= low) match nothing and are left out of
@@ -632,7 +634,7 @@ int ss_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows, const int3
     hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
                        reinterpret_cast<const int*>(w + L.slot), d_totals, q);
     LAUNCHCHK("k_ss_totals");
-    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta};
+    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta, row_base};
     return MQ_OK;
 }
 
@@ -655,16 +657,16 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     if (S.ei) {
         const EiTables T = ei_tables(w + L.ei);
         if (aligned16(S.col))
-            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs);
+            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base);
         else
-            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs);
+            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base);
         LAUNCHCHK("k_ssi_write");
         return MQ_OK;
     }
     if (aligned16(S.col))
-        hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs);
+        hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base);
     else
-        hipLaunchKernelGGL(k_ss_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs);
+        hipLaunchKernelGGL(k_ss_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base);
     LAUNCHCHK("k_ss_write");
     return MQ_OK;
 }
@@ -689,6 +691,12 @@ size_t mq_shared_select_workspace_bytes(uint64_t n, int q) {
 int mq_shared_select_count(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
                            const int32_t* h_highs, int q, uint64_t* h_counts, void* d_ws,
                            size_t ws_bytes, void* stream) {
+    return mq_shared_select_count_at(d_col, n, 0, h_lows, h_highs, q, h_counts, d_ws, ws_bytes, stream);
+}
+
+int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* h_lows,
+                              const int32_t* h_highs, int q, uint64_t* h_counts, void* d_ws,
+                              size_t ws_bytes, void* stream) {
     if (!h_counts) return set_err(MQ_EINVAL, "mq_shared_select_count: NULL counts");
     hipStream_t st = (hipStream_t)stream;
     // totals land in the preds region's tail? keep them in their own small buffer
@@ -698,7 +706,7 @@ int mq_shared_select_count(const int32_t* d_col, uint64_t n, const int32_t* h_lo
     if (rc) return rc;
     if (!d_tot[dev]) HIPCHK(hipMalloc(&d_tot[dev], kMaxQ * sizeof(uint64_t)));
     SsState S;
-    if ((rc = ss_count(d_col, n, h_lows, h_highs, q, d_tot[dev], d_ws, ws_bytes, st, &S))) return rc;
+    if ((rc = ss_count(d_col, n, row_base, h_lows, h_highs, q, d_tot[dev], d_ws, ws_bytes, st, &S))) return rc;
     HIPCHK(hipMemcpyAsync(h_counts, d_tot[dev], sizeof(uint64_t) * q, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     g_last_state = S;
@@ -726,7 +734,7 @@ int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
                                    d_counts, d_ws, ws_bytes, stream);
     SsState S;
     hipStream_t st = (hipStream_t)stream;
-    if ((rc = ss_count(d_col, n, h_lows, h_highs, q, d_counts, d_ws, ws_bytes, st, &S))) return rc;
+    if ((rc = ss_count(d_col, n, 0, h_lows, h_highs, q, d_counts, d_ws, ws_bytes, st, &S))) return rc;
     return ss_write(S, d_pos_out, d_ws, st);
 }
 

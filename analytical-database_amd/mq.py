@@ -106,6 +106,10 @@ _SIGS = {
     "mq_memcpy_h2d": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2h": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2d": (_int, [_vp, _vp, _sz, _vp]),
+    "mq_memcpy_d2h_staged": (_int, [_vp, _vp, _sz, _vp]),
+    "mq_stream_create": (_int, [C.POINTER(_vp)]),
+    "mq_stream_destroy": (_int, [_vp]),
+    "mq_fetch_at": (_int, [_vp, _i32, _vp, _u64, _vp, _vp]),
     "mq_memset": (_int, [_vp, _int, _sz, _vp]),
     "mq_stream_sync": (_int, [_vp]),
     "mq_default_stream": (_vp, []),
@@ -134,6 +138,8 @@ _SIGS = {
     "mq_hashset_elements": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _vp]),
     "mq_random_read": (_int, [_vp, _int, _u64, _vp, _vp]),
     "mq_select_fetch_agg": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _sz, _vp]),
+    "mq_select_positions_at": (_int, [_vp, _vp, _u64, _i32, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,
+                                      _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,
                                    _vp]),
     "mq_index_select": (_int, [_vp, _vp, _u64, _i32, _i32, _vp, _vp, _vp]),
@@ -148,6 +154,7 @@ _SIGS = {
     "mq_shared_select": (_int, [_vp, _u64, _vp, _vp, _int, _vp, _vp, _vp, _sz, _vp]),
     "mq_shared_select_count": (_int, [_vp, _u64, _vp, _vp, _int, _vp, _vp, _sz, _vp]),
     "mq_shared_select_write": (_int, [_vp, _vp, _vp]),
+    "mq_shared_select_count_at": (_int, [_vp, _u64, _i32, _vp, _vp, _int, _vp, _vp, _sz, _vp]),
     "mq_hash_join": (_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _u64, C.POINTER(_u64),
                             _vp]),
     "mq_join_build": (_int, [_vp, _vp, _u64, C.POINTER(_vp), _vp]),

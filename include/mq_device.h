@@ -51,10 +51,17 @@ int mq_malloc(void** dptr, size_t bytes);
 int mq_free(void* dptr);
 int mq_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+/* D2H through the library's pinned staging buffers (synchronous): dst is never
+ * registered with the driver, so it can be write-protected afterwards without
+ * stalling later GPU work (a direct pageable D2H followed by mprotect does). */
+int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memset(void* dptr, int value, size_t bytes, void* stream);
 int mq_stream_sync(void* stream);
 void* mq_default_stream(void);
+/* A non-blocking stream of its own on the calling thread's current device. */
+int mq_stream_create(void** stream);
+int mq_stream_destroy(void* stream);
 /* Release the device scratch libmq keeps cached between calls (join tables and
  * partition buffers, probe arrays); the next call allocates afresh. */
 void mq_trim(void);
@@ -141,6 +148,14 @@ int mq_select_positions(const int32_t* d_col, const int32_t* d_payload, uint64_t
                         int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
                         uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream);
 
+/* The same over a row shard: the rows are d_col[0..n) but number from row_base, so
+ * without a payload the positions written are row_base + i (a column split into row
+ * ranges across devices concatenates its shards' outputs in shard order).
+ * row_base + n must be < 2^31. */
+int mq_select_positions_at(const int32_t* d_col, const int32_t* d_payload, uint64_t n, int32_t row_base,
+                           int has_low, int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
+                           uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream);
+
 /* ---- S6 select_column_sorted_index (query.c:143-198) ----
  * d_values: n int32 sorted ascending; d_positions: n size_t row ids. Restates the
  * reference's binary_search + run adjustment exactly (including its low == high
@@ -166,6 +181,10 @@ int mq_histogram(const int32_t* d_col, uint64_t n, int32_t col_min, int32_t bin_
 
 /* ---- S5 fetch_column: d_out[i] = d_col[d_pos[i]] ---- */
 int mq_fetch(const int32_t* d_col, const int32_t* d_pos, uint64_t k, int32_t* d_out, void* stream);
+/* the same from a row shard holding rows [row_base, row_base + rows) of the column:
+ * d_out[i] = d_col[d_pos[i] - row_base] (every position must lie in the shard) */
+int mq_fetch_at(const int32_t* d_col, int32_t row_base, const int32_t* d_pos, uint64_t k, int32_t* d_out,
+                void* stream);
 
 /* ---- S7/S8/S9 over a values vector (sum/avg/min/max of a Result) ---- */
 int mq_reduce(const int32_t* d_vals, uint64_t n, mq_agg* d_out, void* d_ws, size_t ws_bytes,
@@ -227,6 +246,11 @@ int mq_shared_select_count(const int32_t* d_col, uint64_t n, const int32_t* h_lo
                            const int32_t* h_highs, int q, uint64_t* h_counts, void* d_ws,
                            size_t ws_bytes, void* stream);
 int mq_shared_select_write(void* d_ws, int32_t* const* d_pos_out, void* stream);
+/* count over a row shard whose rows number from row_base (the write then emits
+ * row_base + i), as mq_select_positions_at */
+int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* h_lows,
+                              const int32_t* h_highs, int q, uint64_t* h_counts, void* d_ws,
+                              size_t ws_bytes, void* stream);
 
 /* ---- J1 hash_join as three steps on a handle (lets the caller size the output) ----
  * build: table over (c1, p1); p1 must stay valid until mq_join_free.

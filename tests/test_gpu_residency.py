@@ -193,6 +193,12 @@ def test_operands_survive_a_tiny_shadow_budget(lib, refcpu, monkeypatch):
     s = st()
     out = lib.sub(rb, ra, C.byref(s))
     assert np.array_equal(take(out), refcpu.sub(pb, pa))
+    # the budget is exceeded only by what the last operator held (its two operands
+    # and its output); the next operator evicts down to the budget
+    assert mq.residency(lib)["shadow_bytes"] <= 3 * 4 * n + (1 << 20)
+    s = st()
+    lib.min(rb, C.byref(s))
+    assert s.code == mq.OK
     assert mq.residency(lib)["shadow_bytes"] <= 2 * 4 * n + (1 << 20)
     take(ra)
     take(rb)
