@@ -36,6 +36,7 @@
 
 #include "mq_device.h"
 #include "mq_guard.h"
+#include "mq_shim.h"
 
 /* ---- ABI pins: x86-64 layouts of the reference structs ---- */
 _Static_assert(sizeof(Result) == 24, "Result size");
@@ -115,10 +116,6 @@ typedef struct {
     uint64_t guard_v, guard_p;
     unsigned long long op;
 } IndexEntry;
-
-/* Payloads from this size on keep an HBM shadow (ready() lowers glibc's mmap
- * threshold to it, so they are mmapped chunks, which a guard can cover). */
-#define SHADOW_MIN_BYTES ((size_t)1 << 20)
 
 #define MAX_COLS 1024
 #define MAX_SHADOWS 4096
@@ -208,6 +205,7 @@ static int op_begin(Status* st) {
     if (ready(st)) return -1;
     g_op++;
     sweep();
+    shard_op_begin();
     TRACE("op_begin", t0);
     return 0;
 }
@@ -546,6 +544,7 @@ __attribute__((weak)) bool should_use_index(Column* column, int low, int high) {
 
 /* query.c:92-137 (the body; shared_select calls it inside its own operator) */
 static Result* scan_positions(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
+    if (shard_wants(column)) return shard_select(column, low_pointer, high_pointer, ret_status);
     size_t n = column->row_count;
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
@@ -675,6 +674,11 @@ Result* select_result(Result* column, Result* prev_position, int* low_pointer, i
 /* query.c:223-243 */
 Result* fetch_column(Column* column, Result* position_result, Status* ret_status) {
     if (op_begin(ret_status)) return NULL;
+    if (shard_wants(column)) {
+        Result* r = NULL;
+        const int h = shard_fetch(column, position_result, &r, ret_status);
+        if (h) return h > 0 ? r : NULL;
+    }
     size_t k = position_result->num_tuples;
     const int32_t *dcol, *dpos;
     if (column_device(column, &dcol, ret_status) || result_device(position_result, &dpos, ret_status) ||
@@ -690,6 +694,8 @@ Result* fetch_column(Column* column, Result* position_result, Status* ret_status
 
 static int reduce_result(Result* r, mq_agg* a, Status* st) {
     if (op_begin(st)) return -1;
+    const int h = shard_reduce_result(r, a, st);
+    if (h) return h > 0 ? 0 : -1;
     const int32_t* d;
     if (result_device(r, &d, st) || ensure_ws(0, st)) return -1;
     int rc = mq_reduce(d, r->num_tuples, (mq_agg*)g_small, g_ws, g_ws_bytes, g_stream);
@@ -715,6 +721,13 @@ Result* sum(GeneralizedColumn* column, Status* ret_status) {
     } else {
         if (op_begin(ret_status)) return NULL;
         Column* c = column->column_pointer.column;
+        if (shard_wants(c)) {
+            if (shard_reduce_column(c, &a, ret_status)) return NULL;
+            long* out = (long*)malloc(sizeof(long));
+            *out = (long)a.sum;
+            ret_status->code = OK;
+            return new_result(LONG, 1, out);
+        }
         const int32_t* d;
         if (column_device(c, &d, ret_status) || ensure_ws(0, ret_status)) return NULL;
         int rc = mq_reduce(d, c->row_count, (mq_agg*)g_small, g_ws, g_ws_bytes, g_stream);
@@ -790,8 +803,9 @@ Result* max(Result* column, Status* ret_status) {
 Result** shared_select(SelectOperator* operators, int query_count, Column* column, Status* ret_status) {
     if (op_begin(ret_status)) return NULL;
     size_t n = column->row_count;
-    const int32_t* dcol;
-    if (column_device(column, &dcol, ret_status)) return NULL;
+    if (query_count > 3 && shard_wants(column)) return shard_shared_select(operators, query_count, column, ret_status);
+    const int32_t* dcol = NULL;
+    if (query_count > 3 && column_device(column, &dcol, ret_status)) return NULL;
     Result** out = (Result**)calloc((size_t)(query_count > 0 ? query_count : 1), sizeof(Result*));
     if (query_count <= 3) {  /* a few queries: one ordered-compaction pass each is cheaper */
         for (int j = 0; j < query_count; j++) {
@@ -1387,6 +1401,7 @@ int mq_column_upload(Column* column) {
 void mq_column_invalidate(Column* column) {
     ColEntry* e = col_find(column);
     if (e) col_drop(e);
+    shard_forget_column(column);
 }
 
 const void* mq_result_device_ptr(const Result* result) {
@@ -1407,6 +1422,7 @@ void mq_release_all(void) {
     while (g_ncols) col_drop(&g_cols[g_ncols - 1]);
     while (g_nshadows) shadow_drop(g_nshadows - 1);
     while (g_nidx) idx_drop(&g_idx[g_nidx - 1]);
+    shard_release_all();
     mq_trim();
 }
 
@@ -1421,6 +1437,7 @@ void mq_residency_stats(mq_residency* out) {
     out->columns_resident = (uint64_t)g_ncols;
     out->shadows_resident = (uint64_t)g_nshadows;
     out->shadow_bytes = (uint64_t)g_shadow_bytes;
+    shard_stats(out);
 }
 
 double mq_transfer_seconds(int reset) {
@@ -1428,3 +1445,17 @@ double mq_transfer_seconds(int reset) {
     if (reset) g_xfer_s = 0;
     return t;
 }
+
+/* ------------------------------------------------------------------ */
+/* internal interface for the row-shard executor (mq_shim.h)          */
+/* ------------------------------------------------------------------ */
+
+double shim_now(void) { return now_s(); }
+int shim_trace_on(void) { return trace_on(); }
+int shim_fail(Status* st, const char* what, int rc) { return fail(st, what, rc); }
+void* shim_payload_alloc(size_t bytes) { return payload_alloc(bytes); }
+Result* shim_new_result(DataType t, size_t n, void* payload) { return new_result(t, n, payload); }
+unsigned long long shim_op(void) { return g_op; }
+size_t shim_shadow_budget(void) { return shadow_budget(); }
+mq_residency* shim_stats(void) { return &g_res; }
+void shim_xfer_add(double seconds) { g_xfer_s += seconds; }

@@ -1,0 +1,740 @@
+/*
+ * mq_shard.c — row shards: a long column split into G contiguous row ranges, shard g
+ * resident on its own device and served by its own host thread and stream.
+ *
+ * scans, selects and aggregates partition by row range; per-shard
+ * position lists use local rows plus the shard base, so the global ascending list is
+ * the concatenation in shard order, which is also the order the reference's
+ * shared_select threads concatenate in (src/query.c:563-574); {count, sum, min, max}
+ * combine with one fold (avg = one double division after it, bit-identical to one
+ * device). The fan-out sits inside the operators the server calls for one query or
+ * one batch (server.c:360-399 batches into shared_select), so the reference server
+ * links it unchanged.
+ *
+ * Data movement: each shard uploads its rows from the host column over its own PCIe
+ * link, and downloads its part of every Result straight into the host payload at the
+ * part's offset, so results are assembled in host memory with no device-to-device
+ * exchange. The pieces stay resident as a sharded shadow of the payload: a following
+ * fetch_column / sum / avg / min / max on that Result runs on the shards again.
+ *
+ * The aggregate combine is a host fold of G 32-byte partials: the Result the API returns
+ * is host memory, so a collective would only add a hop (RCCL's all-reduce serves the
+ * one-process-per-GPU bench, analytical-database_amd/dist.py).
+ *
+ * Threads: G workers, each bound to its shard's device for its lifetime; an operator
+ * hands every worker the same task and waits for all (no work is queued across calls).
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mq_guard.h"
+#include "mq_shim.h"
+
+#define MAXS 64
+#define MAX_SCOLS 256
+#define MAX_SSHADOWS 2048
+#define MAXQ 256
+
+typedef struct Shard {
+    int idx, dev;
+    void* stream;
+    void* ws;
+    size_t ws_bytes;
+    void* scratch;
+    size_t scratch_bytes;
+    void* small;  /* counts / aggregates */
+    int rc, quit;
+    double xfer;  /* PCIe seconds of the current task */
+    unsigned long gen0;  /* task generation when the worker was started */
+    pthread_t th;
+    /* per-task outputs */
+    uint64_t k;
+    mq_agg agg;
+    uint64_t kq[MAXQ];
+    void* piece[MAXQ];
+} Shard;
+
+static Shard g_sh[MAXS];
+static int g_G = -1;        /* shard count; 1 = off */
+static size_t g_min_rows;
+static int g_started;
+
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t g_go = PTHREAD_COND_INITIALIZER, g_done = PTHREAD_COND_INITIALIZER;
+static unsigned long g_gen;
+static int g_pending;
+static void (*g_fn)(Shard*, void*);
+static void* g_arg;
+
+/* ------------------------------------------------------------------ */
+/* configuration and workers                                          */
+/* ------------------------------------------------------------------ */
+
+static void configure(void) {
+    if (g_G >= 0) return;
+    memset(g_sh, 0, sizeof g_sh);
+    int devs[MAXS], nd = 0;
+    const char* e = getenv("MQ_DEVICES");
+    while (e && *e && nd < MAXS) {
+        char* end;
+        long v = strtol(e, &end, 10);
+        if (end == e) break;
+        devs[nd++] = (int)v;
+        e = *end == ',' ? end + 1 : end;
+    }
+    const char* s = getenv("MQ_SHARDS");
+    int G = s ? atoi(s) : (nd > 0 ? nd : 1);
+    if (G < 1) G = 1;
+    if (G > MAXS) G = MAXS;
+    const char* pe = getenv("MQ_DEVICE");
+    const int primary = pe ? atoi(pe) : 0;
+    int count = mq_device_count();
+    if (count < 1) count = 1;
+    for (int g = 0; g < G; g++) {
+        g_sh[g].idx = g;
+        g_sh[g].dev = nd > 0 ? devs[g % nd] : (primary + g) % count;
+    }
+    const char* m = getenv("MQ_SHARD_MIN_ROWS");
+    g_min_rows = m ? (size_t)strtoull(m, NULL, 10) : ((size_t)1 << 24);
+    g_G = G;
+}
+
+static void* worker(void* p) {
+    Shard* s = (Shard*)p;
+    unsigned long seen = s->gen0; /* tasks before this worker existed are not its own */
+    for (;;) {
+        pthread_mutex_lock(&g_mu);
+        while (g_gen == seen) pthread_cond_wait(&g_go, &g_mu);
+        seen = g_gen;
+        void (*fn)(Shard*, void*) = g_fn;
+        void* arg = g_arg;
+        pthread_mutex_unlock(&g_mu);
+        s->rc = 0;
+        fn(s, arg);
+        const int quit = s->quit;
+        pthread_mutex_lock(&g_mu);
+        if (--g_pending == 0) pthread_cond_signal(&g_done);
+        pthread_mutex_unlock(&g_mu);
+        if (quit) return NULL;
+    }
+}
+
+/* Run fn on every shard's worker and wait for all; the first nonzero rc, or 0. */
+static int run_all(void (*fn)(Shard*, void*), void* arg) {
+    pthread_mutex_lock(&g_mu);
+    g_fn = fn;
+    g_arg = arg;
+    g_pending = g_G;
+    g_gen++;
+    pthread_cond_broadcast(&g_go);
+    while (g_pending) pthread_cond_wait(&g_done, &g_mu);
+    pthread_mutex_unlock(&g_mu);
+    double x = 0; /* the shards copy in parallel: the task's transfer time is the longest */
+    for (int g = 0; g < g_G; g++) {
+        if (g_sh[g].xfer > x) x = g_sh[g].xfer;
+        g_sh[g].xfer = 0;
+    }
+    shim_xfer_add(x);
+    for (int g = 0; g < g_G; g++)
+        if (g_sh[g].rc) return g_sh[g].rc;
+    return 0;
+}
+
+static void t_init(Shard* s, void* arg) {
+    (void)arg;
+    if ((s->rc = mq_init(s->dev))) return;
+    if ((s->rc = mq_stream_create(&s->stream))) return;
+    s->rc = mq_malloc(&s->small, 4096);
+}
+
+static int start(Status* st) {
+    if (g_started == 1) return 0;
+    if (g_started == -1) return shim_fail(st, "row shards (earlier)", MQ_ENODEV);
+    pthread_mutex_lock(&g_mu);
+    const unsigned long gen0 = g_gen;
+    pthread_mutex_unlock(&g_mu);
+    for (int g = 0; g < g_G; g++) {
+        g_sh[g].gen0 = gen0;
+        if (pthread_create(&g_sh[g].th, NULL, worker, &g_sh[g]) != 0) {
+            g_started = -1;
+            return shim_fail(st, "shard worker start", MQ_EINVAL);
+        }
+        pthread_detach(g_sh[g].th);
+    }
+    int rc = run_all(t_init, NULL);
+    if (rc) {
+        g_started = -1;
+        return shim_fail(st, "shard device init", rc);
+    }
+    g_started = 1;
+    return 0;
+}
+
+int shard_count(void) {
+    configure();
+    return g_G;
+}
+
+int shard_wants(const Column* c) {
+    configure();
+    return g_G > 1 && c && c->row_count >= g_min_rows && c->row_count >= (size_t)g_G &&
+           c->row_count <= (size_t)INT32_MAX;
+}
+
+/* Per-shard scratch on the worker's device (grow-only, pool memory). */
+static int grow(void** buf, size_t* have, size_t need) {
+    if (*have >= need && *buf) return 0;
+    if (*buf) mq_pool_free(*buf);
+    *buf = NULL;
+    *have = 0;
+    size_t want = need + need / 8 + 4096;
+    int rc = mq_pool_malloc(buf, want);
+    if (rc) return rc;
+    *have = want;
+    return 0;
+}
+
+static int ensure(Shard* s, size_t rows) {
+    int rc = grow(&s->ws, &s->ws_bytes, mq_scan_workspace_bytes(rows));
+    if (!rc) rc = grow(&s->scratch, &s->scratch_bytes, (rows ? rows : 1) * sizeof(int32_t));
+    return rc;
+}
+
+/* D2H of one piece of a Result into its slot of the host payload; staged (pinned
+ * buffers) when the payload will be write-guarded, see mq_memcpy_d2h_staged. */
+static int download(Shard* s, void* host, const void* dev, size_t bytes, int staged) {
+    if (!bytes) return 0;
+    double t0 = shim_now();
+    int rc = staged ? mq_memcpy_d2h_staged(host, dev, bytes, s->stream) : mq_memcpy_d2h(host, dev, bytes, s->stream);
+    s->xfer += shim_now() - t0;
+    return rc;
+}
+
+/* ------------------------------------------------------------------ */
+/* sharded columns                                                    */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    const Column* col;
+    const int* host;
+    size_t rows;
+    size_t base[MAXS + 1];
+    void* dev[MAXS];
+    uint64_t guard;
+    unsigned long long op;
+} SCol;
+
+static SCol g_scols[MAX_SCOLS];
+static int g_nscols;
+
+typedef struct {
+    const void* host;  /* payload */
+    size_t n;
+    size_t rows;       /* > 0: the pieces are positions of a rows-row column split as split_of(rows) */
+    size_t off[MAXS + 1];
+    void* dev[MAXS];
+    uint64_t guard;
+    size_t bytes;
+    unsigned long long stamp, op;
+} SShadow;
+
+static SShadow g_ssh[MAX_SSHADOWS];
+static int g_nssh;
+static size_t g_ssh_bytes;
+static unsigned long long g_sstamp;
+static uint64_t g_ops, g_uploads;
+
+/* Row split of a column: whole 1024-row tiles per shard (16-byte aligned slices). */
+static void split_of(size_t rows, size_t* base) {
+    base[0] = 0;
+    for (int g = 1; g < g_G; g++) {
+        size_t b = (size_t)(((unsigned __int128)rows * (unsigned)g) / (unsigned)g_G) & ~(size_t)1023;
+        base[g] = b < base[g - 1] ? base[g - 1] : b;
+    }
+    base[g_G] = rows;
+}
+
+/* Device memory is freed only between operators, when no worker has work queued. */
+static void free_pieces(void* const* dev) {
+    for (int g = 0; g < g_G; g++) mq_pool_free(dev[g]);
+}
+
+static void scol_drop(int i) {
+    mq_guard_release(g_scols[i].guard);
+    free_pieces(g_scols[i].dev);
+    g_scols[i] = g_scols[--g_nscols];
+}
+
+static void ssh_drop(int i) {
+    mq_guard_release(g_ssh[i].guard);
+    free_pieces(g_ssh[i].dev);
+    g_ssh_bytes -= g_ssh[i].bytes;
+    g_ssh[i] = g_ssh[--g_nssh];
+}
+
+typedef struct {
+    SCol* e;
+    const int* host;
+} UpArg;
+
+static void t_upload(Shard* s, void* a) {
+    UpArg* u = (UpArg*)a;
+    const size_t b0 = u->e->base[s->idx], n = u->e->base[s->idx + 1] - b0;
+    if ((s->rc = mq_pool_malloc(&u->e->dev[s->idx], (n ? n : 1) * 4))) return;
+    double t0 = shim_now();
+    if (n) s->rc = mq_memcpy_h2d(u->e->dev[s->idx], u->host + b0, n * 4, s->stream);
+    s->xfer += shim_now() - t0;
+}
+
+static SCol* scol_get(Column* c, Status* st) {
+    if (start(st)) return NULL;
+    for (int i = 0; i < g_nscols; i++) {
+        SCol* e = &g_scols[i];
+        if (e->col != c) continue;
+        if (e->host == c->data && e->rows == c->row_count &&
+            (e->op == shim_op() || (e->guard && mq_guard_clean(e->guard, e->host, e->rows * 4)))) {
+            e->op = shim_op();
+            return e;
+        }
+        scol_drop(i);
+        break;
+    }
+    if (g_nscols == MAX_SCOLS) {
+        int v = 0;
+        for (int i = 0; i < g_nscols; i++)
+            if (g_scols[i].op != shim_op()) v = i;
+        scol_drop(v);
+    }
+    SCol* e = &g_scols[g_nscols];
+    memset(e, 0, sizeof *e);
+    e->col = c;
+    e->host = c->data;
+    e->rows = c->row_count;
+    e->op = shim_op();
+    split_of(e->rows, e->base);
+    UpArg u = {e, c->data};
+    int rc = run_all(t_upload, &u);
+    if (rc) {
+        free_pieces(e->dev);
+        shim_fail(st, "shard column upload", rc);
+        return NULL;
+    }
+    e->guard = mq_guard_arm(c->data, e->rows * 4, MQ_GUARD_FILE);
+    g_nscols++;
+    g_uploads++;
+    shim_stats()->column_uploads++;
+    shim_stats()->column_bytes += e->rows * 4;
+    return e;
+}
+
+static int ssh_find(const void* host, size_t n) {
+    for (int i = 0; i < g_nssh; i++)
+        if (g_ssh[i].host == host) {
+            SShadow* e = &g_ssh[i];
+            if (e->n == n && (e->op == shim_op() || n == 0 || (e->guard && mq_guard_clean(e->guard, host, n * 4)))) {
+                e->op = shim_op();
+                e->stamp = ++g_sstamp;
+                return i;
+            }
+            ssh_drop(i);
+            return -1;
+        }
+    return -1;
+}
+
+/* LRU down to the shadow budget; entries the current operator holds stay. */
+static void ssh_make_room(size_t bytes) {
+    while (g_nssh >= MAX_SSHADOWS || g_ssh_bytes + bytes > shim_shadow_budget()) {
+        int v = -1;
+        for (int i = 0; i < g_nssh; i++)
+            if (g_ssh[i].op != shim_op() && (v < 0 || g_ssh[i].stamp < g_ssh[v].stamp)) v = i;
+        if (v < 0) break;
+        ssh_drop(v);
+    }
+}
+
+/* Register the pieces (owned from now on) as the payload's sharded shadow. */
+static void ssh_put(const void* host, size_t n, size_t rows, const size_t* off, void* const* dev, uint64_t guard) {
+    for (int i = 0; i < g_nssh; i++)
+        if (g_ssh[i].host == host) {
+            ssh_drop(i);
+            break;
+        }
+    ssh_make_room(n * 4);
+    if (g_nssh == MAX_SSHADOWS) ssh_drop(0);
+    SShadow* e = &g_ssh[g_nssh++];
+    e->host = host;
+    e->n = n;
+    e->rows = rows;
+    memcpy(e->off, off, sizeof(size_t) * (size_t)(g_G + 1));
+    memcpy(e->dev, dev, sizeof(void*) * (size_t)g_G);
+    e->guard = guard;
+    e->bytes = n * 4;
+    e->stamp = ++g_sstamp;
+    e->op = shim_op();
+    g_ssh_bytes += e->bytes;
+}
+
+/* Assemble a Result from per-shard pieces already downloaded: guard the payload and
+ * keep the pieces as its shadow, or free them. */
+static Result* finish(void* payload, size_t n, size_t rows, const size_t* off, void** pieces, int keep) {
+    const uint64_t guard = keep && n ? mq_guard_arm(payload, n * 4, MQ_GUARD_CHUNK) : 0;
+    if (guard) {
+        ssh_put(payload, n, rows, off, pieces, guard);
+    } else {
+        free_pieces(pieces);
+    }
+    g_ops++;
+    return shim_new_result(INT, n, payload);
+}
+
+static int keep_payload(const void* p, size_t bytes) {
+    return bytes >= SHADOW_MIN_BYTES && mq_guard_enabled() && mq_guard_chunk_ok(p);
+}
+
+/* ------------------------------------------------------------------ */
+/* operators                                                          */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+    SCol* e;
+    int has_low, has_high;
+    int32_t low, high;
+    /* download step */
+    int32_t* payload;
+    size_t off[MAXS + 1];
+    void* pieces[MAXS];
+    int staged, keep;
+} SelArg;
+
+static void t_select(Shard* s, void* a) {
+    SelArg* x = (SelArg*)a;
+    const size_t b0 = x->e->base[s->idx], n = x->e->base[s->idx + 1] - b0;
+    if ((s->rc = ensure(s, n))) return;
+    s->rc = mq_select_positions_at((const int32_t*)x->e->dev[s->idx], NULL, n, (int32_t)b0, x->has_low, x->low,
+                                   x->has_high, x->high, (int32_t*)s->scratch, (uint64_t*)s->small, s->ws,
+                                   s->ws_bytes, s->stream);
+    if (!s->rc) s->rc = mq_memcpy_d2h(&s->k, s->small, sizeof(uint64_t), s->stream);
+}
+
+/* download shard g's k positions from its scratch; keep a copy as the shadow piece */
+static void t_select_out(Shard* s, void* a) {
+    SelArg* x = (SelArg*)a;
+    const size_t k = x->off[s->idx + 1] - x->off[s->idx];
+    x->pieces[s->idx] = NULL;
+    if ((s->rc = download(s, x->payload + x->off[s->idx], s->scratch, k * 4, x->staged))) return;
+    if (!x->keep) return;
+    if ((s->rc = mq_pool_malloc(&x->pieces[s->idx], (k ? k : 1) * 4))) return;
+    if (!(s->rc = mq_memcpy_d2d(x->pieces[s->idx], s->scratch, k * 4, s->stream))) s->rc = mq_stream_sync(s->stream);
+}
+
+Result* shard_select(Column* c, int* low, int* high, Status* st) {
+    SCol* e = scol_get(c, st);
+    if (!e) return NULL;
+    const double t0 = shim_now();
+    SelArg x;
+    memset(&x, 0, sizeof x);
+    x.e = e;
+    x.has_low = low != NULL;
+    x.low = low ? *low : 0;
+    x.has_high = high != NULL;
+    x.high = high ? *high : 0;
+    int rc = run_all(t_select, &x);
+    if (rc) {
+        shim_fail(st, "shard select", rc);
+        return NULL;
+    }
+    x.off[0] = 0;
+    for (int g = 0; g < g_G; g++) x.off[g + 1] = x.off[g] + g_sh[g].k;
+    const size_t K = x.off[g_G];
+    x.payload = (int32_t*)shim_payload_alloc(K * 4);
+    x.keep = x.staged = keep_payload(x.payload, K * 4);
+    if ((rc = run_all(t_select_out, &x))) {
+        free_pieces(x.pieces);
+        free(x.payload);
+        shim_fail(st, "shard select download", rc);
+        return NULL;
+    }
+    Result* r = finish(x.payload, K, e->rows, x.off, x.pieces, x.keep);
+    if (shim_trace_on()) fprintf(stderr, "mq-trace shard_select(G=%d)      %9.3f ms\n", g_G, 1e3 * (shim_now() - t0));
+    st->code = OK;
+    return r;
+}
+
+typedef struct {
+    SCol* e;
+    SShadow* pos;
+    int32_t* payload;
+    void* pieces[MAXS];
+    int staged, keep;
+} FetchArg;
+
+static void t_fetch(Shard* s, void* a) {
+    FetchArg* x = (FetchArg*)a;
+    const size_t k = x->pos->off[s->idx + 1] - x->pos->off[s->idx];
+    x->pieces[s->idx] = NULL;
+    if ((s->rc = mq_pool_malloc(&x->pieces[s->idx], (k ? k : 1) * 4))) return;
+    if ((s->rc = mq_fetch_at((const int32_t*)x->e->dev[s->idx], (int32_t)x->e->base[s->idx],
+                             (const int32_t*)x->pos->dev[s->idx], k, (int32_t*)x->pieces[s->idx], s->stream)))
+        return;
+    s->rc = download(s, x->payload + x->pos->off[s->idx], x->pieces[s->idx], k * 4, x->staged);
+    if (!s->rc) s->rc = mq_stream_sync(s->stream);
+}
+
+int shard_fetch(Column* c, Result* pos, Result** out, Status* st) {
+    if (g_started != 1) return 0;
+    const int i = ssh_find(pos->payload, pos->num_tuples);
+    if (i < 0 || g_ssh[i].rows != c->row_count) return 0;
+    SCol* e = scol_get(c, st);
+    if (!e) return -1;
+    const int j = ssh_find(pos->payload, pos->num_tuples); /* scol_get may have evicted */
+    if (j < 0) return 0;
+    const double t0 = shim_now();
+    FetchArg x;
+    memset(&x, 0, sizeof x);
+    x.e = e;
+    x.pos = &g_ssh[j];
+    const size_t K = x.pos->n;
+    x.payload = (int32_t*)shim_payload_alloc(K * 4);
+    x.keep = x.staged = keep_payload(x.payload, K * 4);
+    int rc = run_all(t_fetch, &x);
+    if (rc) {
+        free_pieces(x.pieces);
+        free(x.payload);
+        shim_fail(st, "shard fetch", rc);
+        return -1;
+    }
+    size_t off[MAXS + 1];
+    memcpy(off, x.pos->off, sizeof off);
+    *out = finish(x.payload, K, 0, off, x.pieces, x.keep);
+    if (shim_trace_on()) fprintf(stderr, "mq-trace shard_fetch(G=%d)       %9.3f ms\n", g_G, 1e3 * (shim_now() - t0));
+    st->code = OK;
+    return 1;
+}
+
+typedef struct {
+    void* const* dev;    /* per shard */
+    const size_t* len;   /* per shard rows: len[g+1] - len[g] */
+} RedArg;
+
+static void t_reduce(Shard* s, void* a) {
+    RedArg* x = (RedArg*)a;
+    const size_t n = x->len[s->idx + 1] - x->len[s->idx];
+    if ((s->rc = ensure(s, 0))) return;
+    if ((s->rc = mq_reduce((const int32_t*)x->dev[s->idx], n, (mq_agg*)s->small, s->ws, s->ws_bytes, s->stream)))
+        return;
+    s->rc = mq_memcpy_d2h(&s->agg, s->small, sizeof(mq_agg), s->stream);
+}
+
+/* {count, sum, min, max} of the shards, folded: sums add, extremes take min / max */
+static void fold(mq_agg* a) {
+    a->count = 0;
+    a->sum = 0;
+    a->min = INT32_MAX;
+    a->max = INT32_MIN;
+    a->_pad = 0;
+    for (int g = 0; g < g_G; g++) {
+        a->count += g_sh[g].agg.count;
+        a->sum += g_sh[g].agg.sum;
+        if (g_sh[g].agg.count) {
+            if (g_sh[g].agg.min < a->min) a->min = g_sh[g].agg.min;
+            if (g_sh[g].agg.max > a->max) a->max = g_sh[g].agg.max;
+        }
+    }
+}
+
+int shard_reduce_column(Column* c, mq_agg* a, Status* st) {
+    SCol* e = scol_get(c, st);
+    if (!e) return -1;
+    RedArg x = {e->dev, e->base};
+    int rc = run_all(t_reduce, &x);
+    if (rc) return shim_fail(st, "shard sum", rc);
+    fold(a);
+    g_ops++;
+    return 0;
+}
+
+int shard_reduce_result(const Result* r, mq_agg* a, Status* st) {
+    if (g_started != 1) return 0;
+    const int i = ssh_find(r->payload, r->num_tuples);
+    if (i < 0) return 0;
+    RedArg x = {g_ssh[i].dev, g_ssh[i].off};
+    int rc = run_all(t_reduce, &x);
+    if (rc) {
+        shim_fail(st, "shard reduce", rc);
+        return -1;
+    }
+    fold(a);
+    g_ops++;
+    return 1;
+}
+
+/* ---- shared_select ---- */
+
+typedef struct {
+    SCol* e;
+    int q;
+    int32_t lows[MAXQ], highs[MAXQ];
+    int32_t* payload[MAXQ];
+    size_t off[MAXQ][MAXS + 1];
+    int keep[MAXQ];
+} SsArg;
+
+static void t_ss_count(Shard* s, void* a) {
+    SsArg* x = (SsArg*)a;
+    const size_t b0 = x->e->base[s->idx], n = x->e->base[s->idx + 1] - b0;
+    if ((s->rc = grow(&s->ws, &s->ws_bytes, mq_shared_select_workspace_bytes(n, x->q)))) return;
+    s->rc = mq_shared_select_count_at((const int32_t*)x->e->dev[s->idx], n, (int32_t)b0, x->lows, x->highs, x->q,
+                                      s->kq, s->ws, s->ws_bytes, s->stream);
+}
+
+static void t_ss_write(Shard* s, void* a) {
+    SsArg* x = (SsArg*)a;
+    for (int j = 0; j < x->q; j++) s->piece[j] = NULL;
+    for (int j = 0; j < x->q; j++)
+        if ((s->rc = mq_pool_malloc(&s->piece[j], (s->kq[j] ? s->kq[j] : 1) * 4))) return;
+    if ((s->rc = mq_shared_select_write(s->ws, (int32_t* const*)s->piece, s->stream))) return;
+    for (int j = 0; j < x->q; j++)
+        if ((s->rc = download(s, x->payload[j] + x->off[j][s->idx], s->piece[j], s->kq[j] * 4, x->keep[j]))) return;
+    s->rc = mq_stream_sync(s->stream);
+}
+
+Result** shard_shared_select(SelectOperator* ops, int q, Column* c, Status* st) {
+    SCol* e = scol_get(c, st);
+    if (!e) return NULL;
+    Result** out = (Result**)calloc((size_t)(q > 0 ? q : 1), sizeof(Result*));
+    SsArg* x = (SsArg*)calloc(1, sizeof(SsArg));
+    if (!out || !x) {
+        free(out);
+        free(x);
+        shim_fail(st, "shard shared_select", MQ_ENOMEM);
+        return NULL;
+    }
+    x->e = e;
+    int done = 0, rc = 0;
+    for (int q0 = 0; q0 < q && !rc; q0 += MAXQ) {
+        const int m = q - q0 < MAXQ ? q - q0 : MAXQ;
+        x->q = m;
+        for (int j = 0; j < m; j++) { /* the fields as given (query.c:472-479) */
+            x->lows[j] = ops[q0 + j].low;
+            x->highs[j] = ops[q0 + j].high;
+        }
+        if ((rc = run_all(t_ss_count, x))) break;
+        for (int j = 0; j < m; j++) {
+            x->off[j][0] = 0;
+            for (int g = 0; g < g_G; g++) x->off[j][g + 1] = x->off[j][g] + g_sh[g].kq[j];
+            const size_t K = x->off[j][g_G];
+            x->payload[j] = (int32_t*)shim_payload_alloc(K * 4);
+            x->keep[j] = keep_payload(x->payload[j], K * 4);
+        }
+        rc = run_all(t_ss_write, x);
+        for (int j = 0; j < m; j++) {
+            void* pieces[MAXS];
+            for (int g = 0; g < g_G; g++) pieces[g] = g_sh[g].piece[j];
+            if (rc) {
+                free_pieces(pieces);
+                free(x->payload[j]);
+                continue;
+            }
+            out[q0 + j] = finish(x->payload[j], x->off[j][g_G], e->rows, x->off[j], pieces, x->keep[j]);
+            done = q0 + j + 1;
+        }
+    }
+    free(x);
+    if (rc) {
+        for (int j = 0; j < done; j++) {
+            free(out[j]->payload);
+            free(out[j]);
+        }
+        free(out);
+        shim_fail(st, "shard shared_select", rc);
+        return NULL;
+    }
+    st->code = OK;
+    return out;
+}
+
+/* ------------------------------------------------------------------ */
+/* bookkeeping                                                        */
+/* ------------------------------------------------------------------ */
+
+void shard_op_begin(void) {
+    if (g_started != 1) return;
+    for (int i = g_nscols - 1; i >= 0; i--) /* unguardable host rows: single-use copies */
+        if (g_scols[i].op != shim_op() && !g_scols[i].guard) scol_drop(i);
+    for (int i = g_nssh - 1; i >= 0; i--)
+        if (g_ssh[i].op != shim_op() && !g_ssh[i].guard) ssh_drop(i);
+    ssh_make_room(0);
+}
+
+void shard_forget_column(const Column* c) {
+    for (int i = 0; i < g_nscols; i++)
+        if (g_scols[i].col == c) {
+            scol_drop(i);
+            return;
+        }
+}
+
+static void t_trim(Shard* s, void* a) {
+    (void)a;
+    mq_stream_sync(s->stream);
+    mq_pool_free(s->ws);
+    mq_pool_free(s->scratch);
+    s->ws = s->scratch = NULL;
+    s->ws_bytes = s->scratch_bytes = 0;
+    mq_trim();
+}
+
+void shard_release_all(void) {
+    if (g_started != 1) return;
+    while (g_nscols) scol_drop(g_nscols - 1);
+    while (g_nssh) ssh_drop(g_nssh - 1);
+    run_all(t_trim, NULL);
+}
+
+void shard_stats(mq_residency* out) {
+    configure();
+    out->shards = (uint64_t)g_G;
+    out->shard_columns = (uint64_t)g_nscols;
+    out->shard_shadows = (uint64_t)g_nssh;
+    out->shard_ops = g_ops;
+    out->shard_uploads = g_uploads;
+}
+
+static void t_stop(Shard* s, void* a) {
+    (void)a;
+    t_trim(s, NULL);
+    mq_stream_destroy(s->stream);
+    mq_free(s->small);
+    s->stream = s->small = NULL;
+    s->quit = 1;
+}
+
+/* mq_shard_config (mq_query.h): drop every sharded copy, stop the workers, then take
+ * the new layout (G <= 0: back to the environment's). */
+int mq_shard_config(int shards, const int* devices, int ndev, uint64_t min_rows) {
+    if (g_started == 1) {
+        shard_release_all();
+        run_all(t_stop, NULL);
+    }
+    g_started = 0;
+    g_G = -1;
+    if (shards <= 0) return MQ_OK;
+    if (shards > MAXS || (ndev > 0 && !devices)) return MQ_EINVAL;
+    memset(g_sh, 0, sizeof g_sh);
+    const char* pe = getenv("MQ_DEVICE");
+    const int primary = pe ? atoi(pe) : 0;
+    int count = mq_device_count();
+    if (count < 1) count = 1;
+    for (int g = 0; g < shards; g++) {
+        g_sh[g].idx = g;
+        g_sh[g].dev = ndev > 0 ? devices[g % ndev] : (primary + g) % count;
+        if (g_sh[g].dev < 0 || g_sh[g].dev >= count) return MQ_EINVAL;
+    }
+    g_min_rows = (size_t)min_rows;
+    g_G = shards;
+    return MQ_OK;
+}

@@ -188,6 +188,7 @@ _SIGS = {
     "mq_column_invalidate": (None, [C.POINTER(Column)]),
     "mq_result_device_ptr": (_vp, [_PR]),
     "mq_release_all": (None, []),
+    "mq_shard_config": (_int, [_int, C.POINTER(_int), _int, _u64]),
     "mq_transfer_seconds": (C.c_double, [_int]),
     "mq_residency_stats": (None, [C.c_void_p]),
     # write guards (csrc/mq_guard.h; internal, bound for the guard tests)
@@ -204,7 +205,8 @@ class Residency(C.Structure):  # include/mq_query.h mq_residency
     _fields_ = [(n, C.c_uint64) for n in (
         "column_uploads", "column_bytes", "result_uploads", "result_bytes", "guards_armed",
         "guard_clean", "guard_stale", "guards_live", "remap_probe", "columns_resident",
-        "shadows_resident", "shadow_bytes")]
+        "shadows_resident", "shadow_bytes", "shards", "shard_columns", "shard_shadows", "shard_ops",
+        "shard_uploads")]
 
 
 def residency(lib=None) -> dict:

@@ -208,6 +208,15 @@ int mq_column_upload(Column* column);
 void mq_column_invalidate(Column* column);
 /* Device pointer of a libmq-produced Result's shadow copy, or NULL. */
 const void* mq_result_device_ptr(const Result* result);
+/* Row shards: columns of at least min_rows rows are split into `shards`
+ * contiguous row ranges, range g resident on device devices[g % ndev] (ndev = 0: the
+ * primary device + g, modulo the device count) and served by a host thread and stream
+ * of its own; select_column, fetch_column, sum/avg/min/max and shared_select then run
+ * on every shard and concatenate / fold in shard order. Replaces the MQ_SHARDS /
+ * MQ_DEVICES / MQ_SHARD_MIN_ROWS environment (read at first use); drops every sharded
+ * copy first. shards <= 0 returns to the environment's layout. Several shards may
+ * share one device (a rehearsal of the split on a one-GPU machine). */
+int mq_shard_config(int shards, const int* devices, int ndev, uint64_t min_rows);
 /* Drop every cached device copy. */
 void mq_release_all(void);
 /* Residency counters since load (tests and the bench read them). */
@@ -217,6 +226,9 @@ typedef struct mq_residency {
     uint64_t guards_armed, guard_clean, guard_stale, guards_live;
     uint64_t remap_probe;                   /* 1: a remapped range is told apart (MADV_POPULATE_WRITE) */
     uint64_t columns_resident, shadows_resident, shadow_bytes;
+    /* row shards (MQ_SHARDS): shard count, sharded columns and result shadows held,
+     * sharded operator calls served, sharded column uploads */
+    uint64_t shards, shard_columns, shard_shadows, shard_ops, shard_uploads;
 } mq_residency;
 void mq_residency_stats(mq_residency* out);
 /* Seconds spent in host<->device copies by the query API since the last reset. */

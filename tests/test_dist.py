@@ -121,3 +121,112 @@ def test_shard_rows_cover_exactly():
             assert spans[0][0] == 0 and spans[-1][1] == n
             for (a, b), (c, d) in zip(spans, spans[1:]):
                 assert b == c and a <= b
+
+
+# ---------------------------------------------------------------------------
+# The same combine over libmq's own kernels (-m gpu): each rank runs the HIP path
+# on its shard, both ranks on device 0 (gloo carries the exchange: RCCL refuses
+# two ranks on one device), then the world-size-1 RCCL ("nccl") path on its own.
+# ---------------------------------------------------------------------------
+
+def _libmq_worker(rank, world, port, q, backend):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    import refcpu
+    from refapi import mq
+    lib = mq.load()
+    mq.check(lib.mq_init(0), "mq_init")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    mqd = _dist_mod()
+    out = {}
+    ws = torch.empty(lib.mq_scan_workspace_bytes(1 << 21), dtype=torch.uint8, device=dev)
+    # config 4: rank r's own column, seed 42 + r, generated on the device
+    n = 1_000_000
+    lo, hi = n // 4, n // 4 + n // 100
+    col = torch.empty(n, dtype=torch.int32, device=dev)
+    mq.check(lib.mq_gen_uniform(col.data_ptr(), n, 42 + rank, n, None), "gen")
+    agg = mqd.agg_tensor(dev)
+    mq.check(lib.mq_select_agg(col.data_ptr(), n, 1, lo, 1, hi, agg.data_ptr(), ws.data_ptr(),
+                               ws.numel(), None), "select_agg")
+    torch.cuda.synchronize()
+    out["cfg4"] = mqd.combine_full(agg if backend == "nccl" else agg.cpu())
+    # row shards of one column: positions numbered from the shard base on the device
+    N = 1_500_001
+    host = refcpu.gen_uniform(N, 7)
+    a, b = mqd.shard_rows(N, rank, world)
+    shard = torch.from_numpy(host[a:b].copy()).to(dev)
+    posbuf = torch.empty(max(b - a, 1), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    mq.check(lib.mq_select_positions_at(shard.data_ptr(), None, b - a, a, 1, 1000, 1, 900_000,
+                                        posbuf.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                        None), "select_positions_at")
+    agg2 = mqd.agg_tensor(dev)
+    mq.check(lib.mq_select_agg(shard.data_ptr(), b - a, 1, 1000, 1, 900_000, agg2.data_ptr(),
+                               ws.data_ptr(), ws.numel(), None), "select_agg shard")
+    torch.cuda.synchronize()
+    out["rows"] = mqd.combine_full(agg2 if backend == "nccl" else agg2.cpu())
+    p = posbuf[: int(cnt.item())].cpu().tolist()
+    lists = [None] * world
+    dist.all_gather_object(lists, p)
+    out["positions"] = [x for part in lists for x in part]
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def _spawn(world, backend, timeout=240):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_libmq_worker, args=(r, world, port, q, backend)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=timeout) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _expect(refcpu, world):
+    n = 1_000_000
+    lo, hi = n // 4, n // 4 + n // 100
+    vals = []
+    for seed in range(42, 42 + world):
+        d = refcpu.gen_uniform(n, seed)
+        vals.append(d[refcpu.select_scan(d, lo, hi)])
+    cfg4 = refcpu.agg(np.concatenate(vals))
+    col = refcpu.gen_uniform(1_500_001, 7)
+    pos = refcpu.select_scan(col, 1000, 900_000)
+    return cfg4, refcpu.agg(col[pos]), pos
+
+
+def _check(res, refcpu, world):
+    cfg4, rows, pos = _expect(refcpu, world)
+    for r in range(world):
+        for got, want in ((res[r]["cfg4"], cfg4), (res[r]["rows"], rows)):
+            assert (got["count"], got["sum"], got["min"], got["max"]) == (want["count"], want["sum"],
+                                                                          want["min"], want["max"])
+            assert struct.pack("<d", got["avg"]) == struct.pack("<d", want["avg"])
+        assert np.array_equal(np.array(res[r]["positions"], dtype=np.int32), pos)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_ranks_run_libmq_and_combine(refcpu):
+    """the multi-rank combine over libmq's kernels (not stand-ins)."""
+    _check(_spawn(2, "gloo"), refcpu, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_combine_one_rank(refcpu):
+    """The "nccl" backend (RCCL on ROCm) initialised and all-reducing libmq's device
+    aggregate: the collective the driver's multi-GPU bench runs, at world size 1."""
+    _check(_spawn(1, "nccl"), refcpu, 1)
