@@ -33,6 +33,9 @@ uint32_t resident_grid(const DevState* s, uint64_t work_items, const void* fn);
 uint64_t scan_u32_scratch_elems(uint64_t n);
 int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st);
+// The same over u64 elements (in and out may alias); scratch as above.
+int scan_u64_exclusive(const unsigned long long* in, unsigned long long* out, uint64_t n,
+                       unsigned long long* scratch, hipStream_t st);
 
 // Stable LSD radix sort (4 x 8-bit digits) of (int32 key, u32 value) pairs by key
 // (mq_join.hip). vals == nullptr sorts (key, row id). *keys_out receives the keys

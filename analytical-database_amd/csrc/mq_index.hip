@@ -79,9 +79,335 @@ __global__ __launch_bounds__(kTPB) void k_histogram(const int32_t* __restrict__ 
         if (h[i]) atomicAdd(&counts[i], (unsigned long long)h[i]);
 }
 
+// ---------------------------------------------------------------------------
+// The reference's quicksort order (index.c:25-46), level by level.
+//
+// quicksort(low, high) partitions [low, high] around values[high] (Lomuto) and
+// recurses on both sides; disjoint ranges do not interact, so every range of one
+// recursion depth is partitioned at once. One partition of a range with c values
+// below the pivot, restated without its sequential loop:
+//   * the k-th value below the pivot (index j_k, in index order) is swapped with
+//     index low + k, so it ends at low + k: the "<" side is a stable compaction;
+//   * a value >= the pivot moves only when it sits at low + k as the k-th "<" value
+//     is found (j_k is beyond it); it then jumps to j_k. From index x it therefore
+//     follows x -> J[x] -> J[J[x]] ... (J[low + k] = j_k) until the index leaves
+//     [low, low + c): a chain walk, or pointer doubling when a chain is long;
+//   * the final swap puts the pivot at low + c and the value that ended there at high.
+// A range whose values all equal its pivot would recurse one element per level
+// (O(n) depth); its outcome has a closed form: the last value first, then the
+// others in order (by induction over the partitions), so it finishes at once.
+// Values and row ids move as (int32, u32) pairs; SID is each index's range id at the
+// current depth (-1: final). Levels cost a few passes over n each; the host reads
+// one count per level.
+// ---------------------------------------------------------------------------
+struct LSeg {
+    uint32_t lo, hi;
+};
+
+__global__ __launch_bounds__(kTPB) void k_lq_init(const int32_t* __restrict__ col, uint64_t n, int32_t* __restrict__ V,
+                                                  uint32_t* __restrict__ P, int32_t* __restrict__ SID) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        V[i] = col[i];
+        P[i] = (uint32_t)i;
+        SID[i] = 0;
+    }
+}
+
+// per index: (v < pivot) in the low 32 bits, (v > pivot) in the high 32 bits
+__global__ __launch_bounds__(kTPB) void k_lq_flags(const int32_t* __restrict__ V, const int32_t* __restrict__ SID,
+                                                   const LSeg* __restrict__ seg, uint64_t n,
+                                                   unsigned long long* __restrict__ FL) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const int32_t sid = SID[i];
+        unsigned long long f = 0;
+        if (sid >= 0) {
+            const uint32_t hi = seg[sid].hi;
+            if ((uint32_t)i != hi) {
+                const int32_t piv = V[hi], v = V[i];
+                f = (v < piv ? 1ull : 0ull) | (v > piv ? (1ull << 32) : 0ull);
+            }
+        }
+        FL[i] = f;
+    }
+}
+
+// per range: c, all-equal, children (ranges of >= 2 indexes)
+__global__ __launch_bounds__(kTPB) void k_lq_segs(const LSeg* __restrict__ seg, uint32_t S,
+                                                  const unsigned long long* __restrict__ EX,
+                                                  uint32_t* __restrict__ segc, uint32_t* __restrict__ nchild) {
+    for (uint32_t s = blockIdx.x * kTPB + threadIdx.x; s < S; s += gridDim.x * kTPB) {
+        const LSeg g = seg[s];
+        const unsigned long long tot = EX[g.hi] - EX[g.lo];  // the pivot's own flag is 0
+        const uint32_t c = (uint32_t)tot, gt = (uint32_t)(tot >> 32), m = g.hi - g.lo;
+        const bool eq = c == 0 && gt == 0;
+        segc[s] = eq ? 0xFFFFFFFFu : c;
+        nchild[s] = eq ? 0u : (uint32_t)(c >= 2) + (uint32_t)(m - c >= 2);
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_lq_children(const LSeg* __restrict__ seg, uint32_t S,
+                                                      const uint32_t* __restrict__ segc,
+                                                      const uint32_t* __restrict__ nchild,
+                                                      const unsigned long long* __restrict__ cbase,
+                                                      LSeg* __restrict__ next, int32_t* __restrict__ lid,
+                                                      int32_t* __restrict__ rid, unsigned long long* __restrict__ d_snext) {
+    for (uint32_t s = blockIdx.x * kTPB + threadIdx.x; s < S; s += gridDim.x * kTPB) {
+        const LSeg g = seg[s];
+        const uint32_t c = segc[s];
+        uint32_t at = (uint32_t)cbase[s];
+        int32_t l = -1, r = -1;
+        if (c != 0xFFFFFFFFu) {
+            const uint32_t m = g.hi - g.lo;
+            if (c >= 2) {
+                l = (int32_t)at;
+                next[at++] = LSeg{g.lo, g.lo + c - 1};
+            }
+            if (m - c >= 2) {
+                r = (int32_t)at;
+                next[at] = LSeg{g.lo + c + 1, g.hi};
+            }
+        }
+        lid[s] = l;
+        rid[s] = r;
+        if (s == S - 1) *d_snext = cbase[s] + nchild[s];
+    }
+}
+
+// J[lo + rank] = index of the rank-th value below the pivot
+__global__ __launch_bounds__(kTPB) void k_lq_less(const int32_t* __restrict__ V, const int32_t* __restrict__ SID,
+                                                  const LSeg* __restrict__ seg, const unsigned long long* __restrict__ EX,
+                                                  uint64_t n, uint32_t* __restrict__ J) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const int32_t sid = SID[i];
+        if (sid < 0) continue;
+        const LSeg g = seg[sid];
+        if ((uint32_t)i == g.hi || !(V[i] < V[g.hi])) continue;
+        J[g.lo + ((uint32_t)EX[i] - (uint32_t)EX[g.lo])] = (uint32_t)i;
+    }
+}
+
+constexpr int kChainCap = 64;  // chain steps walked before pointer doubling takes over
+
+template <bool USE_F>
+__global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
+                                                   const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
+                                                   const unsigned long long* __restrict__ EX,
+                                                   const uint32_t* __restrict__ segc, const int32_t* __restrict__ lid,
+                                                   const int32_t* __restrict__ rid, const uint32_t* __restrict__ J,
+                                                   uint64_t n, int32_t* __restrict__ Vn, uint32_t* __restrict__ Pn,
+                                                   int32_t* __restrict__ SIDn, unsigned int* __restrict__ long_chain) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const int32_t sid = SID[i];
+        const int32_t v = V[i];
+        const uint32_t row = P[i];
+        uint32_t q = (uint32_t)i;
+        int32_t ns = -1;
+        if (sid >= 0) {
+            const LSeg g = seg[sid];
+            const uint32_t c = segc[sid];
+            if (c == 0xFFFFFFFFu) {                 // all equal: last first, then in order
+                q = (uint32_t)i == g.hi ? g.lo : (uint32_t)i + 1;
+            } else if ((uint32_t)i == g.hi) {       // the pivot
+                q = g.lo + c;
+            } else if (v < V[g.hi]) {              // stable compaction of the "<" side
+                q = g.lo + ((uint32_t)EX[i] - (uint32_t)EX[g.lo]);
+                ns = lid[sid];
+            } else {                                // the >= side: follow the swaps
+                int steps = 0;
+                while (q - g.lo < c) {
+                    q = J[q];
+                    if (!USE_F && ++steps > kChainCap) break;
+                }
+                if (!USE_F && q - g.lo < c) {  // long chain: doubling, then this kernel again
+                    atomicOr(long_chain, 1u);
+                    continue;
+                }
+                if (q == g.lo + c) q = g.hi;        // the final swap with the pivot
+                ns = rid[sid];
+            }
+        }
+        Vn[q] = v;
+        Pn[q] = row;
+        SIDn[q] = ns;
+    }
+}
+
+// pointer doubling on J over each range's "<" zone [lo, lo + c): J[q] <- J[J[q]]
+// while J[q] is still inside the zone (in place: a concurrent update only moves a
+// pointer further along its own chain, never past the chain's end)
+__global__ __launch_bounds__(kTPB) void k_lq_jump(const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
+                                                  const uint32_t* __restrict__ segc, uint64_t n, uint32_t* J,
+                                                  unsigned int* __restrict__ changed) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    unsigned int any = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        const int32_t sid = SID[i];
+        if (sid < 0) continue;
+        const uint32_t lo = seg[sid].lo, c = segc[sid];
+        if (c == 0xFFFFFFFFu || (uint32_t)i - lo >= c) continue;
+        const uint32_t f = J[i];
+        // J[i] == i: the first i - lo + 1 values are all below the pivot; no chain of
+        // a >= value passes there, and it would never converge
+        if (f != (uint32_t)i && f - lo < c) {
+            J[i] = J[f];
+            any = 1;
+        }
+    }
+    if (any) atomicOr(changed, 1u);
+}
+
+__global__ __launch_bounds__(kTPB) void k_lq_emit(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
+                                                  uint64_t n, int32_t* __restrict__ vout,
+                                                  unsigned long long* __restrict__ pout) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        if (vout) vout[i] = V[i];
+        if (pout) pout[i] = P[i];
+    }
+}
+
+// any i with v[i] == v[i+1] in a sorted array
+__global__ __launch_bounds__(kTPB) void k_has_ties(const int32_t* __restrict__ v, uint64_t n, unsigned int* __restrict__ flag) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    unsigned int t = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i + 1 < n; i += stride) t |= v[i] == v[i + 1];
+    if (__ballot(t) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+struct LqBufs {
+    void* blk[24];
+    int nb;
+    ~LqBufs() {
+        for (int i = 0; i < nb; i++) pool_free(blk[i]);
+    }
+    template <typename T>
+    T* get(size_t count) {
+        void* p = pool_alloc((count ? count : 1) * sizeof(T));
+        if (p) blk[nb++] = p;
+        return static_cast<T*>(p);
+    }
+};
+
+int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, hipStream_t st, const DevState* s) {
+    const uint64_t smax = n / 2 + 2;
+    LqBufs b;
+    b.nb = 0;
+    int32_t* V[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
+    uint32_t* P[2] = {b.get<uint32_t>(n), b.get<uint32_t>(n)};
+    int32_t* SID[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
+    unsigned long long* EX = b.get<unsigned long long>(n);
+    uint32_t* J = b.get<uint32_t>(n);
+    LSeg* seg[2] = {b.get<LSeg>(smax), b.get<LSeg>(smax)};
+    uint32_t* segc = b.get<uint32_t>(smax);
+    uint32_t* nchild = b.get<uint32_t>(smax);
+    unsigned long long* cbase = b.get<unsigned long long>(smax);
+    int32_t* lid = b.get<int32_t>(smax);
+    int32_t* rid = b.get<int32_t>(smax);
+    unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(n));
+    unsigned long long* small = b.get<unsigned long long>(4);  // [S_next, long_chain | changed]
+    if (b.nb != 17) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
+    unsigned int* flags = reinterpret_cast<unsigned int*>(small + 1);
+    const uint32_t gn = stream_grid(s, n);
+    hipLaunchKernelGGL(k_lq_init, dim3(gn), dim3(kTPB), 0, st, col, n, V[0], P[0], SID[0]);
+    LAUNCHCHK("k_lq_init");
+    const LSeg root{0u, (uint32_t)(n - 1)};
+    HIPCHK(hipMemcpyAsync(seg[0], &root, sizeof root, hipMemcpyHostToDevice, st));
+    uint64_t S = n >= 2 ? 1 : 0;
+    int cur = 0;
+    while (S) {
+        const uint32_t gs = stream_grid(s, S);
+        hipLaunchKernelGGL(k_lq_flags, dim3(gn), dim3(kTPB), 0, st, V[cur], SID[cur], seg[cur], n, EX);
+        LAUNCHCHK("k_lq_flags");
+        int rc = scan_u64_exclusive(EX, EX, n, scratch, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_lq_segs, dim3(gs), dim3(kTPB), 0, st, seg[cur], (uint32_t)S, EX, segc, nchild);
+        LAUNCHCHK("k_lq_segs");
+        if ((rc = scan_u32_exclusive(nchild, cbase, S, scratch, st))) return rc;
+        hipLaunchKernelGGL(k_lq_children, dim3(gs), dim3(kTPB), 0, st, seg[cur], (uint32_t)S, segc, nchild, cbase,
+                           seg[cur ^ 1], lid, rid, small);
+        LAUNCHCHK("k_lq_children");
+        hipLaunchKernelGGL(k_lq_less, dim3(gn), dim3(kTPB), 0, st, V[cur], SID[cur], seg[cur], EX, n, J);
+        LAUNCHCHK("k_lq_less");
+        HIPCHK(hipMemsetAsync(flags, 0, 8, st));
+        hipLaunchKernelGGL(k_lq_final<false>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
+                           segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags);
+        LAUNCHCHK("k_lq_final");
+        unsigned long long h[2];
+        HIPCHK(hipMemcpyAsync(h, small, 16, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if ((uint32_t)h[1]) {  // a chain longer than kChainCap: double J, then place everyone again
+            for (int it = 0;; it++) {
+                if (it > 40) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
+                HIPCHK(hipMemsetAsync(flags + 1, 0, 4, st));
+                hipLaunchKernelGGL(k_lq_jump, dim3(gn), dim3(kTPB), 0, st, SID[cur], seg[cur], segc, n, J, flags + 1);
+                LAUNCHCHK("k_lq_jump");
+                unsigned int ch = 0;
+                HIPCHK(hipMemcpyAsync(&ch, flags + 1, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                if (!ch) break;
+            }
+            hipLaunchKernelGGL(k_lq_final<true>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
+                               segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags);
+            LAUNCHCHK("k_lq_final");
+        }
+        S = h[0];
+        cur ^= 1;
+    }
+    hipLaunchKernelGGL(k_lq_emit, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], n, vout,
+                       reinterpret_cast<unsigned long long*>(pout));
+    LAUNCHCHK("k_lq_emit");
+    HIPCHK(hipStreamSynchronize(st));  // the scratch goes back to the pool
+    return MQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int mq_index_build_lomuto(const int32_t* d_col, uint64_t n, int32_t* d_values_out, uint64_t* d_positions_out,
+                          void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (n && (!d_col || (!d_values_out && !d_positions_out)))
+        return set_err(MQ_EINVAL, "mq_index_build_lomuto: NULL pointer");
+    if (n >= (1ull << 31)) return set_err(MQ_EINVAL, "mq_index_build_lomuto: n >= 2^31");
+    if (n == 0) return MQ_OK;
+    return lomuto_sort(d_col, n, d_values_out, d_positions_out, (hipStream_t)stream, s);
+}
+
+int mq_index_build_ref(const int32_t* d_col, uint64_t n, int32_t* d_values_out, uint64_t* d_positions_out,
+                       uint64_t exact_max, int* h_exact, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!d_values_out || (n && !d_col)) return set_err(MQ_EINVAL, "mq_index_build_ref: NULL pointer");
+    if (h_exact) *h_exact = 1;
+    if ((rc = mq_index_build(d_col, n, d_values_out, d_positions_out, stream)) || n < 2) return rc;
+    // distinct values: the sort order is unique, the radix result is the reference's
+    hipStream_t st = (hipStream_t)stream;
+    unsigned int* flag = static_cast<unsigned int*>(pool_alloc(4));
+    if (!flag) return set_err(MQ_ENOMEM, "mq_index_build_ref: allocation failed");
+    unsigned int ties = 0;
+    int e = hipMemsetAsync(flag, 0, 4, st) == hipSuccess ? 0 : 1;
+    if (!e) {
+        hipLaunchKernelGGL(k_has_ties, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, d_values_out, n, flag);
+        e = hipGetLastError() != hipSuccess || hipMemcpyAsync(&ties, flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess;
+    }
+    pool_free(flag);
+    if (e) return set_err(MQ_EHIP, "mq_index_build_ref: tie check failed");
+    if (!ties) return MQ_OK;
+    if (n > exact_max || n >= (1ull << 31)) {
+        if (h_exact) *h_exact = 0;  // equal values stay in ascending row order
+        return MQ_OK;
+    }
+    return lomuto_sort(d_col, n, d_values_out, d_positions_out, st, s);
+}
 
 int mq_index_build(const int32_t* d_col, uint64_t n, int32_t* d_values_out,
                    uint64_t* d_positions_out, void* stream) {

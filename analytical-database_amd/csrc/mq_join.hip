@@ -783,6 +783,10 @@ int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st) {
     return scan_exclusive<uint32_t>(in, out, n, scratch, st);
 }
+int scan_u64_exclusive(const unsigned long long* in, unsigned long long* out, uint64_t n,
+                       unsigned long long* scratch, hipStream_t st) {
+    return scan_exclusive<u64>(in, out, n, scratch, st);
+}
 }  // namespace mqi
 
 // ===========================================================================

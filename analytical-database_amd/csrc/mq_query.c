@@ -1280,6 +1280,15 @@ typedef struct MqHistogram { /* cs165_api.h:71-75 */
 } MqHistogram;
 _Static_assert(sizeof(MqHistogram) == 1208, "Histogram size");
 
+/* Up to this many rows an index over equal values reproduces the reference
+ * quicksort's order of them exactly (mq_index_build_lomuto); beyond it (where the
+ * reference's recursion and reorder_column's stack array cannot run) they keep
+ * ascending row order. MQ_INDEX_EXACT_MAX overrides. */
+static uint64_t index_exact_max(void) {
+    const char* e = getenv("MQ_INDEX_EXACT_MAX");
+    return e ? (uint64_t)strtoull(e, NULL, 10) : ((uint64_t)1 << 27);
+}
+
 /* One indexed column (index.c:119-143 + :63-84). Returns 0 or an MQ_E code. */
 static int index_one(Table* t, Column* c, Status* st) {
     const size_t n = c->row_count;
@@ -1295,7 +1304,11 @@ static int index_one(Table* t, Column* c, Status* st) {
         goto bad;
     }
     if ((rc = mq_malloc(&dv, (n ? n : 1) * 4)) || (rc = mq_malloc(&dp, (n ? n : 1) * 8))) goto bad;
-    if ((rc = mq_index_build(dcol, n, dv, dp, g_stream))) goto bad;
+    int exact = 1;
+    if ((rc = mq_index_build_ref(dcol, n, dv, dp, index_exact_max(), &exact, g_stream))) goto bad;
+    if (!exact)
+        fprintf(stderr, "libmq: build_index: %zu rows of %s hold equal values beyond MQ_INDEX_EXACT_MAX; "
+                        "they keep ascending row order instead of the reference quicksort's\n", n, c->name);
     if (n && (rc = d2h(hv, dv, n * 4))) goto bad;
     ix->values = hv;
     if (c->clustered) {

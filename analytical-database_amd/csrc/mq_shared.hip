@@ -430,6 +430,206 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
     }
 }
 
+// ---------------------------------------------------------------------------
+// One read of the column (q >= kEiMinQ, the usual case): the count pass also lists
+// every (query, row) pair of its wave-chunk, in row order, into the wave's slice of
+// the workspace (one u32 per pair: query << 24 | row offset in the wave-chunk);
+// after the scan, k_ssp_scatter sorts each slice by query in LDS, 2048 pairs at a
+// time (stable: 8-ballot match-any ranks), and writes every query's run of rows
+// with consecutive stores. HBM: 4N + 4K (pairs) + 4K + 4K (scatter) instead of
+// 8N + 4K, and no second pass of interval lookups. A slice holds one pair per row
+// of its wave-chunk; a wave-chunk with more pairs (dense queries) flags an overflow
+// and the write falls back to the column pass (k_ssi_write) on the same counts.
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
+                                                    EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
+                                                    uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
+                                                    uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
+    __shared__ uint32_t s_bkt[kBuckets];
+    __shared__ int32_t s_b[kEiMax];
+    __shared__ uint32_t s_qoff[kEiMax];
+    __shared__ uint32_t hist[kWaves][kEiMax];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    stage_buckets(T.bucket, s_bkt, tid);
+    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
+    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
+    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    uint64_t s, e;
+    wave_chunk(n, rpb, wave, &s, &e);
+    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    uint32_t* list = pairs + wc * cap;
+    uint32_t run = 0;  // pairs of this wave-chunk so far (wave-uniform)
+    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
+        int4 v[kSsUnroll];
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++)
+            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++) {
+            const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
+            const int x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t qa[4], qn[4], np = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                qa[k] = 0;
+                qn[k] = 0;
+                if (row + k < e) {
+                    const int ei = ei_of(x[k], M, s_bkt, s_b);
+                    qa[k] = s_qoff[ei];
+                    qn[k] = s_qoff[ei + 1] - qa[k];
+                    if (qn[k]) atomicAdd(&hist[wave][ei], 1u);
+                }
+                np += qn[k];
+            }
+            uint32_t incl = np;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t tot = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+            if (tot == 0) continue;
+            if ((uint64_t)run + tot <= cap) {
+                uint32_t at = run + incl - np;
+                const uint32_t r0 = (uint32_t)(row - s);
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    for (uint32_t i = 0; i < qn[k]; i++) list[at++] = ((uint32_t)T.qlist[qa[k] + i] << 24) | (r0 + k);
+            }
+            run += tot;  // past cap: still counted, the slice is incomplete
+        }
+    }
+    if (lane == 0) {
+        npairs[wc] = run;
+        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // per-query counts from the EI histogram's prefix (as k_ssi_count)
+    uint32_t* h = hist[wave];
+    const int ne = M.m + 2;
+    const int per = (ne + 63) / 64;
+    uint32_t loc = 0;
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) loc += h[j];
+    }
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    uint32_t acc = incl - loc;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) {
+            const uint32_t c = h[j];
+            h[j] = acc;
+            acc += c;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < q; i += 64) {
+        const uint32_t ab = T.qab[i];
+        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
+    }
+}
+
+constexpr int kSpChunk = 2048;                  // pairs sorted in LDS at a time
+constexpr int kSpPerWave = kSpChunk / kWaves;   // 512: 8 rounds of 64
+constexpr int kSpRounds = kSpPerWave / 64;
+
+__global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict__ pairs, uint64_t cap,
+                                                      const uint32_t* __restrict__ npairs,
+                                                      const unsigned long long* __restrict__ offs, uint64_t nwc,
+                                                      int q, int* const* __restrict__ outs, uint64_t rpb,
+                                                      int32_t base) {
+    __shared__ uint32_t s_sorted[kSpChunk];
+    __shared__ uint32_t s_cnt[kWaves][kMaxQ];
+    __shared__ uint32_t s_start[kMaxQ], s_tot[kMaxQ];
+    __shared__ unsigned long long s_run[kMaxQ];
+    __shared__ gint* s_out[kMaxQ];
+    __shared__ uint32_t s_wsum[kWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t wc = blockIdx.x;
+    const uint32_t np = npairs[wc];
+    const uint32_t* list = pairs + wc * cap;
+    const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
+    for (int i = tid; i < q; i += kTPB) {
+        s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
+        s_out[i] = global_ptr(outs[i]);
+    }
+    for (uint32_t c0 = 0; c0 < np; c0 += kSpChunk) {
+        for (int i = tid; i < kWaves * kMaxQ; i += kTPB) (&s_cnt[0][0])[i] = 0;
+        __syncthreads();
+        // this wave's 512 pairs of the chunk, loaded first, then ranked round by round
+        uint32_t x[kSpRounds], loc[kSpRounds];
+#pragma unroll
+        for (int r = 0; r < kSpRounds; r++) {
+            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
+            x[r] = idx < np ? list[idx] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kSpRounds; r++) {
+            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
+            const bool valid = idx < np;
+            const uint32_t qid = x[r] >> 24;
+            const unsigned long long peers = match_any8(qid, __ballot(valid));
+            const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
+            loc[r] = before + (uint32_t)__popcll(peers & ltmask);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (peers & ~ltmask & ~(1ull << lane)) == 0) s_cnt[wave][qid] = before + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        // bucket starts: queries in order, waves in order inside a query
+        uint32_t tq = 0;
+        if (tid < q) {
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) tq += s_cnt[w][tid];
+        }
+        uint32_t incl = tq;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        if (tid < q) {
+            uint32_t st0 = incl - tq;
+            for (int w = 0; w < wave; w++) st0 += s_wsum[w];
+            s_start[tid] = st0;
+            s_tot[tid] = tq;
+            uint32_t a = st0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t c = s_cnt[w][tid];
+                s_cnt[w][tid] = a;
+                a += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kSpRounds; r++) {
+            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
+            if (idx < np) s_sorted[s_cnt[wave][x[r] >> 24] + loc[r]] = x[r];
+        }
+        __syncthreads();
+        const uint32_t cn = np - c0 < (uint32_t)kSpChunk ? np - c0 : (uint32_t)kSpChunk;
+        for (uint32_t i = tid; i < cn; i += kTPB) {
+            const uint32_t y = s_sorted[i], qid = y >> 24;
+            s_out[qid][s_run[qid] + (i - s_start[qid])] = (int)(row0 + (y & 0xFFFFFFu)) + base;
+        }
+        __syncthreads();
+        if (tid < q) s_run[tid] += s_tot[tid];
+    }
+}
+
 // totals[j] = offs[j*nwc + nwc-1] + counts[j*nwc + nwc-1] - offs[j*nwc]
 __global__ void k_ss_totals(const uint32_t* __restrict__ counts,
                             const unsigned long long* __restrict__ offs, uint64_t nwc, int q,

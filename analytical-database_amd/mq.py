@@ -145,6 +145,8 @@ _SIGS = {
     "mq_index_select": (_int, [_vp, _vp, _u64, _i32, _i32, _vp, _vp, _vp]),
     "mq_fetch": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "mq_index_build": (_int, [_vp, _u64, _vp, _vp, _vp]),
+    "mq_index_build_lomuto": (_int, [_vp, _u64, _vp, _vp, _vp]),
+    "mq_index_build_ref": (_int, [_vp, _u64, _vp, _vp, _u64, C.POINTER(_int), _vp]),
     "mq_gather_u64": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "mq_histogram": (_int, [_vp, _u64, _i32, _i32, _vp, _vp]),
     "mq_reduce": (_int, [_vp, _u64, _vp, _vp, _sz, _vp]),

@@ -170,6 +170,18 @@ int mq_index_select(const int32_t* d_values, const uint64_t* d_positions, uint64
  * the values, and the positions of distinct values, are identical.) */
 int mq_index_build(const int32_t* d_col, uint64_t n, int32_t* d_values_out,
                    uint64_t* d_positions_out, void* stream);
+/* The same in the reference quicksort's own order (index.c:25-46), equal values
+ * included: a level-synchronous restatement of the Lomuto recursion (n < 2^31).
+ * Costs a few passes over n per recursion depth (O(log n) depths on distinct-ish
+ * data; a range of equal values finishes in one). */
+int mq_index_build_lomuto(const int32_t* d_col, uint64_t n, int32_t* d_values_out,
+                          uint64_t* d_positions_out, void* stream);
+/* The build_index drop-in's policy: the radix sort; if the values hold ties and
+ * n <= exact_max, the Lomuto order instead (distinct values have one order, so the
+ * radix result is already the reference's). *h_exact = 0 when ties were left in
+ * ascending row order (n > exact_max). d_values_out is required. */
+int mq_index_build_ref(const int32_t* d_col, uint64_t n, int32_t* d_values_out, uint64_t* d_positions_out,
+                       uint64_t exact_max, int* h_exact, void* stream);
 /* reorder_column (index.c:105-114): d_out[i] = d_col[d_positions[i]] (size_t positions) */
 int mq_gather_u64(const int32_t* d_col, const uint64_t* d_positions, uint64_t n, int32_t* d_out,
                   void* stream);

@@ -591,6 +591,63 @@ void rc_index_build(const int32_t* col, size_t n, int32_t* values, uint64_t* pos
     free(p);
 }
 
+/* quicksort + partition exactly as index.c:25-46 (Lomuto, values[high] as the pivot,
+ * `<` sends a value left, the >= side rotated by the swaps), so equal values end in
+ * the reference's own order. Iterative (an explicit stack of [low, high] ranges in
+ * the order the recursion visits them) so that deep recursions (sorted or
+ * duplicate-heavy input: depth n) do not overflow the C stack; the result does not
+ * depend on the order disjoint ranges are visited. Positions start as 0..n-1
+ * (init_column_index :97-99). O(n^2) on duplicates, as the reference. */
+void rc_index_build_lomuto(const int32_t* col, size_t n, int32_t* values, uint64_t* positions) {
+    for (size_t i = 0; i < n; i++) {
+        values[i] = col[i];
+        positions[i] = i;
+    }
+    if (n < 2) return;
+    size_t cap = 64, top = 0;
+    int64_t* stk = malloc(cap * 2 * sizeof(int64_t));
+    stk[0] = 0;
+    stk[1] = (int64_t)n - 1;
+    top = 1;
+    while (top) {
+        top--;
+        const int64_t low = stk[2 * top], high = stk[2 * top + 1];
+        if (low >= high) continue;
+        const int32_t pivot = values[high];
+        int64_t i = low - 1;
+        for (int64_t j = low; j < high; j++) {
+            if (values[j] < pivot) {
+                i++;
+                int32_t tv = values[i];
+                values[i] = values[j];
+                values[j] = tv;
+                uint64_t tp = positions[i];
+                positions[i] = positions[j];
+                positions[j] = tp;
+            }
+        }
+        int32_t tv = values[i + 1];
+        values[i + 1] = values[high];
+        values[high] = tv;
+        uint64_t tp = positions[i + 1];
+        positions[i + 1] = positions[high];
+        positions[high] = tp;
+        const int64_t pv = i + 1;
+        if (top + 2 > cap) {
+            cap *= 2;
+            stk = realloc(stk, cap * 2 * sizeof(int64_t));
+        }
+        /* the recursion sorts [low, pv-1] first, then [pv+1, high]: push in reverse */
+        stk[2 * top] = pv + 1;
+        stk[2 * top + 1] = high;
+        top++;
+        stk[2 * top] = low;
+        stk[2 * top + 1] = pv - 1;
+        top++;
+    }
+    free(stk);
+}
+
 /* build_histogram (index.c:63-84): counts[(v - min) / bin_size]; rows whose bin is
  * outside [0, 100) go to counts[100] (the reference writes past its array). */
 void rc_histogram(const int32_t* col, size_t n, int32_t mn, int32_t bin_size, uint64_t* counts) {

@@ -82,6 +82,7 @@ size_t rc_csv_header_len(const char* text, size_t n);
 
 /* ---- index build (index.c:25-143): stable sort of (value, row) ---- */
 void rc_index_build(const int32_t* col, size_t n, int32_t* values, uint64_t* positions);
+void rc_index_build_lomuto(const int32_t* col, size_t n, int32_t* values, uint64_t* positions);
 /* build_histogram counts (index.c:63-84); counts has 101 entries, [100] = out of range */
 void rc_histogram(const int32_t* col, size_t n, int32_t mn, int32_t bin_size, uint64_t* counts);
 size_t rc_load_csv(const char* text, size_t n, int ncols, int32_t** cols, size_t cap,

@@ -63,6 +63,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rc_csv_header_len": (_sz, [_vp, _sz]),
         "rc_load_csv": (_sz, [_vp, _sz, C.c_int, _vp, _sz, _vp]),
         "rc_index_build": (None, [_vp, _sz, _vp, _vp]),
+        "rc_index_build_lomuto": (None, [_vp, _sz, _vp, _vp]),
         "rc_histogram": (None, [_vp, _sz, _i32, _i32, _vp]),
     }
     for name, (res, args) in sigs.items():
@@ -248,6 +249,16 @@ def index_build(col: np.ndarray):
     v = np.empty(max(len(col), 1), dtype=np.int32)
     p = np.empty(max(len(col), 1), dtype=np.uint64)
     lib().rc_index_build(_a(col), len(col), _a(v), _a(p))
+    return v[:len(col)].copy(), p[:len(col)].copy()
+
+
+def index_build_lomuto(col: np.ndarray):
+    """(sorted values int32, positions uint64) in the reference quicksort's own order
+    (index.c:25-46), equal values included."""
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    v = np.empty(max(len(col), 1), dtype=np.int32)
+    p = np.empty(max(len(col), 1), dtype=np.uint64)
+    lib().rc_index_build_lomuto(_a(col), len(col), _a(v), _a(p))
     return v[:len(col)].copy(), p[:len(col)].copy()
 
 

@@ -119,6 +119,20 @@ def run(csv_path: str, ncols: int, index_spec: str = "") -> dict:
         return out
 
 
+def quicksort(col: np.ndarray):
+    """The reference's own quicksort (index.c:25-46, in libdbm.so) on a copy of col with
+    positions 0..n-1, as init_column_index prepares them (:89-100). In-process: keep n
+    small (its recursion depth reaches n on sorted or duplicate-heavy input)."""
+    L = C.CDLL(LIBDBM)
+    L.quicksort.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    L.quicksort.restype = None
+    v = np.array(col, dtype=np.int32, copy=True)
+    p = np.arange(len(v), dtype=np.uint64)
+    if len(v):
+        L.quicksort(v.ctypes.data, p.ctypes.data, 0, len(v) - 1)
+    return v, p
+
+
 def load(csv_path: str, ncols: int, index_spec: str = "") -> dict:
     """The reference's load (and index build) of csv_path, run in a child process."""
     with tempfile.TemporaryDirectory() as tmp:

@@ -4,15 +4,12 @@
 oracle/refload.py drives oracle/_ref/libdbm.so (src/db_manager.c + utils.c +
 index.c compiled unchanged): create the table, create(idx, ...) per the case's
 spec, load the case's CSV with load_db, then build_index(db) as server.c:125 does.
-For every case of tests/indexcases.py this records, for the reference's result
-after canon() (indexcases.py: positions and clustered-reordered columns sorted
-within runs of equal indexed values, the one thing the reference's quicksort
-decides on its own):
+For every case of tests/indexcases.py this records the reference's result as it is
+(equal values in its quicksort's own order):
   in_fnv                   FNV-1a-64 of the CSV text (pins the input generator)
   ix<j>_values/_positions  FNV of the index arrays (values int32, positions u64)
   hist<j>_*                bin_size, values[100], counts[100] (unclustered)
   cols                     FNV of every column after the build
-and whether the raw (un-canonicalised) positions equal canon's (exact_positions).
 Run here, where /root/reference exists:  python tests/golden/make_index_goldens.py
 """
 from __future__ import annotations
@@ -31,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import refcpu  # noqa: E402
 import refload  # noqa: E402
-from indexcases import canon, cases, csv_text  # noqa: E402
+from indexcases import cases, csv_text  # noqa: E402
 
 
 def fnv(x) -> str:
@@ -60,13 +57,8 @@ def main() -> None:
             open(path, "wb").write(text)
             r = refload.load(path, len(cols), ",".join(f"{j}:{'c' if c else 'u'}" for j, c in spec))
             assert r["code"] == 0 and r["rows"] == cols.shape[1], name
-            c = canon(r, spec)
-            out[name] = {"in_fnv": f"{refcpu.fnv1a64_bytes(text):016x}", "spec": spec,
-                         **digest(c, spec),
-                         "exact_positions": {str(j): bool(np.array_equal(r[f"ix{j}_positions"],
-                                                                         c[f"ix{j}_positions"]))
-                                             for j, _ in spec}}
-            print(name, out[name]["exact_positions"])
+            out[name] = {"in_fnv": f"{refcpu.fnv1a64_bytes(text):016x}", "spec": spec, **digest(r, spec)}
+            print(name)
     with open(os.path.join(HERE, "index_goldens.json"), "w") as f:
         json.dump(out, f, indent=1)
 

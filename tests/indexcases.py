@@ -3,13 +3,12 @@
 
 A case is (name, columns int32[ncols][n], spec) with spec a list of (column,
 clustered) as create(idx, ...) declares them (db_manager.c:154-162).
-model() composes the oracle's stable sort (oracle/refcpu.c rc_index_build) exactly
-as build_index (src/index.c:152-178) does: columns in order; clustered -> sorted
-values, positions 0..n-1, every other column reordered by the permutation;
-unclustered -> sorted values, the permutation, the 100-bin histogram.
-canon() turns an index result into the form the reference must match whatever its
-quicksort does with equal values: within each run of equal sorted values, the
-positions (and, for a clustered index, the reordered columns) sorted.
+model() composes the oracle's restatement of the reference quicksort (oracle/refcpu.c
+rc_index_build_lomuto, equal values in the reference's own order) exactly as
+build_index (src/index.c:152-178) does: columns in order; clustered -> sorted values,
+positions 0..n-1, every other column reordered by the permutation; unclustered ->
+sorted values, the permutation, the 100-bin histogram. Parity is exact: no
+canonicalisation of equal values.
 """
 from __future__ import annotations
 
@@ -65,7 +64,7 @@ def model(refcpu, cols: np.ndarray, spec) -> dict:
     cols = cols.copy()
     out = {}
     for j, clustered in spec:
-        v, p = refcpu.index_build(cols[j])
+        v, p = refcpu.index_build_lomuto(cols[j])
         out[f"ix{j}_values"] = v
         if clustered:
             out[f"ix{j}_positions"] = np.arange(len(v), dtype=np.uint64)
@@ -80,36 +79,3 @@ def model(refcpu, cols: np.ndarray, spec) -> dict:
             out[f"hist{j}_counts"] = refcpu.histogram(cols[j], mn, bin_size)[:BIN_NUM]
     out["cols"] = cols
     return out
-
-
-def runs(sorted_values: np.ndarray):
-    """[start, end) of each run of equal values."""
-    if len(sorted_values) == 0:
-        return []
-    cut = np.flatnonzero(np.diff(sorted_values)) + 1
-    edges = np.concatenate([[0], cut, [len(sorted_values)]])
-    return list(zip(edges[:-1], edges[1:]))
-
-
-def canon_within_runs(sorted_values: np.ndarray, x: np.ndarray) -> np.ndarray:
-    y = np.array(x, copy=True)
-    for a, b in runs(sorted_values):
-        y[a:b] = np.sort(y[a:b])
-    return y
-
-
-def canon(result: dict, spec) -> dict:
-    """The tie-order-free form of an index build result."""
-    c = {"cols": np.array(result["cols"], copy=True)}
-    for j, clustered in spec:
-        v = np.asarray(result[f"ix{j}_values"])
-        c[f"ix{j}_values"] = v
-        c[f"ix{j}_positions"] = canon_within_runs(v, result[f"ix{j}_positions"])
-        if clustered:
-            for o in range(len(c["cols"])):
-                if o != j:
-                    c["cols"][o] = canon_within_runs(v, c["cols"][o])
-        else:
-            for k in ("bin_size", "values", "counts"):
-                c[f"hist{j}_{k}"] = np.asarray(result[f"hist{j}_{k}"])
-    return c

@@ -148,6 +148,7 @@ def run_suite(server_bin: str, workdir: str, tests=TESTS) -> dict:
     results = {}
     try:
         for i, tid in enumerate(tests):
+            print(f"{os.path.basename(server_bin)}: test {tid}", flush=True)  # progress (pytest -s)
             if i == 0 or tid in RESTART_BEFORE or srv.proc is None or srv.proc.poll() is not None:
                 srv.stop()
                 srv.start()
@@ -201,21 +202,16 @@ def test_libmq_dropin_server_passes_suite_and_matches_reference(tmp_path):
 @pytest.mark.skipif(not _have("server_mq_ix"), reason="server_mq_ix not built")
 @pytest.mark.timeout(900)
 def test_libmq_dropin_with_gpu_index_build(tmp_path):
-    """server_mq_ix also links libmq's build_index (GPU radix sort). Its verdicts
-    must be the reference's; its output must equal the reference server's except
-    where the reference's quicksort ordered equal indexed values differently, and
-    there it must equal it line-for-line after sorting (same rows, other order)."""
+    """server_mq_ix also links libmq's build_index (GPU sort in the reference
+    quicksort's own order of equal values). Its verdicts must be the reference's and
+    its output the reference server's, line for line (tests 21, 22, 29 index columns
+    with equal values)."""
     mine = run_suite(os.path.join(REFBIN, "server_mq_ix"), str(tmp_path / "mqix"))
     ref = run_suite(os.path.join(REFBIN, "server_ref"), str(tmp_path / "ref"))
     failed = sorted(t for t, (_, v) in mine.items() if v == "fail")
     assert set(failed) <= {25}, f"server_mq_ix failed {failed}"
-    order_only = []
-    for t in TESTS:
-        if t in REF_FAILS or _ws(mine[t][0]) == _ws(ref[t][0]):
-            continue
-        assert sorted(_ws(mine[t][0]), key=_sortkey) == sorted(_ws(ref[t][0]), key=_sortkey), t
-        order_only.append(t)
-    print(f"tests whose output differs from the reference only in tie order: {order_only}")
+    differ = [t for t in TESTS if t not in REF_FAILS and _ws(mine[t][0]) != _ws(ref[t][0])]
+    assert not differ, f"server_mq_ix output differs from the reference server on tests {differ}"
 
 
 @needs_bins
@@ -231,20 +227,15 @@ RESIDENCY_DSL = "residency_noshutdown.dsl"
 
 @pytest.mark.gpu
 @needs_bins
-@pytest.mark.parametrize("binary", ["server_mq"])
+@pytest.mark.parametrize("binary", ["server_mq", "server_mq_ix"])
 @pytest.mark.timeout(300)
 def test_load_index_query_same_session(tmp_path, binary):
     """load_db keeps the columns resident in HBM, then the index
     build rewrites the other columns in place (reference build_index in server_mq,
     libmq's in server_mq_ix), then select/fetch/sum on them in the same session.
-    The output must be the reference server's, line for line (server_mq_ix: the
-    clustered tie order is libmq's, so there it is compared as sorted lines)."""
+    The output must be the reference server's, line for line."""
     if not _have(binary):
         pytest.skip(f"{binary} not built")
     mine = run_dsl_files(os.path.join(REFBIN, binary), str(tmp_path / "mq"), [RESIDENCY_DSL])
     ref = run_dsl_files(os.path.join(REFBIN, "server_ref"), str(tmp_path / "ref"), [RESIDENCY_DSL])
-    a, b = _ws(mine[RESIDENCY_DSL]), _ws(ref[RESIDENCY_DSL])
-    if binary == "server_mq":
-        assert a == b
-    else:
-        assert sorted(a, key=_sortkey) == sorted(b, key=_sortkey)
+    assert _ws(mine[RESIDENCY_DSL]) == _ws(ref[RESIDENCY_DSL])

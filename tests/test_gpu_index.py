@@ -1,7 +1,9 @@
-"""The index build on gfx950 (mq_index_build / mq_gather_u64 / mq_histogram,
-csrc/mq_index.hip, and the build_index drop-in in mq_query.c) — bit-exact against
-the oracle's stable restatement, and against the reference's own build_index
-goldens in their tie-order-free form (tests/test_oracle_index.py).
+"""The index build on gfx950 (mq_index_build / mq_index_build_lomuto /
+mq_index_build_ref / mq_gather_u64 / mq_histogram, csrc/mq_index.hip, and the
+build_index drop-in in mq_query.c) — bit-exact against the oracle: the stable radix
+sort against the stable restatement, the Lomuto order against the restatement of
+the reference quicksort (pinned to the reference's own quicksort symbol), and the
+drop-in against the reference's own build_index goldens, equal values included.
 """
 import ctypes as C
 
@@ -11,7 +13,7 @@ import pytest
 from devbuf import Dev
 from indexcases import cases, model
 from refapi import mq
-from test_oracle_index import check_index_result
+from test_oracle_index import _lomuto_inputs, check_index_result
 
 pytestmark = pytest.mark.gpu
 CASES = {name: (cols, spec) for name, cols, spec in cases()}
@@ -42,6 +44,52 @@ def test_index_build_vs_oracle(lib, refcpu, n, lo, hi):
     v, p = gpu_index(lib, col)
     wv, wp = refcpu.index_build(col)
     assert np.array_equal(v, wv) and np.array_equal(p, wp)
+
+
+def gpu_lomuto(L, col: np.ndarray):
+    n = len(col)
+    d = Dev.of(col.astype(np.int32)) if n else Dev(4)
+    v, p = Dev(max(n, 1) * 4), Dev(max(n, 1) * 8)
+    mq.check(L.mq_index_build_lomuto(d.ptr, n, v.ptr, p.ptr, None), "mq_index_build_lomuto")
+    return v.get(np.int32, n), p.get(np.uint64, n)
+
+
+def _more_lomuto_inputs():
+    rng = np.random.default_rng(5)
+    # one value >= the pivot followed by a long run below it: a 4999-step swap chain
+    # (pointer doubling past kChainCap)
+    yield "long_chain", np.concatenate([[10**6], np.arange(1, 5000), [10**6 - 1]]).astype(np.int32)
+    yield "chains_mixed", np.concatenate([rng.integers(900, 1000, 40), rng.integers(0, 100, 3000),
+                                          [500]]).astype(np.int32)
+    yield "dups_200k", rng.integers(0, 1000, 200_000).astype(np.int32)
+    yield "distinctish_300k", rng.integers(-2**31, 2**31 - 1, 300_000, dtype=np.int64).astype(np.int32)
+    yield "few_values_100k", rng.integers(0, 3, 100_000).astype(np.int32)
+    yield "runs_sorted_blocks", np.repeat(rng.permutation(2000), 20).astype(np.int32)
+
+
+@pytest.mark.parametrize("name,col", list(_lomuto_inputs()) + list(_more_lomuto_inputs()))
+def test_index_build_lomuto_vs_oracle(lib, refcpu, name, col):
+    """The reference quicksort's order (index.c:25-46), equal values included."""
+    v, p = gpu_lomuto(lib, col)
+    wv, wp = refcpu.index_build_lomuto(col)
+    assert np.array_equal(v, wv), name
+    assert np.array_equal(p, wp), name
+
+
+def test_index_build_ref_policy(lib, refcpu):
+    """distinct values -> the radix result (one order exists); ties -> the Lomuto order
+    up to exact_max rows, ascending row order beyond it."""
+    rng = np.random.default_rng(8)
+    for col, ties in ((rng.permutation(50_000).astype(np.int32), False),
+                      (rng.integers(0, 500, 50_000).astype(np.int32), True)):
+        n = len(col)
+        d, v, p = Dev.of(col), Dev(n * 4), Dev(n * 8)
+        for exact_max, want_exact in ((1 << 40, 1), (1000, 0 if ties else 1)):
+            ex = C.c_int(-1)
+            mq.check(lib.mq_index_build_ref(d.ptr, n, v.ptr, p.ptr, exact_max, C.byref(ex), None))
+            assert ex.value == want_exact
+            wv, wp = (refcpu.index_build_lomuto(col) if want_exact else refcpu.index_build(col))
+            assert np.array_equal(v.get(np.int32, n), wv) and np.array_equal(p.get(np.uint64, n), wp)
 
 
 def test_gather_and_histogram_vs_oracle(lib, refcpu):
@@ -106,9 +154,9 @@ def test_build_index_dropin(lib, refcpu, name):
             got[f"hist{j}_values"] = np.array(h.values[:], dtype=np.int64)
             got[f"hist{j}_counts"] = np.array(h.counts[:], dtype=np.uint64)
     want = model(refcpu, cols, spec)
-    for k, v in want.items():  # bit-exact vs the stable restatement
+    for k, v in want.items():  # bit-exact vs the quicksort restatement
         assert np.array_equal(np.asarray(got[k]), np.asarray(v)), (name, k)
-    check_index_result(refcpu, name, got)  # and vs the reference, tie order aside
+    check_index_result(refcpu, name, got)  # and vs the reference's own build, exactly
     # the index and the reordered columns are resident: a sorted-index select and a
     # select on a reordered column agree with the host arrays
     st = mq.Status(0, None)

@@ -1,12 +1,8 @@
-"""Pin the index-build restatement (oracle/refcpu.c rc_index_build / rc_histogram,
-composed as build_index in tests/indexcases.py model()) against the reference's own
-build_index (tests/golden/index_goldens.json, from oracle/_ref/libdbm.so).
-
-The reference's quicksort decides the order of equal values by itself, so the
-comparison is on canon(): exact sorted values, histogram and, within each run of
-equal indexed values, the sorted positions / reordered rows. Where the reference's
-raw positions are already canonical (distinct values), the restatement's raw output
-must equal them too. CPU only.
+"""Pin the index-build restatement (oracle/refcpu.c rc_index_build_lomuto /
+rc_histogram, composed as build_index in tests/indexcases.py model()) against the
+reference's own build_index (tests/golden/index_goldens.json, from
+oracle/_ref/libdbm.so) and its own quicksort symbol: exact, equal values included.
+CPU only.
 """
 import json
 import os
@@ -14,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from indexcases import canon, cases, csv_text, model
+from indexcases import cases, csv_text, model
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = json.load(open(os.path.join(HERE, "golden", "index_goldens.json")))
@@ -38,13 +34,9 @@ def check_index_result(refcpu, name, result):
     """result: a build_index outcome (cols + ix*/hist* arrays) for case `name`."""
     g = GOLD[name]
     spec = [tuple(x) for x in g["spec"]]
-    got = digest(refcpu, canon(result, spec), spec)
+    got = digest(refcpu, result, spec)
     for k, v in got.items():
         assert v == g[k], (name, k)
-    raw = digest(refcpu, result, spec)
-    for j, exact in g["exact_positions"].items():
-        if exact:
-            assert raw[f"ix{j}_positions"] == g[f"ix{j}_positions"], (name, j)
 
 
 def test_index_inputs_match_goldens(refcpu):
@@ -66,3 +58,32 @@ def test_index_restatement_is_stable(refcpu):
     v, p = refcpu.index_build(col)
     assert np.array_equal(v, np.sort(col, kind="stable"))
     assert np.array_equal(p, np.argsort(col, kind="stable").astype(np.uint64))
+
+
+def _lomuto_inputs():
+    rng = np.random.default_rng(11)
+    yield "empty", np.zeros(0, np.int32)
+    yield "one", np.array([5], np.int32)
+    yield "all_equal", np.full(700, 3, np.int32)
+    yield "sorted", np.arange(900, dtype=np.int32)
+    yield "reverse", np.arange(900, 0, -1).astype(np.int32)
+    yield "two_values", rng.integers(0, 2, 1500).astype(np.int32)
+    yield "few_values", rng.integers(-3, 4, 2000).astype(np.int32)
+    yield "dups", rng.integers(0, 200, 3000).astype(np.int32)
+    yield "distinct", rng.permutation(3000).astype(np.int32)
+    yield "extremes", rng.choice(np.array([-2**31, 2**31 - 1, 0, -1, 1], np.int32), 1200)
+    yield "sorted_dups", np.sort(rng.integers(0, 50, 1000)).astype(np.int32)
+    yield "organ_pipe", np.concatenate([np.arange(500), np.arange(500, 0, -1)]).astype(np.int32)
+
+
+@pytest.mark.parametrize("name,col", list(_lomuto_inputs()))
+def test_lomuto_restatement_equals_reference_quicksort(refcpu, name, col):
+    """rc_index_build_lomuto against the reference's own quicksort symbol (libdbm.so):
+    values AND positions identical, equal values included."""
+    import refload
+    if not refload.have():
+        pytest.skip("oracle/_ref/libdbm.so not built (no /root/reference)")
+    rv, rp = refload.quicksort(col)
+    v, p = refcpu.index_build_lomuto(col)
+    assert np.array_equal(v, rv), name
+    assert np.array_equal(p, rp), name
