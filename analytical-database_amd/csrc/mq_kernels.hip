@@ -1376,7 +1376,9 @@ __global__ __launch_bounds__(kTPB) void k_gen_join(int* __restrict__ out, uint64
     const uint64_t mask = 2 * n - 1;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
         if (kind == 0) out[i] = (int)mix31((uint32_t)i);
-        else out[i] = (int)mix31((uint32_t)(sm64((7ull << 40) | i) & mask));
+        else if (kind == 1) out[i] = (int)mix31((uint32_t)(sm64((7ull << 40) | i) & mask));
+        else if (kind == 2) out[i] = (int)mix31((uint32_t)(i % (n / 2 ? n / 2 : 1)));  // every key twice
+        else out[i] = (int)mix31((uint32_t)(sm64((7ull << 40) | i) & (n - 1)));       // about half hit
     }
 }
 
@@ -1964,7 +1966,8 @@ int mq_gen_join_keys(int32_t* d_out, uint64_t n, int kind, void* stream) {
     int rc = ensure_ready(&s);
     if (rc) return rc;
     if (n == 0) return MQ_OK;
-    if (!d_out || kind < 0 || kind > 1) return set_err(MQ_EINVAL, "mq_gen_join_keys: bad argument");
+    if (!d_out || kind < 0 || kind > 3 || (kind == 3 && (n & (n - 1))))
+        return set_err(MQ_EINVAL, "mq_gen_join_keys: bad argument");
     hipLaunchKernelGGL(k_gen_join, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream,
                        d_out, n, kind);
     LAUNCHCHK("k_gen_join");

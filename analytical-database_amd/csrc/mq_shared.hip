@@ -77,14 +77,31 @@ __device__ __forceinline__ unsigned long long bal(int x, uint32_t lo, uint32_t w
     return __ballot(((uint32_t)x - lo) <= wm1);
 }
 
-// counts[q * nwc + wc], wc = block * 4 + wave
-template <bool VEC>
+// counts[q * nwc + wc], wc = block * 4 + wave. PAIRS: also list every (query, row)
+// match into the wave's pair slice (tile by tile; inside a tile query by query, rows
+// ascending: per query, row order), the single pass of k_ssp_count / k_ssp_scatter
+// below.
+__device__ __forceinline__ void list_pairs(uint32_t* __restrict__ list, uint32_t at, uint32_t j, uint32_t r0,
+                                           unsigned long long m0, unsigned long long m1, unsigned long long m2,
+                                           unsigned long long m3, int lane, unsigned long long ltmask) {
+    const unsigned long long bit = 1ull << lane;
+    at += (uint32_t)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) + __popcll(m2 & ltmask) + __popcll(m3 & ltmask));
+    const uint32_t tag = j << 24;
+    if (m0 & bit) list[at++] = tag | (r0 + 0);
+    if (m1 & bit) list[at++] = tag | (r0 + 1);
+    if (m2 & bit) list[at++] = tag | (r0 + 2);
+    if (m3 & bit) list[at++] = tag | (r0 + 3);
+}
+
+template <bool VEC, bool PAIRS>
 __global__ __launch_bounds__(kTPB) void k_ss_count(const int* __restrict__ col, uint64_t n,
                                                    uint64_t rpb, const Pred* __restrict__ preds,
                                                    int q, uint32_t* __restrict__ counts,
-                                                   uint64_t nwc) {
+                                                   uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
+                                                   uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
     __shared__ uint32_t wcnt[kWaves][kMaxQ];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (int i = tid; i < q; i += kTPB) {
 #pragma unroll
         for (int w = 0; w < kWaves; w++) wcnt[w][i] = 0;
@@ -92,34 +109,48 @@ __global__ __launch_bounds__(kTPB) void k_ss_count(const int* __restrict__ col, 
     __syncthreads();
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
+    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    uint32_t* list = PAIRS ? pairs + wc * cap : nullptr;
+    uint32_t run = 0;
     for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
         int4 v[kSsUnroll];
 #pragma unroll
         for (int u = 0; u < kSsUnroll; u++)
             v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
-        if (t + kWaveTile * kSsUnroll <= e) {  // full: ballots straight off the compares
-            for (int j = 0; j < q; j++) {
-                const Pred p = preds[j];  // uniform index: scalar-cache load
-                uint32_t c = 0;
+        const bool full = t + kWaveTile * kSsUnroll <= e;
+        for (int j = 0; j < q; j++) {
+            const Pred p = preds[j];  // uniform index: scalar-cache load
+            uint32_t c = 0;
 #pragma unroll
-                for (int u = 0; u < kSsUnroll; u++)
-                    c += (uint32_t)(__popcll(bal(v[u].x, p.lo, p.wm1)) + __popcll(bal(v[u].y, p.lo, p.wm1)) +
-                                    __popcll(bal(v[u].z, p.lo, p.wm1)) + __popcll(bal(v[u].w, p.lo, p.wm1)));
-                if (lane == 0) wcnt[wave][j] += c;  // this wave only: no atomics
-            }
-        } else {
-            for (int j = 0; j < q; j++) {
-                const Pred p = preds[j];
-                uint32_t c = 0;
-#pragma unroll
-                for (int u = 0; u < kSsUnroll; u++) {
-                    const uint32_t b = match4(v[u], p, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
-                    c += (uint32_t)(__popcll(__ballot(b & 1u)) + __popcll(__ballot(b & 2u)) +
-                                    __popcll(__ballot(b & 4u)) + __popcll(__ballot(b & 8u)));
+            for (int u = 0; u < kSsUnroll; u++) {
+                const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
+                unsigned long long m0, m1, m2, m3;
+                if (full) {  // ballots straight off the compares
+                    m0 = bal(v[u].x, p.lo, p.wm1);
+                    m1 = bal(v[u].y, p.lo, p.wm1);
+                    m2 = bal(v[u].z, p.lo, p.wm1);
+                    m3 = bal(v[u].w, p.lo, p.wm1);
+                } else {
+                    const uint32_t b = match4(v[u], p, row, e);
+                    m0 = __ballot(b & 1u);
+                    m1 = __ballot(b & 2u);
+                    m2 = __ballot(b & 4u);
+                    m3 = __ballot(b & 8u);
                 }
-                if (lane == 0) wcnt[wave][j] += c;
+                const uint32_t tc = (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
+                if (PAIRS && tc) {
+                    if ((uint64_t)run + tc <= cap)
+                        list_pairs(list, run, (uint32_t)j, (uint32_t)(row - s), m0, m1, m2, m3, lane, ltmask);
+                    run += tc;
+                }
+                c += tc;
             }
+            if (lane == 0) wcnt[wave][j] += c;  // this wave only: no atomics
         }
+    }
+    if (PAIRS && lane == 0) {
+        npairs[wc] = run;
+        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
     }
     __syncthreads();
     for (int i = tid; i < q; i += kTPB) {
@@ -218,6 +249,7 @@ constexpr int kEiMinQ = 12;  // measured crossover (count + write, 1e9 rows): Q=
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
+constexpr int kQlCap = 2048;  // per-EI query-list entries staged in LDS by k_ssp_count
 
 struct EiMeta {
     int m;          // number of bounds
@@ -441,7 +473,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
 // of its wave-chunk; a wave-chunk with more pairs (dense queries) flags an overflow
 // and the write falls back to the column pass (k_ssi_write) on the same counts.
 // ---------------------------------------------------------------------------
-template <bool VEC>
+template <bool VEC, int DBG = 0>
 __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
@@ -450,11 +482,19 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     __shared__ int32_t s_b[kEiMax];
     __shared__ uint32_t s_qoff[kEiMax];
     __shared__ uint32_t hist[kWaves][kEiMax];
+    __shared__ uint16_t s_ql[kQlCap];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     stage_buckets(T.bucket, s_bkt, tid);
     for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
     for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
     for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    // the per-EI query lists: in LDS when they fit (the usual case), else read from HBM
+    const uint32_t nql = s_qoff[M.m + 1];
+    const bool ql_lds = nql <= (uint32_t)kQlCap;
+    if (ql_lds)
+        for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
     __syncthreads();
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
@@ -483,20 +523,24 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
                 }
                 np += qn[k];
             }
-            uint32_t incl = np;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
+            if (DBG == 2) continue;
+            // exclusive prefix of np over the lanes from ballots of np >= t (np is
+            // small: a row is covered by a few queries), no cross-lane shuffle chain
+            uint32_t pre = 0, tot = 0;
+            for (uint32_t t = 1;; t++) {
+                const unsigned long long b = __ballot(np >= t);
+                if (!b) break;
+                pre += (uint32_t)__popcll(b & ltmask);
+                tot += (uint32_t)__popcll(b);
             }
-            const uint32_t tot = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
             if (tot == 0) continue;
-            if ((uint64_t)run + tot <= cap) {
-                uint32_t at = run + incl - np;
+            if (DBG == 0 && (uint64_t)run + tot <= cap && np) {
+                uint32_t at = run + pre;
                 const uint32_t r0 = (uint32_t)(row - s);
 #pragma unroll
                 for (int k = 0; k < 4; k++)
-                    for (uint32_t i = 0; i < qn[k]; i++) list[at++] = ((uint32_t)T.qlist[qa[k] + i] << 24) | (r0 + k);
+                    for (uint32_t i = 0; i < qn[k]; i++)
+                        list[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
             }
             run += tot;  // past cap: still counted, the slice is incomplete
         }
@@ -522,6 +566,145 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
         if (lane >= o) incl += y;
     }
     uint32_t acc = incl - loc;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) {
+            const uint32_t c = h[j];
+            h[j] = acc;
+            acc += c;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < q; i += 64) {
+        const uint32_t ab = T.qab[i];
+        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
+    }
+}
+
+// The same with each lane owning 16 consecutive rows of a 1024-row wave-group (4
+// dwordx4 loads per lane), so one prefix over the lanes orders the group's pairs by
+// row, and a lane's pairs (up to kLcRegs, one query per row) are written by a loop
+// over the pair index: a handful of store instructions per 1024 rows instead of one
+// per element slot and wave-tile. Lanes with more pairs, or rows under overlapping
+// queries, write theirs row by row into their own range after that.
+constexpr int kLcRegs = 8;
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_ssp_count_lc(const int* __restrict__ col, uint64_t n, uint64_t rpb,
+                                                       EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
+                                                       uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
+                                                       uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
+    __shared__ uint32_t s_bkt[kBuckets];
+    __shared__ int32_t s_b[kEiMax];
+    __shared__ uint32_t s_qoff[kEiMax];
+    __shared__ uint32_t hist[kWaves][kEiMax];
+    __shared__ uint16_t s_ql[kQlCap];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    stage_buckets(T.bucket, s_bkt, tid);
+    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
+    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
+    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t nql = s_qoff[M.m + 1];
+    const bool ql_lds = nql <= (uint32_t)kQlCap;
+    if (ql_lds)
+        for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
+    __syncthreads();
+    uint64_t s, e;
+    wave_chunk(n, rpb, wave, &s, &e);
+    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    uint32_t* list = pairs + wc * cap;
+    uint32_t run = 0;
+    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
+        const uint64_t r0 = t + (uint64_t)lane * 16;  // this lane's 16 rows
+        int x[16];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int4 v = load_row4<VEC>(col, r0 + 4 * u, e);
+            x[4 * u] = v.x;
+            x[4 * u + 1] = v.y;
+            x[4 * u + 2] = v.z;
+            x[4 * u + 3] = v.w;
+        }
+        uint32_t ei[16], np = 0;
+        bool multi = false;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            ei[k] = 0xFFFFu;
+            if (r0 + k < e) {
+                const int eidx = ei_of(x[k], M, s_bkt, s_b);
+                const uint32_t a = s_qoff[eidx], c = s_qoff[eidx + 1] - a;
+                if (c) {
+                    atomicAdd(&hist[wave][eidx], 1u);
+                    ei[k] = (uint32_t)eidx;
+                    np += c;
+                    multi |= c > 1;
+                }
+            }
+        }
+        uint32_t incl = np;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t tot = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+        if (tot == 0) continue;
+        if ((uint64_t)run + tot <= cap) {
+            const uint32_t at = run + incl - np;
+            const uint32_t rb = (uint32_t)(r0 - s);
+            const bool fast = !multi && np <= (uint32_t)kLcRegs;
+            uint32_t p[kLcRegs];
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (fast && ei[k] != 0xFFFFu) {
+                    const uint32_t qa = s_qoff[ei[k]];
+                    const uint32_t v = ((uint32_t)(ql_lds ? s_ql[qa] : T.qlist[qa]) << 24) | (rb + k);
+#pragma unroll
+                    for (int r = 0; r < kLcRegs; r++)
+                        if (r == (int)m) p[r] = v;
+                    m++;
+                }
+            }
+            // store loop over the pair index: lane l writes its r-th pair at at + r
+#pragma unroll
+            for (int r = 0; r < kLcRegs; r++) {
+                if (!__ballot(fast && (uint32_t)r < m)) break;
+                if (fast && (uint32_t)r < m) list[at + r] = p[r];
+            }
+            if (!fast) {  // many pairs, or a row under several queries
+                uint32_t a2 = at;
+                for (int k = 0; k < 16; k++) {
+                    if (ei[k] == 0xFFFFu) continue;
+                    const uint32_t qa = s_qoff[ei[k]], c = s_qoff[ei[k] + 1] - qa;
+                    for (uint32_t i = 0; i < c; i++)
+                        list[a2++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | (rb + k);
+                }
+            }
+        }
+        run += tot;
+    }
+    if (lane == 0) {
+        npairs[wc] = run;
+        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* h = hist[wave];
+    const int ne = M.m + 2;
+    const int per = (ne + 63) / 64;
+    uint32_t loc = 0;
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) loc += h[j];
+    }
+    uint32_t inc2 = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc2, o, 64);
+        if (lane >= o) inc2 += y;
+    }
+    uint32_t acc = inc2 - loc;
     __builtin_amdgcn_wave_barrier();
     for (int i = 0; i < per; i++) {
         const int j = lane * per + i;
@@ -643,7 +826,7 @@ __global__ void k_ss_totals(const uint32_t* __restrict__ counts,
 }
 
 struct SsLayout {
-    size_t preds, outs, slot, counts, offs, scratch, ei, total;
+    size_t preds, outs, slot, counts, offs, scratch, ei, flag, npairs, pairs, total;
 };
 
 // EI tables in the workspace: bounds, bucket table, qoff, qab, then qlist
@@ -670,9 +853,17 @@ SsLayout ss_layout(uint64_t nwc, int q) {
     at += al((size_t)scan_u32_scratch_elems((uint64_t)q * nwc) * sizeof(unsigned long long));
     L.ei = at;
     at += al(kEiBytes);
+    L.flag = at;
+    at += 256;
+    L.npairs = at;
+    at += al(nwc * sizeof(uint32_t));
+    L.pairs = at;  // pair slices (single pass), when the workspace extends this far
     L.total = at;
     return L;
 }
+
+// Pair-slice capacity: one u32 per row of the wave-chunk.
+uint64_t pair_cap(uint64_t rpb) { return rpb / kWaves; }
 
 uint64_t max_wave_chunks(const DevState* s) {
     return (uint64_t)s->cus * 8 * kWaves;  // <= 8 resident blocks per CU
@@ -692,6 +883,7 @@ struct SsState {
     bool ei;    // elementary-interval kernels (qk >= kEiMinQ)
     EiMeta meta;
     int32_t base;  // first row number of this (row-shard) column
+    bool pairs;    // the count pass listed the pairs (single pass)
 };
 
 // Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
@@ -805,6 +997,10 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     if (n) geometry(s, n, fn, &g, &rpb, kGranule);
     const uint64_t nwc = (uint64_t)g * kWaves;
     const SsLayout L = ss_layout(nwc, qk > 0 ? qk : 1);
+    const uint64_t cap = pair_cap(rpb);
+    const bool single = n && getenv("MQ_SS_TWOPASS") == nullptr &&
+                        ws_bytes >= L.pairs + (size_t)nwc * cap * sizeof(uint32_t) && cap < (1ull << 24);
+    HIPCHK(hipMemsetAsync(w + L.flag, 0, 4, st));
     HIPCHK(hipMemcpyAsync(w + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(w + L.slot, hslot, sizeof(int) * q, hipMemcpyHostToDevice, st));
     EiMeta meta{0, 0, 0, 0};
@@ -814,17 +1010,47 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
     unsigned long long* offs = reinterpret_cast<unsigned long long*>(w + L.offs);
     if (qk > 0) {
-        if (ei) {
+        if (single && ei) {
+            const EiTables T = ei_tables(w + L.ei);
+            uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
+            uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
+            unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
+            const char* dbg = getenv("MQ_SSP_DEBUG");  // A/B of the pair listing's parts (timing only)
+            const char* lc = getenv("MQ_SSP_LC");
+            if (lc && lc[0] == '1' && vec)
+                hipLaunchKernelGGL(k_ssp_count_lc<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of);
+            else if (dbg && vec && atoi(dbg) == 1)
+                hipLaunchKernelGGL((k_ssp_count<true, 1>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of);
+            else if (dbg && vec && atoi(dbg) == 2)
+                hipLaunchKernelGGL((k_ssp_count<true, 2>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of);
+            else if (vec)
+                hipLaunchKernelGGL(k_ssp_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of);
+            else
+                hipLaunchKernelGGL(k_ssp_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of);
+            LAUNCHCHK("k_ssp_count");
+        } else if (ei) {
             const EiTables T = ei_tables(w + L.ei);
             if (vec)
                 hipLaunchKernelGGL(k_ssi_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
             else
                 hipLaunchKernelGGL(k_ssi_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
             LAUNCHCHK("k_ssi_count");
-        } else if (vec) {
-            hipLaunchKernelGGL(k_ss_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc);
         } else {
-            hipLaunchKernelGGL(k_ss_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc);
+            uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
+            uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
+            unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
+            if (single) {
+                if (vec) hipLaunchKernelGGL((k_ss_count<true, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
+                else hipLaunchKernelGGL((k_ss_count<false, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
+            } else {
+                if (vec) hipLaunchKernelGGL((k_ss_count<true, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
+                else hipLaunchKernelGGL((k_ss_count<false, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
+            }
         }
         LAUNCHCHK("k_ss_count");
         if ((rc = scan_u32_exclusive(counts, offs, (uint64_t)qk * nwc,
@@ -834,7 +1060,7 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
                        reinterpret_cast<const int*>(w + L.slot), d_totals, q);
     LAUNCHCHK("k_ss_totals");
-    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta, row_base};
+    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta, row_base, single && qk > 0};
     return MQ_OK;
 }
 
@@ -854,6 +1080,19 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
     int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
+    if (S.pairs) {
+        unsigned int of = 0;  // a slice overflowed: the pairs are incomplete, use the column pass
+        HIPCHK(hipMemcpyAsync(&of, w + L.flag, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (!of) {
+            hipLaunchKernelGGL(k_ssp_scatter, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+                               reinterpret_cast<const uint32_t*>(w + L.pairs), pair_cap(S.rpb),
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
+                               S.base);
+            LAUNCHCHK("k_ssp_scatter");
+            return MQ_OK;
+        }
+    }
     if (S.ei) {
         const EiTables T = ei_tables(w + L.ei);
         if (aligned16(S.col))
@@ -883,7 +1122,10 @@ size_t mq_shared_select_workspace_bytes(uint64_t n, int q) {
     if (ensure_ready(&s)) return 0;
     if (q < 1) q = 1;
     if (q > kMaxQ) q = kMaxQ;
-    const size_t a = ss_layout(max_wave_chunks(s), q).total;
+    const uint64_t nwc = max_wave_chunks(s);
+    // + the pair slices of the single pass: one u32 per row, each wave-chunk rounded
+    // up to whole granules
+    const size_t a = ss_layout(nwc, q).total + (size_t)(n + nwc * kGranule) * sizeof(uint32_t);
     const size_t b = mq_scan_workspace_bytes(n);  // the Q = 1 path of mq_shared_select
     return a > b ? a : b;
 }
@@ -929,9 +1171,13 @@ int mq_shared_select(const int32_t* d_col, uint64_t n, const int32_t* h_lows,
     if (q < 0 || q > kMaxQ || (q > 0 && (!h_lows || !h_highs || !d_pos_out || !d_counts)))
         return set_err(MQ_EINVAL, "mq_shared_select: bad argument (q = %d, at most %d)", q, kMaxQ);
     if (q == 0) return MQ_OK;
-    if (q == 1)  // one query: the ordered-compaction path reads the column once
-        return mq_select_positions(d_col, nullptr, n, 1, h_lows[0], 1, h_highs[0], d_pos_out[0],
-                                   d_counts, d_ws, ws_bytes, stream);
+    if (q <= 3) {  // a few queries into capacity-n outputs: one ordered compaction each
+        for (int j = 0; j < q; j++)
+            if ((rc = mq_select_positions(d_col, nullptr, n, 1, h_lows[j], 1, h_highs[j], d_pos_out[j],
+                                          d_counts + j, d_ws, ws_bytes, stream)))
+                return rc;
+        return MQ_OK;
+    }
     SsState S;
     hipStream_t st = (hipStream_t)stream;
     if ((rc = ss_count(d_col, n, 0, h_lows, h_highs, q, d_counts, d_ws, ws_bytes, st, &S))) return rc;

@@ -488,6 +488,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
         del pos, col1, vals
     out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
+    out["config5_many_to_many"] = join_dup_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
     out["load_csv_config3_table"] = load_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["index_build"] = index_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
@@ -676,6 +677,68 @@ def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True
         tr = time.perf_counter() - t0
         res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1,
                                      "kind": "reference"}
+    return res
+
+
+def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True) -> dict:
+    """Config 5, many-to-many: every build key twice (rows i and
+    i + n/2), about half the probes hit, two matches each (M ~ n): the duplicate-key
+    build path (stable radix sort into key runs). Parity: M and the pair FNV at 2^22
+    against the reference's own hash_join (tests/golden/make_join_dup_goldens.py);
+    timing at 2^logn (build + probe + write, as join_leg)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu  # checker only (pair hash)
+    sp = mq.stream_of(stream)
+
+    def run(n, keep):
+        with torch.cuda.stream(stream):
+            a = torch.empty(n, dtype=torch.int32, device=dev)
+            b = torch.empty(n, dtype=torch.int32, device=dev)
+            p = torch.empty(n, dtype=torch.int32, device=dev)
+            mq.check(lib.mq_gen_join_keys(a.data_ptr(), n, 2, sp))
+            mq.check(lib.mq_gen_join_keys(b.data_ptr(), n, 3, sp))
+            mq.check(lib.mq_gen_iota(p.data_ptr(), n, sp))
+            times, m, o1, o2 = [], 0, None, None
+            for rep in range(4 if not keep else 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                h = C.c_void_p()
+                mq.check(lib.mq_join_build(a.data_ptr(), p.data_ptr(), n, C.byref(h), sp), "join_build")
+                mm = C.c_uint64()
+                mq.check(lib.mq_join_probe(h, b.data_ptr(), n, C.byref(mm), sp), "join_probe")
+                m = mm.value
+                if o1 is None:
+                    o1 = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+                    o2 = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+                mq.check(lib.mq_join_write(h, p.data_ptr(), o1.data_ptr(), o2.data_ptr(), sp))
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+                mq.check(lib.mq_join_free(h))
+            out = (m, statistics.median(times[1:]) if len(times) > 1 else times[0])
+            if keep:
+                out += (refcpu.fnv1a64_pairs(o1[:m].cpu().numpy(), o2[:m].cpu().numpy()),)
+            del a, b, p, o1, o2
+            return out
+
+    want = [r for r in gold.get("join_dup", []) if r["n"] == 1 << 22]
+    pm, _, pf = run(1 << 22, True)
+    ok = bool(want) and (pm, f"{pf:016x}") == (want[0]["m"], want[0]["pairs_fnv1a64"])
+    n = 1 << logn
+    m, t = run(n, False)
+    res = {"n_build": n, "n_probe": n, "m": m, "ms": 1e3 * t, "rows_per_s": 2 * n / t,
+           "algorithmic_bytes": 16 * n + 8 * m, "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9,
+           "parity_2e22": ok, "note": "wall time incl. the unique-key attempt, its restart on the "
+                                      "duplicate flag, and 2 host syncs"}
+    if cpu and refcpu.have_reference():
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from refapi import Api
+        api = Api(refcpu.reference())
+        k = 1 << 20
+        ka, kb, kp = refcpu.gen_join(k, "build_dup"), refcpu.gen_join(k, "probe_dup"), refcpu.gen_join(k, "iota")
+        t0 = time.perf_counter()
+        api.join(ka, kp, kb, kp, "hash")
+        tr = time.perf_counter() - t0
+        res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1, "kind": "reference"}
     return res
 
 

@@ -80,7 +80,9 @@ void mq_scan_geometry(uint64_t n, uint32_t* blocks, uint64_t* rows_per_block);
 /* ---- synthetic data (bench/tests; SURVEY.md §8(c) generator) ---- */
 /* out[i] = (int32)(sm64(seed*0x100000001B3 + i) % modulus) */
 int mq_gen_uniform(int32_t* d_out, uint64_t n, uint64_t seed, uint64_t modulus, void* stream);
-/* hash-join keys of SURVEY §8(c) config 5 (kind 0 = build mix31(i), 1 = probe) and iota */
+/* hash-join keys of SURVEY §8(c) config 5 (kind 0 = build mix31(i), 1 = probe) and its
+ * many-to-many variant (2 = build mix31(i mod n/2): every key twice; 3 = probe
+ * mix31(sm64((7<<40)|j) mod n), n a power of two: about half hit), and iota */
 int mq_gen_join_keys(int32_t* d_out, uint64_t n, int kind, void* stream);
 int mq_gen_iota(int32_t* d_out, uint64_t n, void* stream);
 

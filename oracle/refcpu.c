@@ -85,6 +85,21 @@ void rc_gen_join_probe(int32_t* out, size_t n) {
         out[j] = (int32_t)rc_mix31((uint32_t)(rc_sm64((7ull << 40) | (uint64_t)j) & mask));
 }
 
+/* config 5, many-to-many variant: every build key twice,
+ * a[i] = mix31(i mod n/2) (rows i and i + n/2, spread over the build order), probe
+ * keys mix31(sm64((7 << 40) | j) mod n): about half the probes hit a key, each with
+ * two matches, so M ~ n; the reference multimap's probing stays linear. */
+void rc_gen_join_build_dup(int32_t* out, size_t n) {
+    const size_t h = n / 2 ? n / 2 : 1;
+    for (size_t i = 0; i < n; i++) out[i] = (int32_t)rc_mix31((uint32_t)(i % h));
+}
+
+void rc_gen_join_probe_dup(int32_t* out, size_t n) {
+    uint64_t mask = (uint64_t)n - 1;  /* n a power of two */
+    for (size_t j = 0; j < n; j++)
+        out[j] = (int32_t)rc_mix31((uint32_t)(rc_sm64((7ull << 40) | (uint64_t)j) & mask));
+}
+
 void rc_iota(int32_t* out, size_t n) {
     for (size_t i = 0; i < n; i++) out[i] = (int32_t)i;
 }

@@ -32,6 +32,8 @@ void rc_gen_uniform(int32_t* out, size_t n, uint64_t seed, uint64_t modulus, int
  * probe b[j]=mix31(sm64((7<<40)|j) & (2n-1)) */
 void rc_gen_join_build(int32_t* out, size_t n);
 void rc_gen_join_probe(int32_t* out, size_t n);
+void rc_gen_join_build_dup(int32_t* out, size_t n);
+void rc_gen_join_probe_dup(int32_t* out, size_t n);
 void rc_iota(int32_t* out, size_t n);
 uint64_t rc_fnv1a64(const void* p, size_t bytes);
 uint64_t rc_fnv1a64_pairs(const int32_t* a, const int32_t* b, size_t m);

@@ -40,6 +40,8 @@ def _bind(lib: C.CDLL) -> C.CDLL:
         "rc_gen_uniform": (None, [_vp, _sz, _u64, _u64, C.c_int]),
         "rc_gen_join_build": (None, [_vp, _sz]),
         "rc_gen_join_probe": (None, [_vp, _sz]),
+        "rc_gen_join_build_dup": (None, [_vp, _sz]),
+        "rc_gen_join_probe_dup": (None, [_vp, _sz]),
         "rc_iota": (None, [_vp, _sz]),
         "rc_fnv1a64": (_u64, [_vp, _sz]),
         "rc_fnv1a64_pairs": (_u64, [_vp, _vp, _sz]),
@@ -130,6 +132,7 @@ def gen_uniform(n: int, seed: int, modulus: int | None = None, nthreads: int = 8
 def gen_join(n: int, kind: str) -> np.ndarray:
     out = np.empty(n, dtype=np.int32)
     {"build": lib().rc_gen_join_build, "probe": lib().rc_gen_join_probe,
+     "build_dup": lib().rc_gen_join_build_dup, "probe_dup": lib().rc_gen_join_probe_dup,
      "iota": lib().rc_iota}[kind](_a(out), n)
     return out
 

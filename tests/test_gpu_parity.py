@@ -524,9 +524,14 @@ def _dev_join(lib, c1, p1, c2, p2):
     return o1.get(np.int32, m), o2.get(np.int32, m)
 
 
+@pytest.mark.parametrize("runs", [True, False])
 @pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
                                   "unique_partitioned", "dups_partitioned", "ragged_hits"])
-def test_hash_join_vs_oracle(lib, refcpu, case):
+def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
+    """runs: duplicate keys as sorted runs behind the windowed table of distinct keys
+    (default); MQ_JOIN_RUNS=0: the global-CAS table of run heads (the fallback)."""
+    if not runs:
+        monkeypatch.setenv("MQ_JOIN_RUNS", "0")
     rng = np.random.default_rng(hash(case) % 1000)
     if case == "unique":
         c1 = rng.permutation(200_000).astype(np.int32)
@@ -596,10 +601,10 @@ def test_hash_join_scratch_reuse_and_trim(lib, refcpu):
             lib.mq_trim()
 
 
-def _join_golden(lib, refcpu, n):
+def _join_golden(lib, refcpu, n, dup=False, keep=False):
     D = {k: Dev(n * 4) for k in ("a", "b", "p")}
-    mq.check(lib.mq_gen_join_keys(D["a"].ptr, n, 0, None))
-    mq.check(lib.mq_gen_join_keys(D["b"].ptr, n, 1, None))
+    mq.check(lib.mq_gen_join_keys(D["a"].ptr, n, 2 if dup else 0, None))
+    mq.check(lib.mq_gen_join_keys(D["b"].ptr, n, 3 if dup else 1, None))
     mq.check(lib.mq_gen_iota(D["p"].ptr, n, None))
     h = C.c_void_p()
     mq.check(lib.mq_join_build(D["a"].ptr, D["p"].ptr, n, C.byref(h), None))
@@ -609,7 +614,10 @@ def _join_golden(lib, refcpu, n):
     o1, o2 = Dev(m * 4), Dev(m * 4)
     mq.check(lib.mq_join_write(h, D["p"].ptr, o1.ptr, o2.ptr, None))
     mq.check(lib.mq_join_free(h))
-    return m, refcpu.fnv1a64_pairs(o1.get(np.int32, m), o2.get(np.int32, m))
+    g1, g2 = o1.get(np.int32, m), o2.get(np.int32, m)
+    if keep:
+        return m, refcpu.fnv1a64_pairs(g1, g2), g1, g2
+    return m, refcpu.fnv1a64_pairs(g1, g2)
 
 
 def test_hash_join_goldens(lib, refcpu, goldens):
@@ -618,6 +626,34 @@ def test_hash_join_goldens(lib, refcpu, goldens):
     for r in rows:
         m, h = _join_golden(lib, refcpu, r["n"])
         assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"]), r["n"]
+
+
+@pytest.mark.parametrize("runs", [True, False])
+def test_hash_join_dup_goldens(lib, refcpu, goldens, monkeypatch, runs):
+    """Many-to-many config 5 (every build key twice, tests/golden/make_join_dup_goldens.py):
+    the duplicate-key build path against the reference's own hash_join."""
+    if not runs:
+        monkeypatch.setenv("MQ_JOIN_RUNS", "0")
+    for r in goldens["join_dup"]:
+        m, h = _join_golden(lib, refcpu, r["n"], dup=True)
+        assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"]), r["n"]
+
+
+@pytest.mark.big
+def test_hash_join_dup_2e28_properties(lib, refcpu):
+    """2^28 x 2^28 many-to-many (beyond the reference's reach): every pair joins equal
+    keys, pairs are probe-major with build positions ascending inside a probe row (the
+    multimap's insertion order, query.c:669-681), and M equals the number of
+    (probe, build) key matches counted on the host."""
+    n = 1 << 28
+    m, _, o1, o2 = _join_golden(lib, refcpu, n, dup=True, keep=True)
+    a, b = refcpu.gen_join(n, "build_dup"), refcpu.gen_join(n, "probe_dup")
+    # the n/2 distinct build keys (mix31 is a bijection) each occur twice
+    assert m == 2 * int(np.isin(b, a[: n // 2]).sum())
+    assert np.array_equal(a[o1], b[o2])
+    assert np.all(o2[1:] >= o2[:-1])
+    same = o2[1:] == o2[:-1]
+    assert np.all(o1[1:][same] > o1[:-1][same])
 
 
 @pytest.mark.big
@@ -630,9 +666,12 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
 # ---------------------------------------------------------------------------
 # S11 shared_select (device API): Q predicates, two passes, exact-size outputs
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("twopass", [False, True])
 @pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
-                                 (3_000_017, 20)])
-def test_shared_select_vs_oracle(lib, refcpu, n, q):
+                                 (3_000_017, 20), (2_000_003, 2)])
+def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass):
+    if twopass:
+        monkeypatch.setenv("MQ_SS_TWOPASS", "1")
     rng = np.random.default_rng(n + q)
     d = rng.integers(-1000, 1000, n, dtype=np.int32)
     if n > 8:
@@ -681,16 +720,23 @@ def _shared_run(lib, d, lows, highs):
     return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
 
 
-@pytest.mark.parametrize("impl", ["ei", "ballot"])
+@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_lc"])
 @pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
                                   "mixed256", "narrow_domain"])
 def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
-    """q >= 24 runs the elementary-interval kernels (k_ssi_count / k_ssi_write,
-    MQ_SS_IMPL=ballot forces the per-query ballot kernels): sparse and dense
-    queries (dense tiles fall back to ballots inside k_ssi_write), nested and
-    identical ranges, INT32 extremes, all 256 queries, a 7-value domain."""
-    if impl == "ballot":
+    """q >= 12 runs the elementary-interval kernels (MQ_SS_IMPL=ballot forces the
+    per-query ballot kernels); by default the count pass lists (query, row) pairs and
+    k_ssp_scatter writes them (one column read), MQ_SS_TWOPASS=1 forces the column
+    pass (k_ssi_write / k_ss_write), which is also what a pair-slice overflow (the
+    dense case) falls back to. Sparse and dense queries (dense tiles fall back to
+    ballots inside k_ssi_write), nested and identical ranges, INT32 extremes, all 256
+    queries, a 7-value domain."""
+    if impl.startswith("ballot"):
         monkeypatch.setenv("MQ_SS_IMPL", "ballot")
+    if impl.endswith("twopass"):
+        monkeypatch.setenv("MQ_SS_TWOPASS", "1")
+    if impl == "ei_lc":  # lane-contiguous pair listing (k_ssp_count_lc)
+        monkeypatch.setenv("MQ_SSP_LC", "1")
     rng = np.random.default_rng(hash(case) % 2 ** 32)
     n = 1_000_003
     d = rng.integers(0, 10 ** 6, n).astype(np.int32)

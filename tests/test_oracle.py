@@ -89,6 +89,16 @@ def test_oracle_matches_join_goldens(refcpu, goldens):
         assert f"{refcpu.fnv1a64_pairs(o1, o2):016x}" == r["pairs_fnv1a64"]
 
 
+def test_oracle_matches_join_dup_goldens(refcpu, goldens):
+    """The many-to-many config-5 variant (every build key twice) against the
+    reference's own hash_join (tests/golden/make_join_dup_goldens.py)."""
+    for r in goldens["join_dup"]:
+        n = r["n"]
+        p = refcpu.gen_join(n, "iota")
+        o1, o2 = refcpu.hash_join(refcpu.gen_join(n, "build_dup"), p, refcpu.gen_join(n, "probe_dup"), p)
+        assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"]), n
+
+
 def test_oracle_reproduces_survey_join_2e24(refcpu, goldens):
     r = [x for x in goldens["join_survey"] if x["n"] == 1 << 24][0]
     n = r["n"]

@@ -15,12 +15,13 @@ from refapi import mq  # noqa: E402
 L = mq.load(os.environ['MQ_LIB']) if os.environ.get('MQ_LIB') else mq.load()
 mq.check(L.mq_init(0))
 logn = int(sys.argv[1]) if len(sys.argv) > 1 else 28
+dup = len(sys.argv) > 2 and sys.argv[2] == "dup"  # the many-to-many variant (kinds 2 / 3)
 n = 1 << logn
 a = torch.empty(n, dtype=torch.int32, device="cuda")
 b = torch.empty(n, dtype=torch.int32, device="cuda")
 p = torch.empty(n, dtype=torch.int32, device="cuda")
-mq.check(L.mq_gen_join_keys(a.data_ptr(), n, 0, 0))
-mq.check(L.mq_gen_join_keys(b.data_ptr(), n, 1, 0))
+mq.check(L.mq_gen_join_keys(a.data_ptr(), n, 2 if dup else 0, 0))
+mq.check(L.mq_gen_join_keys(b.data_ptr(), n, 3 if dup else 1, 0))
 mq.check(L.mq_gen_iota(p.data_ptr(), n, 0))
 rows = []
 o1 = o2 = None
@@ -45,4 +46,5 @@ for rep in range(5):
         rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
 med = [1e3 * statistics.median(r[i] for r in rows) for i in range(4)]
 print(json.dumps({"n": n, "m": mm.value, "ms_build": med[0], "ms_probe": med[1], "ms_write": med[2],
-                  "ms_total": med[3], "m_ok": (mm.value == 134232477) if logn == 28 else None}))
+                  "ms_total": med[3], "dup": dup,
+                  "m_ok": (mm.value == 134232477) if logn == 28 and not dup else None}))
