@@ -249,7 +249,14 @@ constexpr int kEiMinQ = 12;  // measured crossover (count + write, 1e9 rows): Q=
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
-constexpr int kQlCap = 2048;  // per-EI query-list entries staged in LDS by k_ssp_count
+constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
+// Pairs of one 1024-row wave-group held in LDS until the next group's loads are
+// issued, then written with at most 4 straight-line coalesced stores: vmcnt retires
+// loads and stores in order, so stores issued before a group's loads (or a
+// data-dependent number of them, which makes the compiler wait for all) would put
+// their round trip on every group (k_ssp_count with direct per-pair stores ran at
+// 2.3 ms, 1.2 without the stores, at Q = 150).
+constexpr uint32_t kPb = 256;
 
 struct EiMeta {
     int m;          // number of bounds
@@ -473,7 +480,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
 // of its wave-chunk; a wave-chunk with more pairs (dense queries) flags an overflow
 // and the write falls back to the column pass (k_ssi_write) on the same counts.
 // ---------------------------------------------------------------------------
-template <bool VEC, int DBG = 0>
+template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
@@ -483,6 +490,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     __shared__ uint32_t s_qoff[kEiMax];
     __shared__ uint32_t hist[kWaves][kEiMax];
     __shared__ uint16_t s_ql[kQlCap];
+    __shared__ uint32_t s_pb[kWaves][kPb];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     stage_buckets(T.bucket, s_bkt, tid);
@@ -500,12 +508,26 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     wave_chunk(n, rpb, wave, &s, &e);
     const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
     uint32_t* list = pairs + wc * cap;
+    uint32_t* pb = s_pb[wave];
     uint32_t run = 0;  // pairs of this wave-chunk so far (wave-uniform)
+    uint32_t pend = 0, pend_at = 0;  // the previous group's pairs, still in pb
     for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
         int4 v[kSsUnroll];
 #pragma unroll
         for (int u = 0; u < kSsUnroll; u++)
             v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+        {  // the previous group's pairs, behind this group's loads
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < (int)(kPb / 64); k++) {
+                const uint32_t i = (uint32_t)(k * 64 + lane);
+                if (i < pend) list[pend_at + i] = pb[i];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint32_t grp_at = run;
+        uint32_t fill = 0;   // this group's pairs in pb
+        bool direct = false; // the group outgrew pb: its later tiles store directly
 #pragma unroll
         for (int u = 0; u < kSsUnroll; u++) {
             const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
@@ -523,28 +545,60 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
                 }
                 np += qn[k];
             }
-            if (DBG == 2) continue;
-            // exclusive prefix of np over the lanes from ballots of np >= t (np is
-            // small: a row is covered by a few queries), no cross-lane shuffle chain
+            // exclusive prefix of np over the lanes from ballots (np is small: a row is
+            // covered by a few queries), no cross-lane shuffle chain: np < 8 from its
+            // three bits, else from ballots of np >= t
             uint32_t pre = 0, tot = 0;
-            for (uint32_t t = 1;; t++) {
-                const unsigned long long b = __ballot(np >= t);
-                if (!b) break;
-                pre += (uint32_t)__popcll(b & ltmask);
-                tot += (uint32_t)__popcll(b);
+            if (!__ballot(np >= 8u)) {
+#pragma unroll
+                for (int bit = 0; bit < 3; bit++) {
+                    const unsigned long long b = __ballot((np >> bit) & 1u);
+                    pre += (uint32_t)__popcll(b & ltmask) << bit;
+                    tot += (uint32_t)__popcll(b) << bit;
+                }
+            } else {
+                for (uint32_t t = 1;; t++) {
+                    const unsigned long long b = __ballot(np >= t);
+                    if (!b) break;
+                    pre += (uint32_t)__popcll(b & ltmask);
+                    tot += (uint32_t)__popcll(b);
+                }
             }
             if (tot == 0) continue;
-            if (DBG == 0 && (uint64_t)run + tot <= cap && np) {
-                uint32_t at = run + pre;
+            if ((uint64_t)run + tot <= cap) {
+                direct = direct || fill + tot > kPb;
                 const uint32_t r0 = (uint32_t)(row - s);
+                if (!direct) {
+                    uint32_t at = fill + pre;
+                    if (!__ballot(qn[0] > 1u || qn[1] > 1u || qn[2] > 1u || qn[3] > 1u)) {
+                        // one query per covered row (disjoint ranges): straight-line writes
 #pragma unroll
-                for (int k = 0; k < 4; k++)
-                    for (uint32_t i = 0; i < qn[k]; i++)
-                        list[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
+                        for (int k = 0; k < 4; k++) {
+                            if (qn[k]) pb[at] = ((uint32_t)(ql_lds ? s_ql[qa[k]] : T.qlist[qa[k]]) << 24) | (r0 + k);
+                            at += qn[k];
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            for (uint32_t i = 0; i < qn[k]; i++)
+                                pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
+                    }
+                    fill += tot;
+                } else {
+                    uint32_t at = run + pre;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        for (uint32_t i = 0; i < qn[k]; i++)
+                            list[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
+                }
             }
             run += tot;  // past cap: still counted, the slice is incomplete
         }
+        pend = fill;
+        pend_at = grp_at;
     }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
     if (lane == 0) {
         npairs[wc] = run;
         if ((uint64_t)run > cap) atomicOr(overflow, 1u);
@@ -566,145 +620,6 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
         if (lane >= o) incl += y;
     }
     uint32_t acc = incl - loc;
-    __builtin_amdgcn_wave_barrier();
-    for (int i = 0; i < per; i++) {
-        const int j = lane * per + i;
-        if (j < ne) {
-            const uint32_t c = h[j];
-            h[j] = acc;
-            acc += c;
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int i = lane; i < q; i += 64) {
-        const uint32_t ab = T.qab[i];
-        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
-    }
-}
-
-// The same with each lane owning 16 consecutive rows of a 1024-row wave-group (4
-// dwordx4 loads per lane), so one prefix over the lanes orders the group's pairs by
-// row, and a lane's pairs (up to kLcRegs, one query per row) are written by a loop
-// over the pair index: a handful of store instructions per 1024 rows instead of one
-// per element slot and wave-tile. Lanes with more pairs, or rows under overlapping
-// queries, write theirs row by row into their own range after that.
-constexpr int kLcRegs = 8;
-template <bool VEC>
-__global__ __launch_bounds__(kTPB) void k_ssp_count_lc(const int* __restrict__ col, uint64_t n, uint64_t rpb,
-                                                       EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
-                                                       uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
-                                                       uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
-    __shared__ uint32_t s_bkt[kBuckets];
-    __shared__ int32_t s_b[kEiMax];
-    __shared__ uint32_t s_qoff[kEiMax];
-    __shared__ uint32_t hist[kWaves][kEiMax];
-    __shared__ uint16_t s_ql[kQlCap];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    stage_buckets(T.bucket, s_bkt, tid);
-    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
-    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
-    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t nql = s_qoff[M.m + 1];
-    const bool ql_lds = nql <= (uint32_t)kQlCap;
-    if (ql_lds)
-        for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
-    __syncthreads();
-    uint64_t s, e;
-    wave_chunk(n, rpb, wave, &s, &e);
-    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
-    uint32_t* list = pairs + wc * cap;
-    uint32_t run = 0;
-    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
-        const uint64_t r0 = t + (uint64_t)lane * 16;  // this lane's 16 rows
-        int x[16];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int4 v = load_row4<VEC>(col, r0 + 4 * u, e);
-            x[4 * u] = v.x;
-            x[4 * u + 1] = v.y;
-            x[4 * u + 2] = v.z;
-            x[4 * u + 3] = v.w;
-        }
-        uint32_t ei[16], np = 0;
-        bool multi = false;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            ei[k] = 0xFFFFu;
-            if (r0 + k < e) {
-                const int eidx = ei_of(x[k], M, s_bkt, s_b);
-                const uint32_t a = s_qoff[eidx], c = s_qoff[eidx + 1] - a;
-                if (c) {
-                    atomicAdd(&hist[wave][eidx], 1u);
-                    ei[k] = (uint32_t)eidx;
-                    np += c;
-                    multi |= c > 1;
-                }
-            }
-        }
-        uint32_t incl = np;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        const uint32_t tot = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
-        if (tot == 0) continue;
-        if ((uint64_t)run + tot <= cap) {
-            const uint32_t at = run + incl - np;
-            const uint32_t rb = (uint32_t)(r0 - s);
-            const bool fast = !multi && np <= (uint32_t)kLcRegs;
-            uint32_t p[kLcRegs];
-            uint32_t m = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (fast && ei[k] != 0xFFFFu) {
-                    const uint32_t qa = s_qoff[ei[k]];
-                    const uint32_t v = ((uint32_t)(ql_lds ? s_ql[qa] : T.qlist[qa]) << 24) | (rb + k);
-#pragma unroll
-                    for (int r = 0; r < kLcRegs; r++)
-                        if (r == (int)m) p[r] = v;
-                    m++;
-                }
-            }
-            // store loop over the pair index: lane l writes its r-th pair at at + r
-#pragma unroll
-            for (int r = 0; r < kLcRegs; r++) {
-                if (!__ballot(fast && (uint32_t)r < m)) break;
-                if (fast && (uint32_t)r < m) list[at + r] = p[r];
-            }
-            if (!fast) {  // many pairs, or a row under several queries
-                uint32_t a2 = at;
-                for (int k = 0; k < 16; k++) {
-                    if (ei[k] == 0xFFFFu) continue;
-                    const uint32_t qa = s_qoff[ei[k]], c = s_qoff[ei[k] + 1] - qa;
-                    for (uint32_t i = 0; i < c; i++)
-                        list[a2++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | (rb + k);
-                }
-            }
-        }
-        run += tot;
-    }
-    if (lane == 0) {
-        npairs[wc] = run;
-        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t* h = hist[wave];
-    const int ne = M.m + 2;
-    const int per = (ne + 63) / 64;
-    uint32_t loc = 0;
-    for (int i = 0; i < per; i++) {
-        const int j = lane * per + i;
-        if (j < ne) loc += h[j];
-    }
-    uint32_t inc2 = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc2, o, 64);
-        if (lane >= o) inc2 += y;
-    }
-    uint32_t acc = inc2 - loc;
     __builtin_amdgcn_wave_barrier();
     for (int i = 0; i < per; i++) {
         const int j = lane * per + i;
@@ -1015,18 +930,7 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
             uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
             uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
             unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
-            const char* dbg = getenv("MQ_SSP_DEBUG");  // A/B of the pair listing's parts (timing only)
-            const char* lc = getenv("MQ_SSP_LC");
-            if (lc && lc[0] == '1' && vec)
-                hipLaunchKernelGGL(k_ssp_count_lc<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                   nwc, pr, cap, npr, of);
-            else if (dbg && vec && atoi(dbg) == 1)
-                hipLaunchKernelGGL((k_ssp_count<true, 1>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                   nwc, pr, cap, npr, of);
-            else if (dbg && vec && atoi(dbg) == 2)
-                hipLaunchKernelGGL((k_ssp_count<true, 2>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                   nwc, pr, cap, npr, of);
-            else if (vec)
+            if (vec)
                 hipLaunchKernelGGL(k_ssp_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
                                    nwc, pr, cap, npr, of);
             else

@@ -720,7 +720,7 @@ def _shared_run(lib, d, lows, highs):
     return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
 
 
-@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_lc"])
+@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass"])
 @pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
                                   "mixed256", "narrow_domain"])
 def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
@@ -735,8 +735,6 @@ def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
         monkeypatch.setenv("MQ_SS_IMPL", "ballot")
     if impl.endswith("twopass"):
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
-    if impl == "ei_lc":  # lane-contiguous pair listing (k_ssp_count_lc)
-        monkeypatch.setenv("MQ_SSP_LC", "1")
     rng = np.random.default_rng(hash(case) % 2 ** 32)
     n = 1_000_003
     d = rng.integers(0, 10 ** 6, n).astype(np.int32)
