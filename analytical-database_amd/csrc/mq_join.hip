@@ -196,6 +196,34 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1,
     hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
+// The same histogram from the digit bytes the previous scatter wrote (1 B per row
+// instead of the 8-byte words): one 16-byte load per thread covers its 16 rows.
+__global__ __launch_bounds__(kTPB) void k_sortw_hist_bytes(const uint8_t* __restrict__ dig, uint64_t n,
+                                                           uint32_t* __restrict__ hist, uint32_t ntiles) {
+    __shared__ uint32_t h[kRadix];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const uint64_t base = (uint64_t)tile * kSortTile + (uint64_t)threadIdx.x * kSortItems;
+    static_assert(kSortItems == 16, "one 16-byte load per thread");
+    if (base + kSortItems <= n) {
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(dig + base));
+        const uint32_t x[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            atomicAdd(&h[x[k] & 0xFF], 1u);
+            atomicAdd(&h[(x[k] >> 8) & 0xFF], 1u);
+            atomicAdd(&h[(x[k] >> 16) & 0xFF], 1u);
+            atomicAdd(&h[x[k] >> 24], 1u);
+        }
+    } else {
+        for (uint64_t i = base; i < n && i < base + kSortItems; i++) atomicAdd(&h[dig[i]], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+}
+
 // LAST: 0 = packed words to out, 1 = split into kout (flipped keys) / vout,
 // 2 = an index: kout as int32 values (key ^ 2^31 undone), pout as size_t rows.
 template <bool FIRST, int LAST>
@@ -203,7 +231,8 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
                                                         const u64* __restrict__ in, uint64_t n, int shift,
                                                         const u64* __restrict__ goff, uint32_t ntiles,
                                                         u64* __restrict__ out, uint32_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout, u64* __restrict__ pout) {
+                                                        uint32_t* __restrict__ vout, u64* __restrict__ pout,
+                                                        uint8_t* __restrict__ dig) {
     __shared__ uint32_t wcnt[kTPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
@@ -284,6 +313,7 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
                 if (pout) pout[dst] = v >> 32;
             } else {
                 out[dst] = v;
+                if (dig) dig[dst] = (uint8_t)((uint32_t)v >> (shift + 8));  // the next pass's digit
             }
         }
     }
@@ -1289,6 +1319,7 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
     }
     u64 *w0 = nullptr, *w1 = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t* hist = nullptr;
+    uint8_t* dig = nullptr;  // the next pass's digit of every row, written by the scatter
     const uint64_t ntiles = ceil_div(n, kSortTile);
     const uint64_t nh = ntiles * kRadix;
     auto done = [&](int rc) {
@@ -1297,14 +1328,16 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
         pool_free(hist);
         pool_free(hscan);
         pool_free(scratch);
+        pool_free(dig);
         return rc;
     };
     w0 = (u64*)pool_alloc(n * 8);
+    dig = (uint8_t*)pool_alloc(n + 16);
     w1 = (u64*)pool_alloc(n * 8);
     hist = (uint32_t*)pool_alloc(nh * 4);
     hscan = (u64*)pool_alloc(nh * 8);
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
-    if (!w0 || !w1 || !hist || !hscan || !scratch)
+    if (!w0 || !w1 || !hist || !hscan || !scratch || !dig)
         return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
     const dim3 g((uint32_t)ntiles), b(kTPB);
     for (int pass = 0; pass < 4; pass++) {
@@ -1312,22 +1345,22 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
         if (pass == 0)
             hipLaunchKernelGGL((k_sortw_hist<true>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
         else
-            hipLaunchKernelGGL((k_sortw_hist<false>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL(k_sortw_hist_bytes, g, b, 0, st, dig, n, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return done(rc);
         const uint32_t nt = (uint32_t)ntiles;
         if (pass == 0)
             hipLaunchKernelGGL((k_sortw_scatter<true, 0>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan, nt, w1,
-                               nullptr, nullptr, nullptr);
+                               nullptr, nullptr, nullptr, dig);
         else if (pass < 3)
             hipLaunchKernelGGL((k_sortw_scatter<false, 0>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
-                               nt, w1, nullptr, nullptr, nullptr);
+                               nt, w1, nullptr, nullptr, nullptr, dig);
         else if (mode == 1)
             hipLaunchKernelGGL((k_sortw_scatter<false, 1>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
-                               nt, nullptr, kout, vout, nullptr);
+                               nt, nullptr, kout, vout, nullptr, nullptr);
         else
             hipLaunchKernelGGL((k_sortw_scatter<false, 2>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
-                               nt, nullptr, kout, nullptr, pout);
+                               nt, nullptr, kout, nullptr, pout, nullptr);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "sort: launch"));
         u64* t = w0;
         w0 = w1;

@@ -27,7 +27,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <climits>
 #include <cstdarg>
@@ -1839,6 +1841,75 @@ struct Staging {
     bool ready;
 };
 thread_local Staging g_staging[kMaxDev];
+
+// The host side of the staged D2H: each chunk copied out of the pinned buffer by
+// the calling thread and kCopyHelpers helpers (one memcpy thread moved ~10 GB/s,
+// a quarter of the DMA rate). One pool per calling thread (row-shard workers copy
+// concurrently); helpers are started on first use and joined at thread exit.
+struct CopyPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go, done;
+    char* dst = nullptr;
+    const char* src = nullptr;
+    size_t len = 0;
+    unsigned long gen = 0;
+    int pending = 0, parts = 1;
+    bool quit = false;
+
+    void start() {
+        const char* e = getenv("MQ_COPY_THREADS");
+        parts = e ? atoi(e) : 4;
+        if (parts < 1) parts = 1;
+        if (parts > 16) parts = 16;
+        for (int i = 1; i < parts; i++) th.emplace_back([this, i] { loop(i); });
+    }
+    void slice(int i) {
+        const size_t a = len * (size_t)i / (size_t)parts, b = len * (size_t)(i + 1) / (size_t)parts;
+        if (b > a) memcpy(dst + a, src + a, b - a);
+    }
+    void loop(int i) {
+        unsigned long seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu);
+            go.wait(lk, [&] { return quit || gen != seen; });
+            if (quit) return;
+            seen = gen;
+            lk.unlock();
+            slice(i);
+            lk.lock();
+            if (--pending == 0) done.notify_one();
+        }
+    }
+    void copy(void* d, const void* s, size_t n) {
+        if (th.empty() && parts == 1 && gen == 0) start();
+        if (parts == 1 || n < ((size_t)1 << 20)) {
+            memcpy(d, s, n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            dst = static_cast<char*>(d);
+            src = static_cast<const char*>(s);
+            len = n;
+            pending = parts - 1;
+            gen++;
+        }
+        go.notify_all();
+        slice(0);
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return pending == 0; });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        go.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+thread_local CopyPool g_copy;
 }  // namespace
 
 int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream) {
@@ -1869,7 +1940,7 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
         const int b = (int)(c % kStageBufs);
         HIPCHK(hipEventSynchronize(S.ev[b]));
         const size_t off = c * kStageBytes, len = bytes - off < kStageBytes ? bytes - off : kStageBytes;
-        memcpy(static_cast<char*>(dst) + off, S.buf[b], len);
+        g_copy.copy(static_cast<char*>(dst) + off, S.buf[b], len);
         if (c + kStageBufs < nchunks && (rc = issue(c + kStageBufs))) return rc;
     }
     return MQ_OK;
