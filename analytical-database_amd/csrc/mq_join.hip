@@ -600,6 +600,8 @@ constexpr uint32_t kBucket = 4;
 __device__ __forceinline__ uint64_t ht_home(uint32_t key, uint64_t mask) {
     return hash32(key) & mask & ~(uint64_t)(kBucket - 1);
 }
+// a full bucket's overflow mark (windowed builds, k_win_build): slot order
+__device__ __forceinline__ bool bucket_ovf(u64 s0, u64 s1) { return (uint32_t)s0 > (uint32_t)s1; }
 
 // Global-CAS insert (builds below kWindowBuildRows): sets *general on a duplicate
 // key, the empty marker, or a full window.
@@ -815,6 +817,27 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
         }
     }
     __syncthreads();
+    // A full bucket records in its slot order whether any key homed there went on
+    // past it (then key(slot 0) > key(slot 1), else <; the keys are distinct), so a
+    // probe that misses in a full bucket without overflow ends there (bucket_ovf).
+    // One pass over the slots: a key outside its home bucket marks that bucket.
+    __shared__ uint8_t ovf[(1 << kWinLog) / kBucket];
+    for (uint32_t x = threadIdx.x; x < W / kBucket; x += kWinTPB) ovf[x] = 0;
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) {
+        const u64 v = tab[x];
+        if (v == kEmpty) continue;
+        const uint32_t hb = (uint32_t)ht_home((uint32_t)v, t.wmask) / kBucket;
+        if (hb != x / kBucket) ovf[hb] = 1;
+    }
+    __syncthreads();
+    for (uint32_t bk = threadIdx.x; bk < W / kBucket; bk += kWinTPB) {
+        const uint32_t s0 = bk * kBucket;
+        const u64 a = tab[s0], c = tab[s0 + 1];
+        if (a == kEmpty || c == kEmpty || tab[s0 + 2] == kEmpty || tab[s0 + 3] == kEmpty) continue;
+        if (((uint32_t)a > (uint32_t)c) != (ovf[bk] != 0)) tab[s0] = c, tab[s0 + 1] = a;
+    }
+    __syncthreads();
     u64* dst = words + (uint64_t)w * W;
     for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) dst[x] = tab[x];
 }
@@ -826,14 +849,61 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
 // 8.8 ms at 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8
 // had beaten 1 (7.9 vs 8.4 ms).
 constexpr int kProbeILP = 2;
+constexpr uint32_t kContCap = 320;  // queued continuations per wave (64 taken + 2 x 128 new fit)
+
+// One probe row's outputs. RUNS: the run start and length (0 = no match), from the
+// packed payload or, for a long run (or unpacked), from rs. Unique: the payload (the
+// build position), whose hit bit is the caller's.
+template <bool RUNS>
+__device__ __forceinline__ void probe_emit(uint64_t j, bool hit, uint32_t payload, uint32_t* __restrict__ pstart,
+                                           const uint32_t* __restrict__ rs, uint32_t* __restrict__ cnt,
+                                           bool packed) {
+    if constexpr (RUNS) {
+        uint32_t a = 0, L = 0;
+        if (hit) {
+            L = packed ? payload & 15u : 15u;
+            a = packed ? payload >> 4 : payload;
+            if (L == 15u) {
+                L = rs[a + 1] - rs[a];
+                a = rs[a];
+            }
+        }
+        pstart[j] = a;
+        cnt[j] = L;
+    } else {
+        pstart[j] = payload;  // (misses store 0: whole lines)
+    }
+}
+
+// kProbeILP probes per thread per step: the keys are loaded coalesced, then all
+// their home buckets (4 slots, 32 B, two 16-byte loads) are requested before any
+// is examined. Random reads cost per 32-B sector (tools/random_read: a 64-B bucket
+// takes 10.4 ms at 2^28 where 32 B take 5.6), so every slot read past the bucket
+// costs about as much as the bucket itself; a line is long gone from L2 by the
+// time a wave comes back to it. Two things keep those reads rare:
+//  * overflow marks (windowed builds): a full bucket's slot order says whether any
+//    key homed there lies past it; a miss in a full bucket without one ends there
+//    (continuations at load 1/2: 10 % of probes -> 5 %; 8.2 -> 6.8 ms);
+//  * the rest are not followed on the spot, where the wave would wait for one
+//    dependent read per slot: the row goes to a per-wave queue in LDS, and each
+//    step the wave takes up to 64 queued rows and requests their next slot with
+//    the new buckets, in the same round trip (an unresolved row is requeued).
 // RUNS (duplicate keys as runs, the payload a packed run, see run_payload): per row
-// the run's start in pstart and its length in cnt (0 = no match) instead of hit words.
+// the run's start in pstart and its length in cnt (0 = no match) instead of hit
+// words. Row indices and steps are kept as u32 (n2 <= 2^31 rows).
 template <bool RUNS>
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
                                                           u64* __restrict__ hits, const uint32_t* __restrict__ rs,
-                                                          uint32_t* __restrict__ cnt, bool packed) {
+                                                          uint32_t* __restrict__ cnt, bool packed, bool marks) {
+    __shared__ uint32_t q_j[kTPB / 64][kContCap], q_h[kTPB / 64][kContCap], q_k[kTPB / 64][kContCap];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* const qj = q_j[wave];
+    uint32_t* const qh = q_h[wave];
+    uint32_t* const qk = q_k[wave];
+    uint32_t nq = 0;  // queued rows (wave-uniform)
+    const uint64_t lt = (1ull << lane) - 1;
     const uint64_t stride = (uint64_t)gridDim.x * kTPB * kProbeILP;
     uint64_t j0 = (uint64_t)blockIdx.x * kTPB * kProbeILP + threadIdx.x;
     // the next step's keys are loaded while this step's buckets are in flight;
@@ -844,10 +914,55 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
         const uint64_t j = j0 + (uint64_t)u * kTPB;
         knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
     }
-    for (; j0 < n2; j0 += stride) {
+    // a queued row: cj, its key ck and ch, the slot it is at as steps from its home
+    // slot (kBucket.. W-1); the slot itself is recomputed from the key
+    auto cont_slot = [&](uint32_t ck, uint32_t ch) {
+        const uint64_t hh = ht_home(ck, t.mask);
+        return (hh & ~t.wmask) | ((hh + ch) & t.wmask);
+    };
+    // a continuation: row cj at step ch with key ck (lanes < ntake hold one)
+    auto cont_resolve = [&](bool has, uint32_t cj, uint32_t ch, uint32_t ck, u64 c) {
+        // c: the slot's word. Resolved on the key or an empty slot; otherwise requeued.
+        bool again = false;
+        if (has) {
+            if (c == kEmpty || (uint32_t)c == ck || ch >= t.wmask) {  // (a full window: a miss)
+                const bool hit = c != kEmpty && (uint32_t)c == ck;
+                const uint32_t payload = hit ? (uint32_t)(c >> 32) : 0u;
+                if (RUNS || hit) probe_emit<RUNS>(cj, hit, payload, pstart, rs, cnt, packed);
+                if (!RUNS && hit) atomicOr(&hits[cj >> 6], 1ull << (cj & 63));  // word stored in an earlier step
+            } else {
+                again = true;
+            }
+        }
+        const u64 am = __ballot(again);
+        if (again) {
+            const uint32_t at = nq + (uint32_t)__popcll(am & lt);
+            qj[at] = cj;
+            qh[at] = ch + 1;
+            qk[at] = ck;
+        }
+        nq += (uint32_t)__popcll(am);
+    };
+    // the loop runs while the wave's first row is in range, so all 64 lanes take
+    // every step together (the queue count is per wave)
+    for (; j0 - (uint64_t)lane < n2; j0 += stride) {
         uint32_t key[kProbeILP];
         uint64_t h[kProbeILP];
         ulonglong2 b0[kProbeILP], b1[kProbeILP];  // the home bucket, slots 0-1 and 2-3
+        // up to 64 queued rows from the back of the queue, their slots requested
+        // with this step's buckets
+        const uint32_t ntake = nq < 64 ? nq : 64;
+        const bool has = (uint32_t)lane < ntake;
+        uint32_t cj = 0, ch = 0, ck = 0;
+        if (has) {
+            const uint32_t e = nq - ntake + (uint32_t)lane;
+            cj = qj[e];
+            ch = qh[e];
+            ck = qk[e];
+        }
+        nq -= ntake;
+        u64 c = 0;
+        if (has) c = words[cont_slot(ck, ch)];
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             key[u] = knext[u];
@@ -861,6 +976,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             const uint64_t j = j0 + stride + (uint64_t)u * kTPB;
             knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
         }
+        cont_resolve(has, cj, ch, ck, c);
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
@@ -870,47 +986,58 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
 #pragma unroll
             for (uint32_t i = 0; i < kBucket; i++) {
                 if (done) break;
-                const u64 c = sl[i];
-                if (c == kEmpty) done = true;
-                else if ((uint32_t)c == key[u]) hit = done = true, payload = (uint32_t)(c >> 32);
+                const u64 w = sl[i];
+                if (w == kEmpty) done = true;
+                else if ((uint32_t)w == key[u]) hit = done = true, payload = (uint32_t)(w >> 32);
             }
-            if (!done) {  // a full bucket without the key: on along the window
-                uint64_t hh = h[u];
-                for (uint32_t i = 0; i < kBucket; i++) hh = win_next(hh, t);
-                for (uint64_t step = kBucket; step <= t.wmask; step++) {
-                    const u64 c = words[hh];
-                    if (c == kEmpty) break;
-                    if ((uint32_t)c == key[u]) {
-                        hit = true;
-                        payload = (uint32_t)(c >> 32);
-                        break;
-                    }
-                    hh = win_next(hh, t);
-                }
+            // a full bucket without the key: on along the window, unless its mark
+            // says no key homed here went on (j < n2 here)
+            const bool defer = !done && !(marks && !bucket_ovf(sl[0], sl[1]));
+            const u64 dm = __ballot(defer);
+            if (defer) {
+                const uint32_t at = nq + (uint32_t)__popcll(dm & lt);
+                qj[at] = (uint32_t)j;
+                qh[at] = kBucket;
+                qk[at] = key[u];
             }
-            if constexpr (RUNS) {
-                if (j < n2) {
-                    uint32_t a = 0, L = 0;
-                    if (hit) {
-                        L = packed ? payload & 15u : 15u;
-                        a = packed ? payload >> 4 : payload;
-                        if (L == 15u) {  // a long run (or unpacked): its bounds from rs
-                            L = rs[a + 1] - rs[a];
-                            a = rs[a];
-                        }
-                    }
-                    pstart[j] = a;
-                    cnt[j] = L;
-                }
-            } else {
+            nq += (uint32_t)__popcll(dm);
+            if (j < n2 && !defer) probe_emit<RUNS>(j, hit, payload, pstart, rs, cnt, packed);
+            if constexpr (!RUNS) {
                 // a wave's 64 lanes hold 64 consecutive rows: their hits are one word
+                // (a deferred row's bit is set when it resolves)
                 const u64 m = __ballot(hit);
-                if (j < n2) {
-                    if (hit) pstart[j] = payload;  // the build position itself
-                    if ((threadIdx.x & 63) == 0) hits[j >> 6] = m;
-                }
+                if (j < n2 && lane == 0) hits[j >> 6] = m;
             }
         }
+        // keep room for a step's worst case (64 requeued + 64 x kProbeILP new):
+        // drain in place when the queue runs long
+        while (nq > kContCap - 64 - 64 * kProbeILP) {
+            const uint32_t nt = nq < 64 ? nq : 64;
+            const bool hs = (uint32_t)lane < nt;
+            uint32_t dj = 0, dh = 0, dk = 0;
+            u64 dc = 0;
+            if (hs) {
+                const uint32_t e = nq - nt + (uint32_t)lane;
+                dj = qj[e], dh = qh[e], dk = qk[e];
+                dc = words[cont_slot(dk, dh)];
+            }
+            nq -= nt;
+            cont_resolve(hs, dj, dh, dk, dc);
+        }
+    }
+    // the queue's rest
+    while (nq) {
+        const uint32_t nt = nq < 64 ? nq : 64;
+        const bool hs = (uint32_t)lane < nt;
+        uint32_t dj = 0, dh = 0, dk = 0;
+        u64 dc = 0;
+        if (hs) {
+            const uint32_t e = nq - nt + (uint32_t)lane;
+            dj = qj[e], dh = qh[e], dk = qk[e];
+            dc = words[cont_slot(dk, dh)];
+        }
+        nq -= nt;
+        cont_resolve(hs, dj, dh, dk, dc);
     }
 }
 
@@ -1086,6 +1213,7 @@ struct mq_join {
     int unique;            // 1: windowed {key, payload} table (words only); 0: words/start/len;
                            // 2: windowed table of distinct keys -> run index, runs in rs
     const uint32_t* rs;    // unique == 2: first sorted row of each run, + n1
+    bool marks;            // the unique table's full buckets carry overflow marks (k_win_build)
     bool packed;           // unique == 2: payloads carry start << 4 | length (k_run_payload)
     uint64_t n1, mask;
     Win win;               // unique table geometry
@@ -1130,6 +1258,7 @@ constexpr uint64_t kWindowBuildRows = 1ull << 16;
 int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
                   uint32_t* general, hipStream_t st, const DevState* s) {
     const Win t = j->win;
+    j->marks = n >= kWindowBuildRows && !getenv("MQ_JOIN_NOMARKS");
     if (n < kWindowBuildRows) {
         HIPCHK(hipMemsetAsync(j->words, 0xFF, slots * 8, st));
         hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, p1,
@@ -1332,20 +1461,24 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
         return rc;
     };
     w0 = (u64*)pool_alloc(n * 8);
-    dig = (uint8_t*)pool_alloc(n + 16);
+    const char* de = getenv("MQ_SORT_DIGITS");
+    const bool use_dig = !(de && de[0] == '0');
+    if (use_dig) dig = (uint8_t*)pool_alloc(n + 16);
     w1 = (u64*)pool_alloc(n * 8);
     hist = (uint32_t*)pool_alloc(nh * 4);
     hscan = (u64*)pool_alloc(nh * 8);
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
-    if (!w0 || !w1 || !hist || !hscan || !scratch || !dig)
+    if (!w0 || !w1 || !hist || !hscan || !scratch || (use_dig && !dig))
         return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
     const dim3 g((uint32_t)ntiles), b(kTPB);
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
         if (pass == 0)
             hipLaunchKernelGGL((k_sortw_hist<true>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
-        else
+        else if (use_dig)
             hipLaunchKernelGGL(k_sortw_hist_bytes, g, b, 0, st, dig, n, hist, (uint32_t)ntiles);
+        else
+            hipLaunchKernelGGL((k_sortw_hist<false>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return done(rc);
         const uint32_t nt = (uint32_t)ntiles;
@@ -1486,6 +1619,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     int rc = ensure_ready(&s);
     if (rc) return rc;
     if (!j || !h_m || (n2 && !d_c2)) return set_err(MQ_EINVAL, "mq_join_probe: bad argument");
+    if (n2 > (1ull << 31)) return set_err(MQ_EINVAL, "mq_join_probe: %llu rows (int32 positions)", (unsigned long long)n2);
     hipStream_t st = (hipStream_t)stream;
     if (j->pstart) HIPCHK(hipDeviceSynchronize());  // a queued write may still read them
     pool_free(j->pstart);
@@ -1512,13 +1646,15 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     const uint64_t nscan = words_scan ? nw : n2;
     uint32_t* const cnt = j->unique == 1 ? j->plen + 2 * nw : j->plen;
     if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
-        hipLaunchKernelGGL(k_ht_probe_unique<true>, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)&k_ht_probe_unique<true>)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed);
+        auto kern = k_ht_probe_unique<true>;
+        hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
-        hipLaunchKernelGGL(k_ht_probe_unique<false>, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)&k_ht_probe_unique<false>)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false);
+        auto kern = k_ht_probe_unique<false>;
+        hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
+                           j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false, j->marks);
         LAUNCHCHK("k_ht_probe_unique");
         hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
         LAUNCHCHK("k_hits_count");

@@ -526,7 +526,8 @@ def _dev_join(lib, c1, p1, c2, p2):
 
 @pytest.mark.parametrize("runs", [True, False])
 @pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
-                                  "unique_partitioned", "dups_partitioned", "ragged_hits"])
+                                  "unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned",
+                                  "ragged_hits"])
 def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
     """runs: duplicate keys as sorted runs behind the windowed table of distinct keys
     (default); MQ_JOIN_RUNS=0: the global-CAS table of run heads (the fallback)."""
@@ -555,7 +556,9 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
     elif case == "ragged_hits":  # unique keys, probe rows 64k+1 with hits at the word edges
         c1 = rng.permutation(1000).astype(np.int32)
         c2 = np.concatenate([np.arange(129), rng.integers(500, 2000, 64 * 7 + 1), [999]]).astype(np.int32)
-    elif case in ("unique_partitioned", "dups_partitioned"):
+    elif case in ("unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned"):
+        if case.endswith("nomarks"):  # the windowed table without overflow marks
+            monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
         # > 2^22 build rows: the window-partitioned insert. Keys from the spread
         # config-5 generator: the oracle restates the reference's `key % size`
         # multimap, which goes quadratic on dense or arithmetic key runs.

@@ -58,18 +58,20 @@ __global__ __launch_bounds__(256) void k_bucket(const unsigned long long* __rest
     unsigned long long acc = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * 2;
     for (uint64_t j0 = (uint64_t)blockIdx.x * 256 * 2 + threadIdx.x; j0 < p; j0 += stride) {
-        ulonglong2 a[2], b[2];
+        ulonglong2 a[2], b[2], c[2], d[2];
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             const uint64_t j = j0 + (uint64_t)u * 256;
             const unsigned k = DEP ? keys[j < p ? j : p - 1] : (unsigned)j;
-            const uint64_t h = (uint64_t)mix(k) & mask & ~3ull;
+            const uint64_t h = (uint64_t)mix(k) & mask & ~(MODE == 4 ? 7ull : 3ull);
             const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t + h);
             a[u] = q[0];
-            b[u] = MODE == 2 ? q[1] : make_ulonglong2(0, 0);
+            b[u] = MODE >= 2 ? q[1] : make_ulonglong2(0, 0);
+            c[u] = MODE == 4 ? q[2] : make_ulonglong2(0, 0);
+            d[u] = MODE == 4 ? q[3] : make_ulonglong2(0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 2; u++) acc ^= a[u].x ^ a[u].y ^ b[u].x ^ b[u].y;
+        for (int u = 0; u < 2; u++) acc ^= a[u].x ^ a[u].y ^ b[u].x ^ b[u].y ^ c[u].x ^ c[u].y ^ d[u].x ^ d[u].y;
     }
     if (acc == 0x123456789ull) out[0] = acc;
 }
@@ -129,8 +131,9 @@ int main(int argc, char** argv) {
             std::sort(ms.begin(), ms.end());
             return ms[ms.size() / 2];
         };
-        printf("{\"bucket_1x16\": %.3f, \"bucket_2x16\": %.3f, \"bucket_2x16_key_loaded\": %.3f}\n",
-               tb(k_bucket<1, false>), tb(k_bucket<2, false>), tb(k_bucket<2, true>));
+        printf("{\"bucket_1x16\": %.3f, \"bucket_2x16\": %.3f, \"bucket_2x16_key_loaded\": %.3f, "
+               "\"bucket_4x16_key_loaded\": %.3f}\n",
+               tb(k_bucket<1, false>), tb(k_bucket<2, false>), tb(k_bucket<2, true>), tb(k_bucket<4, true>));
         CK(hipFree(keys));
     }
     for (int grid_mul : {8}) {
