@@ -37,6 +37,7 @@ constexpr int kScanTile = kTPB * kScanItems;  // 4096
 constexpr int kSortItems = 16;  // 8: 36.3 ms, 32: 40.5 ms for the 1e9-row index (16: 31.2)
 constexpr int kSortTile = kTPB * kSortItems;  // 4096
 constexpr int kRadix = 256;
+constexpr int kSortTPB = 512;  // sort tile = kSortTPB x kSortItems words (radix_sort_tiles)
 
 typedef unsigned long long u64;
 
@@ -152,7 +153,7 @@ int scan_exclusive(const Tin* in, u64* out, uint64_t n, u64* scratch, hipStream_
 
 // ---------------------------------------------------------------------------
 // stable LSD radix sort of packed words {key ^ 2^31 (low 32), value (high 32)},
-// 8-bit digits. Per 4096-word tile: an LDS histogram (k_sortw_hist), an exclusive
+// 8-bit digits. Per tile of TPB x IT words (8192): an LDS histogram (k_sortw_hist), an exclusive
 // scan over (digit, tile), then a scatter that ranks equal digits with 8 wave
 // ballots (stable) and stages the tile in LDS, so every digit run leaves the block
 // as contiguous stores. (Element-by-element scatter measured 0.5 TB/s at 1e9 rows.)
@@ -169,44 +170,47 @@ __device__ __forceinline__ u64 sort_word(const int* c1, const int* p1, const u64
     }
 }
 
-template <bool FIRST>
-__global__ __launch_bounds__(kTPB) void k_sortw_hist(const int* __restrict__ c1, const u64* __restrict__ in,
-                                                     uint64_t n, int shift, uint32_t* __restrict__ hist,
-                                                     uint32_t ntiles) {
+template <bool FIRST, int TPB, int IT>
+__global__ __launch_bounds__(TPB) void k_sortw_hist(const int* __restrict__ c1, const u64* __restrict__ in,
+                                                    uint64_t n, int shift, uint32_t* __restrict__ hist,
+                                                    uint32_t ntiles) {
+    constexpr uint32_t kTile = TPB * IT;
     __shared__ uint32_t h[kRadix];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kSortTile;
+    const uint64_t base = (uint64_t)tile * kTile;
     // all of the lane's items are loaded before any is counted (indices clamped,
     // no branch), so the loads share one round trip instead of one each; the words
     // are read once, nontemporal (1.72 -> 1.62 ms per pass over 8 GB at 1e9 rows)
-    uint32_t key[kSortItems];
+    uint32_t key[IT];
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
+    for (int k = 0; k < IT; k++) {
+        const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
         const uint64_t ic = i < n ? i : n - 1;
         key[k] = FIRST ? ((uint32_t)__builtin_nontemporal_load(c1 + ic) ^ 0x80000000u)
                        : (uint32_t)__builtin_nontemporal_load(in + ic);
     }
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++)
-        if (base + (uint64_t)k * kTPB + threadIdx.x < n) atomicAdd(&h[(key[k] >> shift) & 0xFF], 1u);
+    for (int k = 0; k < IT; k++)
+        if (base + (uint64_t)k * TPB + threadIdx.x < n) atomicAdd(&h[(key[k] >> shift) & 0xFF], 1u);
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+    if (threadIdx.x < kRadix) hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // The same histogram from the digit bytes the previous scatter wrote (1 B per row
 // instead of the 8-byte words): one 16-byte load per thread covers its 16 rows.
-__global__ __launch_bounds__(kTPB) void k_sortw_hist_bytes(const uint8_t* __restrict__ dig, uint64_t n,
-                                                           uint32_t* __restrict__ hist, uint32_t ntiles) {
+template <int TPB, int IT>
+__global__ __launch_bounds__(TPB) void k_sortw_hist_bytes(const uint8_t* __restrict__ dig, uint64_t n,
+                                                          uint32_t* __restrict__ hist, uint32_t ntiles) {
+    constexpr uint32_t kTile = TPB * IT;
     __shared__ uint32_t h[kRadix];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kSortTile + (uint64_t)threadIdx.x * kSortItems;
-    static_assert(kSortItems == 16, "one 16-byte load per thread");
-    if (base + kSortItems <= n) {
+    const uint64_t base = (uint64_t)tile * kTile + (uint64_t)threadIdx.x * IT;
+    static_assert(IT == 16, "one 16-byte load per thread");
+    if (base + IT <= n) {
         typedef unsigned int v4u __attribute__((ext_vector_type(4)));
         const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(dig + base));
         const uint32_t x[4] = {w.x, w.y, w.z, w.w};
@@ -218,46 +222,47 @@ __global__ __launch_bounds__(kTPB) void k_sortw_hist_bytes(const uint8_t* __rest
             atomicAdd(&h[x[k] >> 24], 1u);
         }
     } else {
-        for (uint64_t i = base; i < n && i < base + kSortItems; i++) atomicAdd(&h[dig[i]], 1u);
+        for (uint64_t i = base; i < n && i < base + IT; i++) atomicAdd(&h[dig[i]], 1u);
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+    if (threadIdx.x < kRadix) hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
 }
 
 // LAST: 0 = packed words to out, 1 = split into kout (flipped keys) / vout,
 // 2 = an index: kout as int32 values (key ^ 2^31 undone), pout as size_t rows.
-template <bool FIRST, int LAST>
-__global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
+template <bool FIRST, int LAST, int TPB, int IT>
+__global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
                                                         const u64* __restrict__ in, uint64_t n, int shift,
                                                         const u64* __restrict__ goff, uint32_t ntiles,
                                                         u64* __restrict__ out, uint32_t* __restrict__ kout,
                                                         uint32_t* __restrict__ vout, u64* __restrict__ pout,
                                                         uint8_t* __restrict__ dig) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    constexpr int kW = TPB / 64;
+    constexpr uint32_t kTile = TPB * IT;
+    __shared__ uint32_t wcnt[kW][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ u64 stage[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ u64 stage[kTile];
+    __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    for (int x = tid; x < kW * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
-    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    const uint64_t tile0 = (uint64_t)tile * kTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * IT);
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    u64 el[kSortItems];
-    uint32_t dr[kSortItems];
+    u64 el[IT];
+    uint32_t dr[IT];
     // all items loaded first (indices clamped, no branch): one round trip, not one
     // per item (the ranking's ballots kept the compiler from hoisting the loads)
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
+    for (int k = 0; k < IT; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         el[k] = sort_word<FIRST>(c1, p1, in, i < n ? i : n - 1);
     }
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
+    for (int k = 0; k < IT; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool valid = i < n;
         const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
@@ -270,37 +275,43 @@ __global__ __launch_bounds__(kTPB) void k_sortw_scatter(const int* __restrict__ 
         dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    uint32_t tot = 0;
+    // per digit (thread tid < 256): prefix over the waves, then the tile-local
+    // exclusive scan of the digit totals (waves 0-3)
+    uint32_t tot = 0, incl = 0;
+    if (tid < kRadix) {
 #pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
+        for (int w = 0; w < kW; w++) {
+            const uint32_t c = wcnt[w][tid];
+            wcnt[w][tid] = tot;
+            tot += c;
+        }
+        incl = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
     }
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
+    __syncthreads();
+    if (tid < kRadix) {
+        uint32_t excl = incl - tot;
+        for (int w = 0; w < wave; w++) excl += wsum[w];
+        loff[tid] = excl;
     }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
+    for (int k = 0; k < IT; k++) {
         if (dr[k] != 0xFFFFFFFFu) {
             const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
             stage[loff[d] + wcnt[wave][d] + r] = el[k];
         }
     }
     __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint32_t e = (uint32_t)(k * kTPB + tid);
+    for (int k = 0; k < IT; k++) {
+        const uint32_t e = (uint32_t)(k * TPB + tid);
         if (e < tn) {
             const u64 v = stage[e];
             const uint32_t d = ((uint32_t)v >> shift) & 0xFF;
@@ -1432,6 +1443,10 @@ int radix_sort_onesweep(const int* c1, const int* p1, uint64_t n, int mode, uint
     return done(MQ_OK);
 }
 
+template <int TPB, int IT>
+int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
+                     u64* pout, hipStream_t st);
+
 int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
                    u64* pout, hipStream_t st) {
     // MQ_SORT_IMPL=onesweep: decoupled look-back instead of a histogram pass per pass.
@@ -1446,10 +1461,20 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
         if (rc) return rc;
         return radix_sort_onesweep(c1, p1, n, mode, kout, vout, pout, st, s);
     }
+    // tiles of 512 x 16 words: 18.7 ms for the 1e9-row index, against 21.6 with
+    // 256 x 16 (digit runs of 16 words leave the block as 128-B pieces), 25.9 with
+    // 1024 x 8 and 22.3 with 512 x 8 (tools/sorttpb_cmd.sh)
+    return radix_sort_tiles<kSortTPB, kSortItems>(c1, p1, n, mode, kout, vout, pout, st);
+}
+
+template <int TPB, int IT>
+int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
+                     u64* pout, hipStream_t st) {
+    constexpr uint64_t kTile = (uint64_t)TPB * IT;
     u64 *w0 = nullptr, *w1 = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t* hist = nullptr;
     uint8_t* dig = nullptr;  // the next pass's digit of every row, written by the scatter
-    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t ntiles = ceil_div(n, kTile);
     const uint64_t nh = ntiles * kRadix;
     auto done = [&](int rc) {
         pool_free(w0);
@@ -1470,29 +1495,29 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
     scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
     if (!w0 || !w1 || !hist || !hscan || !scratch || (use_dig && !dig))
         return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
-    const dim3 g((uint32_t)ntiles), b(kTPB);
+    const dim3 g((uint32_t)ntiles), b(TPB);
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
         if (pass == 0)
-            hipLaunchKernelGGL((k_sortw_hist<true>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL((k_sortw_hist<true, TPB, IT>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
         else if (use_dig)
-            hipLaunchKernelGGL(k_sortw_hist_bytes, g, b, 0, st, dig, n, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL((k_sortw_hist_bytes<TPB, IT>), g, b, 0, st, dig, n, hist, (uint32_t)ntiles);
         else
-            hipLaunchKernelGGL((k_sortw_hist<false>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL((k_sortw_hist<false, TPB, IT>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return done(rc);
         const uint32_t nt = (uint32_t)ntiles;
         if (pass == 0)
-            hipLaunchKernelGGL((k_sortw_scatter<true, 0>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan, nt, w1,
+            hipLaunchKernelGGL((k_sortw_scatter<true, 0, TPB, IT>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan, nt, w1,
                                nullptr, nullptr, nullptr, dig);
         else if (pass < 3)
-            hipLaunchKernelGGL((k_sortw_scatter<false, 0>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+            hipLaunchKernelGGL((k_sortw_scatter<false, 0, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
                                nt, w1, nullptr, nullptr, nullptr, dig);
         else if (mode == 1)
-            hipLaunchKernelGGL((k_sortw_scatter<false, 1>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+            hipLaunchKernelGGL((k_sortw_scatter<false, 1, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
                                nt, nullptr, kout, vout, nullptr, nullptr);
         else
-            hipLaunchKernelGGL((k_sortw_scatter<false, 2>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+            hipLaunchKernelGGL((k_sortw_scatter<false, 2, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
                                nt, nullptr, kout, nullptr, pout, nullptr);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "sort: launch"));
         u64* t = w0;
