@@ -189,7 +189,9 @@ template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, uint64_t n,
                                                    uint64_t rpb, const Pred* __restrict__ preds,
                                                    int q, const unsigned long long* __restrict__ offs,
-                                                   uint64_t nwc, int* const* __restrict__ outs, int32_t base) {
+                                                   uint64_t nwc, int* const* __restrict__ outs, int32_t base,
+                                                   const unsigned int* __restrict__ only_if) {
+    if (only_if && !*only_if) return;  // single pass without overflow: k_ssp_scatter wrote
     __shared__ unsigned long long run[kWaves][kMaxQ];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -250,6 +252,9 @@ constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
 constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
+constexpr int kBucketsP = kBuckets / 2;  // k_ssp_count's bucket table (LDS)
+constexpr int kCoarse = 16384;           // k_ssp_count's coverage bitmap cells
+constexpr uint32_t kRing = 320;          // k_ssp_count's queued rows per wave (< 64 + a 256-row tile)
 // Pairs of one 1024-row wave-group held in LDS until the next group's loads are
 // issued, then written with at most 4 straight-line coalesced stores: vmcnt retires
 // loads and stores in order, so stores issued before a group's loads (or a
@@ -262,6 +267,7 @@ struct EiMeta {
     int m;          // number of bounds
     int shift;      // bucket width 2^shift
     int bmin, bmax; // first / last bound
+    int cshift;     // coverage cell width 2^cshift
 };
 
 struct EiTables {  // device copies, filled by the host (ss_count)
@@ -270,6 +276,7 @@ struct EiTables {  // device copies, filled by the host (ss_count)
     const uint32_t* qoff;       // m + 2: CSR offsets of the per-EI query lists
     const uint16_t* qlist;      // queries covering each EI, ascending
     const uint32_t* qab;        // per query: ea (low 16) | eb (high 16)
+    const uint32_t* cov;        // kCoarse bits over [bmin, bmax]: a covered EI meets the cell
 };
 
 __device__ __forceinline__ int ei_of(int32_t v, const EiMeta& M, const uint32_t* s_bkt,
@@ -369,7 +376,9 @@ template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, const Pred* __restrict__ preds,
                                                     int q, const unsigned long long* __restrict__ offs,
-                                                    uint64_t nwc, int* const* __restrict__ outs, int32_t base) {
+                                                    uint64_t nwc, int* const* __restrict__ outs, int32_t base,
+                                                    const unsigned int* __restrict__ only_if) {
+    if (only_if && !*only_if) return;  // single pass without overflow: k_ssp_scatter wrote
     __shared__ uint32_t s_bkt[kBuckets];
     __shared__ int32_t s_b[kEiMax];
     __shared__ uint32_t s_qoff[kEiMax];
@@ -480,125 +489,215 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
 // of its wave-chunk; a wave-chunk with more pairs (dense queries) flags an overflow
 // and the write falls back to the column pass (k_ssi_write) on the same counts.
 // ---------------------------------------------------------------------------
+// Rows no query covers (most of them at the usual selectivities) are dropped before
+// the interval lookup by a coarse bitmap over [bmin, bmax] (kCoarse cells, a cell
+// set when any covered EI meets it); the rows that pass are queued per wave in LDS
+// in row order and looked up 64 at a time, so the lookup and the pair listing run
+// on full waves instead of on every row slot of every tile.
 template <bool VEC>
 __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
                                                     uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
-    __shared__ uint32_t s_bkt[kBuckets];
+    __shared__ uint32_t s_bkt[kBucketsP];
     __shared__ int32_t s_b[kEiMax];
     __shared__ uint32_t s_qoff[kEiMax];
     __shared__ uint32_t hist[kWaves][kEiMax];
     __shared__ uint16_t s_ql[kQlCap];
     __shared__ uint32_t s_pb[kWaves][kPb];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint32_t s_cov[kCoarse / 32];
+    __shared__ int32_t s_qv[kWaves][kRing];
+    __shared__ uint32_t s_qr[kWaves][kRing];
+    // (the wave index through readfirstlane: the chunk bounds and the per-group
+    // branches below are then scalar)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    stage_buckets(T.bucket, s_bkt, tid);
+    {  // the 2048-bucket table: bucket k covers the 4096-bucket table's 2k and 2k+1
+        constexpr int kPer = kBucketsP / kTPB;
+        uint32_t u[kPer], w[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) u[k] = T.bucket[2 * (tid + k * kTPB)], w[k] = T.bucket[2 * (tid + k * kTPB) + 1];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) s_bkt[tid + k * kTPB] = (u[k] & 0xFFFFu) | (w[k] & 0xFFFF0000u);
+    }
+    for (int i = tid; i < kCoarse / 32; i += kTPB) s_cov[i] = T.cov[i];
     for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
     for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
     for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
     __syncthreads();
+    EiMeta MP = M;
+    MP.shift = M.shift + 1;
     // the per-EI query lists: in LDS when they fit (the usual case), else read from HBM
     const uint32_t nql = s_qoff[M.m + 1];
     const bool ql_lds = nql <= (uint32_t)kQlCap;
     if (ql_lds)
         for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
     __syncthreads();
+    const uint32_t span = (uint32_t)M.bmax - (uint32_t)M.bmin;
+    const bool tail_cov = s_qoff[M.m + 1] > s_qoff[M.m];  // values past bmax are in EI m
+    const bool tail_in = tail_cov;
+    auto covered = [&](int32_t v) -> bool {  // branch-free: outside [bmin, bmax] reads word 0
+        const uint32_t d = (uint32_t)v - (uint32_t)M.bmin;
+        const bool in = d <= span;
+        const uint32_t c = in ? d >> M.cshift : 0u;
+        const bool bit = (s_cov[c >> 5] >> (c & 31)) & 1u;
+        return in ? bit : (v > M.bmax && tail_in);
+    };
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
     const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
     uint32_t* list = pairs + wc * cap;
     uint32_t* pb = s_pb[wave];
+    int32_t* qv = s_qv[wave];
+    uint32_t* qr = s_qr[wave];
     uint32_t run = 0;  // pairs of this wave-chunk so far (wave-uniform)
     uint32_t pend = 0, pend_at = 0;  // the previous group's pairs, still in pb
+    uint32_t head = 0, tail = 0;  // queued rows [head, tail) of qv / qr
+    uint32_t fill = 0;    // this group's pairs in pb
+    bool direct = false;  // the group outgrew pb: its later pairs are stored directly
+    // one round: up to 64 queued rows (lanes < nr), their EI, counts and pairs
+    auto round = [&](uint32_t nr) {
+        const bool has = (uint32_t)lane < nr;
+        uint32_t qa = 0, qn = 0, r = 0;
+        if (has) {
+            const uint32_t slot = head + (uint32_t)lane;
+            const int32_t x = qv[slot];
+            r = qr[slot];
+            const int ei = ei_of(x, MP, s_bkt, s_b);
+            qa = s_qoff[ei];
+            qn = s_qoff[ei + 1] - qa;
+            if (qn) atomicAdd(&hist[wave][ei], 1u);
+        }
+        head += nr;
+        // exclusive prefix of qn over the lanes (a row is covered by a few queries)
+        uint32_t pre = 0, tot = 0;
+        if (!__ballot(qn >= 8u)) {
+#pragma unroll
+            for (int bit = 0; bit < 3; bit++) {
+                const unsigned long long bm = __ballot((qn >> bit) & 1u);
+                pre += (uint32_t)__popcll(bm & ltmask) << bit;
+                tot += (uint32_t)__popcll(bm) << bit;
+            }
+        } else {
+            for (uint32_t t = 1;; t++) {
+                const unsigned long long bm = __ballot(qn >= t);
+                if (!bm) break;
+                pre += (uint32_t)__popcll(bm & ltmask);
+                tot += (uint32_t)__popcll(bm);
+            }
+        }
+        if (tot == 0) return;
+        if ((uint64_t)run + tot <= cap) {
+            direct = direct || fill + tot > kPb;
+            if (!direct) {
+                uint32_t at = fill + pre;
+                if (!__ballot(qn > 1u)) {
+                    if (qn) pb[at] = ((uint32_t)(ql_lds ? s_ql[qa] : T.qlist[qa]) << 24) | r;
+                } else {
+                    for (uint32_t i = 0; i < qn; i++)
+                        pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
+                }
+                fill += tot;
+            } else {
+                uint32_t at = run + pre;
+                for (uint32_t i = 0; i < qn; i++)
+                    list[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
+            }
+        }
+        run += tot;  // past cap: still counted, the slice is incomplete
+    };
+    // the slice as a buffer resource: a store at an offset past it is dropped, so the
+    // deferred stores below are always the same kPb / 64 instructions (a conditional
+    // store makes the count of stores behind a group's loads unknown to the compiler,
+    // which then waits for all of them, store acks included, before using the loads)
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
     for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
         int4 v[kSsUnroll];
+        const bool whole = t + kWaveTile * kSsUnroll <= e;  // no row past the chunk's end
+        if (whole) {  // (wave-uniform) straight-line loads
 #pragma unroll
-        for (int u = 0; u < kSsUnroll; u++)
-            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+            for (int u = 0; u < kSsUnroll; u++)
+                v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kSsUnroll; u++)
+                v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
+        }
         {  // the previous group's pairs, behind this group's loads
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int k = 0; k < (int)(kPb / 64); k++) {
                 const uint32_t i = (uint32_t)(k * 64 + lane);
-                if (i < pend) list[pend_at + i] = pb[i];
+                __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, i < pend ? (int)((pend_at + i) * 4u) : (int)0x80000000u,
+                                                      0, 0);
             }
             __builtin_amdgcn_wave_barrier();
         }
         const uint32_t grp_at = run;
-        uint32_t fill = 0;   // this group's pairs in pb
-        bool direct = false; // the group outgrew pb: its later tiles store directly
+        fill = 0;
+        direct = false;
 #pragma unroll
         for (int u = 0; u < kSsUnroll; u++) {
             const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
             const int x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            uint32_t qa[4], qn[4], np = 0;
+            bool c[4];
+            uint32_t nc = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                qa[k] = 0;
-                qn[k] = 0;
-                if (row + k < e) {
-                    const int ei = ei_of(x[k], M, s_bkt, s_b);
-                    qa[k] = s_qoff[ei];
-                    qn[k] = s_qoff[ei + 1] - qa[k];
-                    if (qn[k]) atomicAdd(&hist[wave][ei], 1u);
-                }
-                np += qn[k];
+                c[k] = covered(x[k]) && (whole || row + k < e);
+                nc += c[k] ? 1u : 0u;
             }
-            // exclusive prefix of np over the lanes from ballots (np is small: a row is
-            // covered by a few queries), no cross-lane shuffle chain: np < 8 from its
-            // three bits, else from ballots of np >= t
+            // queue the covered rows in row order: exclusive prefix of nc (< 8)
             uint32_t pre = 0, tot = 0;
-            if (!__ballot(np >= 8u)) {
 #pragma unroll
-                for (int bit = 0; bit < 3; bit++) {
-                    const unsigned long long b = __ballot((np >> bit) & 1u);
-                    pre += (uint32_t)__popcll(b & ltmask) << bit;
-                    tot += (uint32_t)__popcll(b) << bit;
-                }
-            } else {
-                for (uint32_t t = 1;; t++) {
-                    const unsigned long long b = __ballot(np >= t);
-                    if (!b) break;
-                    pre += (uint32_t)__popcll(b & ltmask);
-                    tot += (uint32_t)__popcll(b);
-                }
+            for (int bit = 0; bit < 3; bit++) {
+                const unsigned long long bm = __ballot((nc >> bit) & 1u);
+                pre += (uint32_t)__popcll(bm & ltmask) << bit;
+                tot += (uint32_t)__popcll(bm) << bit;
             }
             if (tot == 0) continue;
-            if ((uint64_t)run + tot <= cap) {
-                direct = direct || fill + tot > kPb;
-                const uint32_t r0 = (uint32_t)(row - s);
-                if (!direct) {
-                    uint32_t at = fill + pre;
-                    if (!__ballot(qn[0] > 1u || qn[1] > 1u || qn[2] > 1u || qn[3] > 1u)) {
-                        // one query per covered row (disjoint ranges): straight-line writes
+            uint32_t at = tail + pre;
+            const uint32_t r0 = (uint32_t)(row - s);
 #pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            if (qn[k]) pb[at] = ((uint32_t)(ql_lds ? s_ql[qa[k]] : T.qlist[qa[k]]) << 24) | (r0 + k);
-                            at += qn[k];
-                        }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            for (uint32_t i = 0; i < qn[k]; i++)
-                                pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
-                    }
-                    fill += tot;
-                } else {
-                    uint32_t at = run + pre;
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        for (uint32_t i = 0; i < qn[k]; i++)
-                            list[at++] = ((uint32_t)(ql_lds ? s_ql[qa[k] + i] : T.qlist[qa[k] + i]) << 24) | (r0 + k);
+            for (int k = 0; k < 4; k++) {
+                if (c[k]) {
+                    qv[at] = x[k];
+                    qr[at] = r0 + (uint32_t)k;
+                    at++;
                 }
             }
-            run += tot;  // past cap: still counted, the slice is incomplete
+            tail += tot;
+            __builtin_amdgcn_wave_barrier();
+            if (tail >= 64u) {
+                do {
+                    round(64u);
+                    __builtin_amdgcn_wave_barrier();
+                } while (tail - head >= 64u);
+                // the rest (< 64) to the front: the queue stays linear, no modulo
+                const uint32_t rest = tail - head;
+                int32_t mv = 0;
+                uint32_t mr = 0;
+                if ((uint32_t)lane < rest) mv = qv[head + lane], mr = qr[head + lane];
+                __builtin_amdgcn_wave_barrier();
+                if ((uint32_t)lane < rest) qv[lane] = mv, qr[lane] = mr;
+                __builtin_amdgcn_wave_barrier();
+                head = 0;
+                tail = rest;
+            }
         }
         pend = fill;
         pend_at = grp_at;
     }
+    // the rows still queued: their pairs go straight to the slice, after pb's
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
+    __builtin_amdgcn_wave_barrier();
+    fill = 0;
+    direct = true;
+    while (tail != head) {
+        round(tail - head < 64u ? tail - head : 64u);
+        __builtin_amdgcn_wave_barrier();
+    }
     if (lane == 0) {
         npairs[wc] = run;
         if ((uint64_t)run > cap) atomicOr(overflow, 1u);
@@ -644,7 +743,8 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
                                                       int q, int* const* __restrict__ outs, uint64_t rpb,
-                                                      int32_t base) {
+                                                      int32_t base, const unsigned int* __restrict__ overflow) {
+    if (*overflow) return;  // a slice overflowed: k_ssi_write's column pass writes
     __shared__ uint32_t s_sorted[kSpChunk];
     __shared__ uint32_t s_cnt[kWaves][kMaxQ];
     __shared__ uint32_t s_start[kMaxQ], s_tot[kMaxQ];
@@ -747,34 +847,76 @@ struct SsLayout {
 // EI tables in the workspace: bounds, bucket table, qoff, qab, then qlist
 constexpr size_t kEiBoundsB = (size_t)kEiMax * 4, kEiBucketB = (size_t)kBuckets * 4,
                  kEiQoffB = (size_t)kEiMax * 4, kEiQabB = (size_t)kMaxQ * 4,
-                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2;
-constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiQlistB;
+                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2, kEiCovB = (size_t)kCoarse / 8;
+constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB + kEiQlistB;
 
 SsLayout ss_layout(uint64_t nwc, int q) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     SsLayout L;
     size_t at = 0;
+    // preds, slot, the EI tables and the flag word are one host upload (ss_count)
     L.preds = at;
     at += al((size_t)kMaxQ * sizeof(Pred));
-    L.outs = at;
-    at += al((size_t)kMaxQ * sizeof(int*));
     L.slot = at;
     at += al((size_t)kMaxQ * sizeof(int));
+    L.ei = at;
+    at += al(kEiBytes);
+    L.flag = at;
+    at += 256;
+    L.outs = at;
+    at += al((size_t)kMaxQ * sizeof(int*));
     L.counts = at;
     at += al((size_t)q * nwc * sizeof(uint32_t));
     L.offs = at;
     at += al((size_t)q * nwc * sizeof(unsigned long long));
     L.scratch = at;
     at += al((size_t)scan_u32_scratch_elems((uint64_t)q * nwc) * sizeof(unsigned long long));
-    L.ei = at;
-    at += al(kEiBytes);
-    L.flag = at;
-    at += 256;
     L.npairs = at;
     at += al(nwc * sizeof(uint32_t));
     L.pairs = at;  // pair slices (single pass), when the workspace extends this far
     L.total = at;
     return L;
+}
+
+// Host staging for the uploads (pinned, per thread, device and use: 0 = count's
+// tables, 1 = write's output pointers). A call waits for the previous call's copy
+// out of its buffer (an event recorded behind the copy) before refilling it, so
+// neither count nor write synchronises the stream for its uploads.
+struct Staging {
+    char* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+};
+Staging& staging_slot(int dev, int which) {
+    static thread_local Staging st[kMaxDev][2];
+    return st[dev][which];
+}
+int staging_get(int which, size_t bytes, char** p) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    Staging& S = staging_slot(dev, which);
+    if (S.ev) HIPCHK(hipEventSynchronize(S.ev));
+    else HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    if (S.cap < bytes) {
+        if (S.p) HIPCHK(hipHostFree(S.p));
+        S.p = nullptr;
+        S.cap = 0;
+        HIPCHK(hipHostMalloc((void**)&S.p, bytes, hipHostMallocDefault));
+        S.cap = bytes;
+    }
+    *p = S.p;
+    return MQ_OK;
+}
+// copies the staged bytes to the device and marks the buffer busy until they are out
+int staging_put(int which, void* dst, size_t bytes, hipStream_t st) {
+    int dev;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    Staging& S = staging_slot(dev, which);
+    HIPCHK(hipMemcpyAsync(dst, S.p, bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(S.ev, st));
+    return MQ_OK;
 }
 
 // Pair-slice capacity: one u32 per row of the wave-chunk.
@@ -799,11 +941,12 @@ struct SsState {
     EiMeta meta;
     int32_t base;  // first row number of this (row-shard) column
     bool pairs;    // the count pass listed the pairs (single pass)
+    int slot[kMaxQ];  // kernel index of query i, or -1
 };
 
 // Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
 // the bucket table, written to the workspace's EI region (ss_layout).
-int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, hipStream_t st) {
+int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
     std::vector<long long> L(qk), H(qk), b;
     b.reserve(2 * qk);
     for (int i = 0; i < qk; i++) {
@@ -819,6 +962,7 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, hipStream_t st)
     static thread_local int32_t hb[kEiMax];
     static thread_local uint32_t hbkt[kBuckets], hqoff[kEiMax], hqab[kMaxQ];
     static thread_local uint16_t hql[(size_t)kEiMax * kMaxQ];
+    static thread_local uint32_t hcov[kCoarse / 32];
     for (int j = 0; j < m; j++) hb[j] = (int32_t)b[j];
     std::vector<int> ea(qk), eb(qk);
     for (int i = 0; i < qk; i++) {
@@ -846,17 +990,39 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, hipStream_t st)
         if (hi > bmax) hi = bmax;
         hbkt[k] = (uint32_t)eof(lo) | ((uint32_t)eof(hi) << 16);
     }
-    *meta = EiMeta{m, shift, (int)bmin, (int)bmax};
+    // coverage bitmap: cell c (values bmin + [c, c+1) << cshift) is set when a covered
+    // EI meets it; EI e (1 <= e < m) holds [b[e-1], b[e]), EI m holds [b[m-1], ...)
+    int cshift = 0;
+    while (((bmax - bmin) >> cshift) >= kCoarse) cshift++;
+    {
+        static thread_local int diff[kCoarse + 1];
+        std::fill(diff, diff + kCoarse + 1, 0);
+        for (int e = 1; e <= m; e++) {
+            if (hqoff[e + 1] == hqoff[e]) continue;
+            const long long lo = b[e - 1], hi = e < m ? b[e] - 1 : bmax;
+            diff[(lo - bmin) >> cshift]++;
+            diff[((hi - bmin) >> cshift) + 1]--;
+        }
+        std::fill(hcov, hcov + kCoarse / 32, 0u);
+        int acc = 0;
+        for (int c = 0; c < kCoarse; c++) {
+            acc += diff[c];
+            if (acc > 0) hcov[c >> 5] |= 1u << (c & 31);
+        }
+    }
+    *meta = EiMeta{m, shift, (int)bmin, (int)bmax, cshift};
     size_t o = 0;
-    HIPCHK(hipMemcpyAsync(region + o, hb, (size_t)m * 4, hipMemcpyHostToDevice, st));
+    std::memcpy(region + o, hb, (size_t)m * 4);
     o += kEiBoundsB;
-    HIPCHK(hipMemcpyAsync(region + o, hbkt, kEiBucketB, hipMemcpyHostToDevice, st));
+    std::memcpy(region + o, hbkt, kEiBucketB);
     o += kEiBucketB;
-    HIPCHK(hipMemcpyAsync(region + o, hqoff, (size_t)(m + 2) * 4, hipMemcpyHostToDevice, st));
+    std::memcpy(region + o, hqoff, (size_t)(m + 2) * 4);
     o += kEiQoffB;
-    HIPCHK(hipMemcpyAsync(region + o, hqab, (size_t)qk * 4, hipMemcpyHostToDevice, st));
+    std::memcpy(region + o, hqab, (size_t)qk * 4);
     o += kEiQabB;
-    if (at) HIPCHK(hipMemcpyAsync(region + o, hql, (size_t)at * 2, hipMemcpyHostToDevice, st));
+    std::memcpy(region + o, hcov, kEiCovB);
+    o += kEiCovB;
+    if (at) std::memcpy(region + o, hql, (size_t)at * 2);
     return MQ_OK;
 }
 
@@ -871,6 +1037,8 @@ EiTables ei_tables(char* region) {
     o += kEiQoffB;
     T.qab = reinterpret_cast<const uint32_t*>(region + o);
     o += kEiQabB;
+    T.cov = reinterpret_cast<const uint32_t*>(region + o);
+    o += kEiCovB;
     T.qlist = reinterpret_cast<const uint16_t*>(region + o);
     return T;
 }
@@ -915,12 +1083,15 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     const uint64_t cap = pair_cap(rpb);
     const bool single = n && getenv("MQ_SS_TWOPASS") == nullptr &&
                         ws_bytes >= L.pairs + (size_t)nwc * cap * sizeof(uint32_t) && cap < (1ull << 24);
-    HIPCHK(hipMemsetAsync(w + L.flag, 0, 4, st));
-    HIPCHK(hipMemcpyAsync(w + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(w + L.slot, hslot, sizeof(int) * q, hipMemcpyHostToDevice, st));
-    EiMeta meta{0, 0, 0, 0};
-    if (ei && (rc = ei_build(hp, qk, w + L.ei, &meta, st))) return rc;
-    HIPCHK(hipStreamSynchronize(st));  // the staging arrays are reused by the next call
+    // preds, slot, EI tables and the zeroed flag: one upload from pinned staging
+    char* up = nullptr;
+    if ((rc = staging_get(0, L.outs, &up))) return rc;
+    std::memcpy(up + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1));
+    std::memcpy(up + L.slot, hslot, sizeof(int) * q);
+    std::memset(up + L.flag, 0, 4);
+    EiMeta meta{0, 0, 0, 0, 0};
+    if (ei && (rc = ei_build(hp, qk, up + L.ei, &meta))) return rc;
+    if ((rc = staging_put(0, w, L.outs, st))) return rc;
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
     unsigned long long* offs = reinterpret_cast<unsigned long long*>(w + L.offs);
@@ -964,52 +1135,58 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
                        reinterpret_cast<const int*>(w + L.slot), d_totals, q);
     LAUNCHCHK("k_ss_totals");
-    *state = SsState{g, rpb, q, qk, n, d_col, ei, meta, row_base, single && qk > 0};
+    state->g = g;
+    state->rpb = rpb;
+    state->q = q;
+    state->qk = qk;
+    state->n = n;
+    state->col = d_col;
+    state->ei = ei;
+    state->meta = meta;
+    state->base = row_base;
+    state->pairs = single && qk > 0;
+    std::memcpy(state->slot, hslot, sizeof(int) * q);
     return MQ_OK;
 }
 
 int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_t st) {
     if (S.qk == 0) return MQ_OK;
-    static thread_local int32_t* hout[kMaxQ];
-    static thread_local int hslot[kMaxQ];
     char* w = static_cast<char*>(d_ws);
     const uint64_t nwc = (uint64_t)S.g * kWaves;
     const SsLayout L = ss_layout(nwc, S.qk);
-    HIPCHK(hipMemcpyAsync(hslot, w + L.slot, sizeof(int) * S.q, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    char* hp = nullptr;
+    int rc = staging_get(1, sizeof(int*) * kMaxQ, &hp);
+    if (rc) return rc;
+    int32_t** hout = reinterpret_cast<int32_t**>(hp);
     for (int i = 0; i < S.q; i++)
-        if (hslot[i] >= 0) hout[hslot[i]] = d_pos_out[i];
-    HIPCHK(hipMemcpyAsync(w + L.outs, hout, sizeof(int*) * S.qk, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
+        if (S.slot[i] >= 0) hout[S.slot[i]] = d_pos_out[i];
+    if ((rc = staging_put(1, w + L.outs, sizeof(int*) * S.qk, st))) return rc;
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
     int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
+    const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
     if (S.pairs) {
-        unsigned int of = 0;  // a slice overflowed: the pairs are incomplete, use the column pass
-        HIPCHK(hipMemcpyAsync(&of, w + L.flag, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        if (!of) {
-            hipLaunchKernelGGL(k_ssp_scatter, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
-                               reinterpret_cast<const uint32_t*>(w + L.pairs), pair_cap(S.rpb),
-                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
-                               S.base);
-            LAUNCHCHK("k_ssp_scatter");
-            return MQ_OK;
-        }
+        // the pair scatter, or (a slice overflowed: the pairs are incomplete) the
+        // column pass: both launched, each checks the flag on the device
+        hipLaunchKernelGGL(k_ssp_scatter, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+                           reinterpret_cast<const uint32_t*>(w + L.pairs), pair_cap(S.rpb),
+                           reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
+                           S.base, of);
+        LAUNCHCHK("k_ssp_scatter");
     }
     if (S.ei) {
         const EiTables T = ei_tables(w + L.ei);
         if (aligned16(S.col))
-            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base);
+            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
         else
-            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base);
+            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
         LAUNCHCHK("k_ssi_write");
         return MQ_OK;
     }
     if (aligned16(S.col))
-        hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base);
+        hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
     else
-        hipLaunchKernelGGL(k_ss_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base);
+        hipLaunchKernelGGL(k_ss_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
     LAUNCHCHK("k_ss_write");
     return MQ_OK;
 }
