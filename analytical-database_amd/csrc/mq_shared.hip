@@ -533,15 +533,12 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     if (ql_lds)
         for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
     __syncthreads();
-    const uint32_t span = (uint32_t)M.bmax - (uint32_t)M.bmin;
-    const bool tail_cov = s_qoff[M.m + 1] > s_qoff[M.m];  // values past bmax are in EI m
-    const bool tail_in = tail_cov;
-    auto covered = [&](int32_t v) -> bool {  // branch-free: outside [bmin, bmax] reads word 0
-        const uint32_t d = (uint32_t)v - (uint32_t)M.bmin;
-        const bool in = d <= span;
-        const uint32_t c = in ? d >> M.cshift : 0u;
-        const bool bit = (s_cov[c >> 5] >> (c & 31)) & 1u;
-        return in ? bit : (v > M.bmax && tail_in);
+    // the cell of v - bmin, clamped to the last cell: the host sets every cell past
+    // bmax's (and the last, which values below bmin also reach) to "EI m is covered";
+    // a value below bmin that lands on a set cell only costs a lookup (EI 0 has no query)
+    auto covered = [&](int32_t v) -> bool {
+        const uint32_t c = min(((uint32_t)v - (uint32_t)M.bmin) >> M.cshift, (uint32_t)kCoarse - 1u);
+        return (s_cov[c >> 5] >> (c & 31)) & 1u;
     };
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
@@ -993,7 +990,7 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
     // coverage bitmap: cell c (values bmin + [c, c+1) << cshift) is set when a covered
     // EI meets it; EI e (1 <= e < m) holds [b[e-1], b[e]), EI m holds [b[m-1], ...)
     int cshift = 0;
-    while (((bmax - bmin) >> cshift) >= kCoarse) cshift++;
+    while (((bmax - bmin) >> cshift) >= kCoarse - 1) cshift++;  // the last cell: outside
     {
         static thread_local int diff[kCoarse + 1];
         std::fill(diff, diff + kCoarse + 1, 0);
@@ -1005,9 +1002,11 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
         }
         std::fill(hcov, hcov + kCoarse / 32, 0u);
         int acc = 0;
+        const int cmax = (int)((bmax - bmin) >> cshift);  // bmax's cell
+        const bool tail = hqoff[m + 1] > hqoff[m];       // EI m = [bmax, ...) is covered
         for (int c = 0; c < kCoarse; c++) {
             acc += diff[c];
-            if (acc > 0) hcov[c >> 5] |= 1u << (c & 31);
+            if (acc > 0 || (c > cmax && tail)) hcov[c >> 5] |= 1u << (c & 31);
         }
     }
     *meta = EiMeta{m, shift, (int)bmin, (int)bmax, cshift};
