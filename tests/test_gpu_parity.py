@@ -586,6 +586,56 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
             assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
 
 
+def _inv_fmix32(h):
+    """Inverse of libmq's table hash (the murmur3 finaliser, mq_join.hip hash32), so a
+    test can pick the home slot of every key."""
+    M = np.uint64(0xFFFFFFFF)
+    x = h.astype(np.uint64)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(pow(0xC2B2AE35, -1, 1 << 32))) & M
+    x ^= (x >> np.uint64(13)) ^ (x >> np.uint64(26))
+    x = (x * np.uint64(pow(0x85EBCA6B, -1, 1 << 32))) & M
+    x ^= x >> np.uint64(16)
+    return x.astype(np.uint32).view(np.int32)
+
+
+@pytest.mark.parametrize("dup", [False, True])
+@pytest.mark.parametrize("marks", [True, False])
+def test_hash_join_clustered_window(lib, refcpu, monkeypatch, dup, marks):
+    """One 8192-slot window of the unique table holds a 5000-slot cluster: 5000 keys
+    homed in 16 buckets at its start, so probes of those keys (hits) and of other keys
+    homed there (misses) follow chains of up to ~5000 slots through the per-wave
+    continuation queue (requeued every step, then drained at the end; the in-step
+    drain runs when more than 128 rows wait), with and without the overflow marks.
+    dup: every cluster key twice (the runs table behind the same windowed build)."""
+    if not marks:
+        monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
+    rng = np.random.default_rng(4242)
+    n_rand, n_cl = 295_000, 5000
+    slots = 1 << 20  # the table of ~300K build rows: 2^20 slots, 128 windows of 8192
+    w0 = 7
+    i = np.arange(n_cl, dtype=np.uint64)
+    home = np.uint64(w0 * 8192) + np.uint64(4) * (i % np.uint64(16))
+    h_cl = home | ((i // np.uint64(16)) << np.uint64(20))  # distinct, all homed in 16 buckets
+    h_rand = rng.choice(1 << 32, size=3 * n_rand, replace=False).astype(np.uint64)
+    h_rand = h_rand[((h_rand & np.uint64(slots - 1)) >> np.uint64(13)) != np.uint64(w0)][:n_rand]
+    k_cl, k_rand = _inv_fmix32(h_cl), _inv_fmix32(h_rand)
+    c1 = np.concatenate([k_rand, k_cl, k_cl if dup else k_cl[:0]])
+    c1 = c1[rng.permutation(len(c1))]
+    # probes: cluster hits, misses homed in the cluster's buckets, random hits and misses
+    j = np.arange(3000, dtype=np.uint64)
+    h_miss = (np.uint64(w0 * 8192) + np.uint64(4) * (j % np.uint64(16))) | ((np.uint64(400) + j) << np.uint64(20))
+    c2 = np.concatenate([rng.choice(k_cl, 3000), _inv_fmix32(h_miss), rng.choice(k_rand, 100_000),
+                         rng.integers(-2 ** 31, 2 ** 31 - 1, 50_000, dtype=np.int64).astype(np.int32)])
+    c2 = c2[rng.permutation(len(c2))]
+    p1 = rng.integers(0, 10 ** 7, len(c1), dtype=np.int32)
+    p2 = rng.integers(0, 10 ** 7, len(c2), dtype=np.int32)
+    g1, g2 = _dev_join(lib, c1, p1, c2, p2)
+    w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
+    assert len(w1) >= 3000 * (2 if dup else 1)
+    assert np.array_equal(g1, w1) and np.array_equal(g2, w2)
+
+
 def test_hash_join_scratch_reuse_and_trim(lib, refcpu):
     """Join scratch comes from libmq's caching pool: back-to-back joins of
     different sizes reuse (and outgrow) blocks, mq_trim() releases them, and every
