@@ -1266,6 +1266,52 @@ void jfree_all(mq_join* j) {
 // wherever the line lives, so the atomics themselves have to go.)
 constexpr uint64_t kWindowBuildRows = 1ull << 16;
 
+// Duplicate keys in a strided sample of the build side (a CAS set of the sampled
+// keys): when the sample already has one, the build has many and goes straight to
+// the runs build instead of attempting (and abandoning) the unique table.
+__global__ __launch_bounds__(kTPB) void k_sample_dups(const int* __restrict__ keys, uint64_t stride, uint32_t ns,
+                                                      u64* tab, uint32_t tmask, uint32_t* __restrict__ flag) {
+    for (uint32_t i = blockIdx.x * kTPB + threadIdx.x; i < ns; i += gridDim.x * kTPB) {
+        const uint32_t key = (uint32_t)keys[(uint64_t)i * stride];
+        const u64 w = (u64)key | (1ull << 32);
+        uint32_t h = hash32(key) & tmask;
+        for (uint32_t step = 0; step <= tmask; step++) {
+            const u64 old = atomicCAS(&tab[h], 0ull, w);
+            if (old == 0) break;
+            if (old == w) {
+                *flag = 1;
+                break;
+            }
+            h = (h + 1) & tmask;
+        }
+    }
+}
+
+// 1 when a sample of the build keys holds a duplicate (builds of 2^20 rows and up;
+// MQ_JOIN_SAMPLE=0 turns the check off)
+int sample_has_dups(const int* c1, uint64_t n, uint32_t* dflag, hipStream_t st, const DevState* s, bool* dups) {
+    *dups = false;
+    const char* e = getenv("MQ_JOIN_SAMPLE");
+    if (n < (1ull << 20) || (e && e[0] == '0')) return MQ_OK;
+    constexpr uint32_t kSample = 1u << 18;
+    u64* tab = (u64*)pool_alloc((size_t)2 * kSample * 8);
+    if (!tab) return set_err(MQ_ENOMEM, "join: sample set");
+    HIPCHK(hipMemsetAsync(tab, 0, (size_t)2 * kSample * 8, st));
+    HIPCHK(hipMemsetAsync(dflag + 1, 0, 4, st));
+    hipLaunchKernelGGL(k_sample_dups, dim3(stream_grid(s, kSample)), dim3(kTPB), 0, st, c1, n / kSample, kSample, tab,
+                       2 * kSample - 1, dflag + 1);
+    if (hipGetLastError() != hipSuccess) {
+        pool_free(tab);
+        return set_err(MQ_EHIP, "join: sample launch");
+    }
+    uint32_t f = 0;
+    HIPCHK(hipMemcpyAsync(&f, dflag + 1, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    pool_free(tab);
+    *dups = f != 0;
+    return MQ_OK;
+}
+
 int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
                   uint32_t* general, hipStream_t st, const DevState* s) {
     const Win t = j->win;
@@ -1589,14 +1635,22 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     j->unique = 1;
     if (n1) {
         HIPCHK(hipMemsetAsync(dflag, 0, 4, st));
-        if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s))) {
+        bool sampled = false;
+        if ((rc = sample_has_dups(d_c1, n1, dflag, st, s, &sampled))) {
             jfree_all(j);
             delete j;
             return rc;
         }
-        uint32_t dup = 0;
-        HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        uint32_t dup = sampled ? 1u : 0u;
+        if (!sampled) {
+            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s))) {
+                jfree_all(j);
+                delete j;
+                return rc;
+            }
+            HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
         if (dup) {  // general path: stable sort by key, runs in insertion order
             j->unique = 0;
             j->bpos = d_p1;

@@ -682,11 +682,16 @@ def test_hash_join_goldens(lib, refcpu, goldens):
 
 
 @pytest.mark.parametrize("runs", [True, False])
-def test_hash_join_dup_goldens(lib, refcpu, goldens, monkeypatch, runs):
+@pytest.mark.parametrize("sample", [True, False])
+def test_hash_join_dup_goldens(lib, refcpu, goldens, monkeypatch, runs, sample):
     """Many-to-many config 5 (every build key twice, tests/golden/make_join_dup_goldens.py):
-    the duplicate-key build path against the reference's own hash_join."""
+    the duplicate-key build path against the reference's own hash_join. sample: builds
+    of 2^20 rows and up go straight to the runs build when a sample of the keys has a
+    duplicate; MQ_JOIN_SAMPLE=0: the unique attempt first, abandoned on the duplicate."""
     if not runs:
         monkeypatch.setenv("MQ_JOIN_RUNS", "0")
+    if not sample:
+        monkeypatch.setenv("MQ_JOIN_SAMPLE", "0")
     for r in goldens["join_dup"]:
         m, h = _join_golden(lib, refcpu, r["n"], dup=True)
         assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"]), r["n"]
