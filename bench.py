@@ -573,8 +573,9 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
 
 
 def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:
-    """S11 shared_select on the 1e9-row column: Q range queries of 0.1 % each, two
-    passes (count + write) vs Q separate ordered selects."""
+    """S11 shared_select on the 1e9-row column: Q range queries of 0.1 % each,
+    count + write (the host gets the counts in between, as the query API does) vs Q
+    separate ordered selects; outputs allocated once, medians of repeated runs."""
     import numpy as np
     sp = mq.stream_of(stream)
     res = {}
@@ -588,25 +589,36 @@ def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:
         with torch.cuda.stream(stream):
             ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
             k = (C.c_uint64 * q)()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
+            # one untimed call sizes the outputs (the caller's allocation is not the
+            # operator's work) and takes the first-call setup; then count + write,
+            # median of 5, each ending in a device sync
             mq.check(lib.mq_shared_select_count(col.data_ptr(), n, lo_c, hi_c, q, k, ws.data_ptr(), wsb, sp))
             outs = [torch.empty(max(int(x), 1), dtype=torch.int32, device=dev) for x in k]
             ptrs = (C.c_void_p * q)(*[o.data_ptr() for o in outs])
             mq.check(lib.mq_shared_select_write(ws.data_ptr(), ptrs, sp))
-            torch.cuda.synchronize()
-            t1 = time.perf_counter() - t0
-            # the same with q separate ordered selects
+            ts = []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                mq.check(lib.mq_shared_select_count(col.data_ptr(), n, lo_c, hi_c, q, k, ws.data_ptr(), wsb, sp))
+                mq.check(lib.mq_shared_select_write(ws.data_ptr(), ptrs, sp))
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            t1 = statistics.median(ts)
+            # the same with q separate ordered selects (median of 3)
             sws = lib.mq_scan_workspace_bytes(n)
             ws2 = torch.empty(sws, dtype=torch.uint8, device=dev)
             cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for j in range(q):
-                mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, int(lows[j]), 1, int(highs[j]),
-                                                 outs[j].data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
-            torch.cuda.synchronize()
-            t2 = time.perf_counter() - t0
+            ts = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for j in range(q):
+                    mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, int(lows[j]), 1, int(highs[j]),
+                                                     outs[j].data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            t2 = statistics.median(ts)
             del outs, ws, ws2
         res[f"q{q}"] = {"ms_shared": 1e3 * t1, "ms_q_separate_selects": 1e3 * t2,
                         "rows_x_queries_per_s": n * q / t1, "k_total": int(sum(k))}
