@@ -732,17 +732,27 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     }
 }
 
-constexpr int kSpChunk = 2048;                  // pairs sorted in LDS at a time
-constexpr int kSpPerWave = kSpChunk / kWaves;   // 512: 8 rounds of 64
+constexpr int kSpChunk = 4096;                  // pairs sorted in LDS at a time
+constexpr int kSpPerWave = kSpChunk / kWaves;   // 1024: 16 rounds of 64
 constexpr int kSpRounds = kSpPerWave / 64;
+constexpr int kSpBatch = 4;                     // rounds whose pairs are loaded together
+constexpr int kSpPer = kSpChunk / kTPB;         // entries each thread places
 
+// Ranks go to LDS as they are made (the pair itself in s_buf, its rank among the
+// wave's earlier pairs of its query in s_loc), not into registers held across the
+// block's scan: 2048-pair chunks held that way needed 102 VGPRs, and 4096 / 8192
+// 144 / 225. The placement reads a thread's entries, syncs, and writes them sorted
+// into the same s_buf. Longer chunks make longer runs per query in the output
+// (≈ 27 entries at Q = 150 instead of ≈ 14), fewer partial lines: 0.55 -> 0.52 ms
+// at Q = 150 on 1e9 rows; 8192-pair chunks (2 waves per SIMD) took 0.77 ms.
 __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict__ pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
                                                       int q, int* const* __restrict__ outs, uint64_t rpb,
                                                       int32_t base, const unsigned int* __restrict__ overflow) {
     if (*overflow) return;  // a slice overflowed: k_ssi_write's column pass writes
-    __shared__ uint32_t s_sorted[kSpChunk];
+    __shared__ uint32_t s_buf[kSpChunk];
+    __shared__ uint16_t s_loc[kSpChunk];
     __shared__ uint32_t s_cnt[kWaves][kMaxQ];
     __shared__ uint32_t s_start[kMaxQ], s_tot[kMaxQ];
     __shared__ unsigned long long s_run[kMaxQ];
@@ -761,24 +771,28 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
     for (uint32_t c0 = 0; c0 < np; c0 += kSpChunk) {
         for (int i = tid; i < kWaves * kMaxQ; i += kTPB) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
-        // this wave's 512 pairs of the chunk, loaded first, then ranked round by round
-        uint32_t x[kSpRounds], loc[kSpRounds];
+        // this wave's 1024 pairs of the chunk, kSpBatch rounds' loads at a time
+        for (int r0 = 0; r0 < kSpRounds; r0 += kSpBatch) {
+            uint32_t x[kSpBatch];
 #pragma unroll
-        for (int r = 0; r < kSpRounds; r++) {
-            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
-            x[r] = idx < np ? list[idx] : 0u;
-        }
+            for (int b = 0; b < kSpBatch; b++) {
+                const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
+                x[b] = idx < np ? list[idx] : 0u;
+            }
 #pragma unroll
-        for (int r = 0; r < kSpRounds; r++) {
-            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
-            const bool valid = idx < np;
-            const uint32_t qid = x[r] >> 24;
-            const unsigned long long peers = match_any8(qid, __ballot(valid));
-            const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
-            loc[r] = before + (uint32_t)__popcll(peers & ltmask);
-            __builtin_amdgcn_wave_barrier();
-            if (valid && (peers & ~ltmask & ~(1ull << lane)) == 0) s_cnt[wave][qid] = before + (uint32_t)__popcll(peers);
-            __builtin_amdgcn_wave_barrier();
+            for (int b = 0; b < kSpBatch; b++) {
+                const uint32_t li = (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
+                const bool valid = c0 + li < np;
+                const uint32_t qid = x[b] >> 24;
+                const unsigned long long peers = match_any8(qid, __ballot(valid));
+                const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
+                s_buf[li] = x[b];
+                s_loc[li] = (uint16_t)(before + (uint32_t)__popcll(peers & ltmask));
+                __builtin_amdgcn_wave_barrier();
+                if (valid && (peers & ~ltmask & ~(1ull << lane)) == 0)
+                    s_cnt[wave][qid] = before + (uint32_t)__popcll(peers);
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         __syncthreads();
         // bucket starts: queries in order, waves in order inside a query
@@ -809,15 +823,21 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
             }
         }
         __syncthreads();
+        const uint32_t cn = np - c0 < (uint32_t)kSpChunk ? np - c0 : (uint32_t)kSpChunk;
+        uint32_t px[kSpPer], pd[kSpPer];
 #pragma unroll
-        for (int r = 0; r < kSpRounds; r++) {
-            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
-            if (idx < np) s_sorted[s_cnt[wave][x[r] >> 24] + loc[r]] = x[r];
+        for (int k = 0; k < kSpPer; k++) {
+            const uint32_t i = (uint32_t)(k * kTPB + tid);
+            px[k] = s_buf[i];
+            pd[k] = i < cn ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
         }
         __syncthreads();
-        const uint32_t cn = np - c0 < (uint32_t)kSpChunk ? np - c0 : (uint32_t)kSpChunk;
+#pragma unroll
+        for (int k = 0; k < kSpPer; k++)
+            if (pd[k] != 0xFFFFFFFFu) s_buf[pd[k]] = px[k];
+        __syncthreads();
         for (uint32_t i = tid; i < cn; i += kTPB) {
-            const uint32_t y = s_sorted[i], qid = y >> 24;
+            const uint32_t y = s_buf[i], qid = y >> 24;
             s_out[qid][s_run[qid] + (i - s_start[qid])] = (int)(row0 + (y & 0xFFFFFFu)) + base;
         }
         __syncthreads();
