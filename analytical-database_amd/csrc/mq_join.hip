@@ -789,9 +789,15 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
                                                     u64* __restrict__ words, Win t,
                                                     uint32_t* __restrict__ general) {
     __shared__ u64 tab[1 << kWinLog];
+    // A full bucket records in its slot order whether any key homed there went on
+    // past it (then key(slot 0) > key(slot 1), else <; the keys are distinct), so a
+    // probe that misses in a full bucket without overflow ends there (bucket_ovf).
+    // An insert that lands outside its home bucket marks that bucket.
+    __shared__ uint8_t ovf[(1 << kWinLog) / kBucket];
     const uint32_t W = (uint32_t)t.wmask + 1;
     const uint32_t w = blockIdx.x;
     for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) tab[x] = kEmpty;
+    for (uint32_t x = threadIdx.x; x < W / kBucket; x += kWinTPB) ovf[x] = 0;
     __syncthreads();
     const uint32_t b = wstart[w], e = wstart[w + 1];
     if (e - b > W - W / 4) {  // over 3/4 full: probes would run long (adversarial keys)
@@ -815,10 +821,14 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
                 continue;
             }
             const uint32_t key = (uint32_t)v;
-            uint32_t h = (uint32_t)ht_home(key, t.wmask);
+            const uint32_t h0 = (uint32_t)ht_home(key, t.wmask);
+            uint32_t h = h0;
             for (uint32_t step = 0; step < W; step++) {
                 const u64 old = atomicCAS(&tab[h], kEmpty, v);
-                if (old == kEmpty) break;
+                if (old == kEmpty) {
+                    if (step >= kBucket) ovf[h0 / kBucket] = 1;
+                    break;
+                }
                 if ((uint32_t)old == key) {
                     *general = 1;
                     break;
@@ -826,20 +836,6 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
                 h = (h + 1) & (W - 1);
             }
         }
-    }
-    __syncthreads();
-    // A full bucket records in its slot order whether any key homed there went on
-    // past it (then key(slot 0) > key(slot 1), else <; the keys are distinct), so a
-    // probe that misses in a full bucket without overflow ends there (bucket_ovf).
-    // One pass over the slots: a key outside its home bucket marks that bucket.
-    __shared__ uint8_t ovf[(1 << kWinLog) / kBucket];
-    for (uint32_t x = threadIdx.x; x < W / kBucket; x += kWinTPB) ovf[x] = 0;
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) {
-        const u64 v = tab[x];
-        if (v == kEmpty) continue;
-        const uint32_t hb = (uint32_t)ht_home((uint32_t)v, t.wmask) / kBucket;
-        if (hb != x / kBucket) ovf[hb] = 1;
     }
     __syncthreads();
     for (uint32_t bk = threadIdx.x; bk < W / kBucket; bk += kWinTPB) {
@@ -853,12 +849,8 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
     for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) dst[x] = tab[x];
 }
 
-// kProbeILP probes per thread per step: the keys are loaded coalesced, then all
-// their home buckets (4 slots, 32 B, two 16-byte loads) are requested before any
-// is examined. Only a full bucket without the key continues along the window,
-// slot by slot. With whole-bucket loads 2 probes per thread beat 8 (8.25 vs
-// 8.8 ms at 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8
-// had beaten 1 (7.9 vs 8.4 ms).
+// 2 probes per thread per step: with whole-bucket loads 2 beat 8 (8.25 vs 8.8 ms at
+// 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8 had beaten 1.
 constexpr int kProbeILP = 2;
 constexpr uint32_t kContCap = 320;  // queued continuations per wave (64 taken + 2 x 128 new fit)
 
