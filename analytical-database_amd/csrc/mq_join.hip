@@ -1157,29 +1157,96 @@ __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict_
 // ---- duplicate keys as runs (the build sorted by key, stable: a key's rows are one
 // run in insertion order); the distinct keys go into the windowed unique table with
 // their run index as payload ----
-__global__ __launch_bounds__(kTPB) void k_run_flags(const uint32_t* __restrict__ skeys, uint64_t n,
-                                                    uint32_t* __restrict__ head) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride)
-        head[i] = (i == 0 || skeys[i - 1] != skeys[i]) ? 1u : 0u;
+// Runs of the key-sorted build in two passes over the keys: k_run_count counts the
+// run heads (a row whose key differs from the row before) per 4096-row tile, an
+// exclusive scan of those counts gives each tile its first run, and k_run_emit
+// ranks the heads inside the tile (each thread 16 consecutive rows, a block scan of
+// the per-thread counts) and writes run r's key dk[r] (unflipped) and first sorted
+// row rs[r]; rs[R] = n. k_run_payload then gives every run its payload rid[r]. (Was: a head flag per row, a scan of
+// 2^28 flags into 8-byte ranks and a compaction: ≈ 10 GB of traffic, 2.2 ms.)
+constexpr int kRunPer = 16;
+constexpr uint64_t kRunTile = (uint64_t)kTPB * kRunPer;  // 4096
+
+__device__ __forceinline__ uint32_t run_heads16(const uint32_t* __restrict__ skeys, uint64_t n, uint64_t i0,
+                                                uint32_t (&k)[kRunPer]) {
+    // bit m set <=> row i0 + m (< n) starts a run; k[] = the 16 keys
+    uint32_t prev = i0 ? skeys[i0 - 1] : 0u, bits = 0;
+    if (i0 + kRunPer <= n) {
+        const uint4* q = reinterpret_cast<const uint4*>(skeys + i0);
+#pragma unroll
+        for (int v = 0; v < kRunPer / 4; v++) {
+            const uint4 x = q[v];
+            k[4 * v] = x.x, k[4 * v + 1] = x.y, k[4 * v + 2] = x.z, k[4 * v + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < kRunPer; m++) k[m] = i0 + m < n ? skeys[i0 + m] : 0u;
+    }
+#pragma unroll
+    for (int m = 0; m < kRunPer; m++) {
+        if (i0 + m < n && (i0 + m == 0 || k[m] != prev)) bits |= 1u << m;
+        prev = k[m];
+    }
+    return bits;
 }
 
-// run r (= its head's exclusive rank): key dk[r] (unflipped), first sorted row rs[r],
-// payload rid[r] = r; rs[R] = n
-__global__ __launch_bounds__(kTPB) void k_run_compact(const uint32_t* __restrict__ skeys, uint64_t n,
-                                                      const uint32_t* __restrict__ head, const u64* __restrict__ rank,
-                                                      int* __restrict__ dk, uint32_t* __restrict__ rs,
-                                                      int* __restrict__ rid) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        if (head[i]) {
-            const u64 r = rank[i];
-            dk[r] = (int)(skeys[i] ^ 0x80000000u);
-            rs[r] = (uint32_t)i;
-            rid[r] = (int)r;
-        }
-        if (i == n - 1) rs[rank[i] + head[i]] = (uint32_t)n;
+__global__ __launch_bounds__(kTPB) void k_run_count(const uint32_t* __restrict__ skeys, uint64_t n,
+                                                    uint32_t* __restrict__ tcount) {
+    __shared__ uint32_t s_w[kTPB / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kRunTile + (uint64_t)threadIdx.x * kRunPer;
+    uint32_t k[kRunPer];
+    uint32_t c = i0 < n ? (uint32_t)__popc(run_heads16(skeys, n, i0, k)) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kTPB / 64; w++) t += s_w[w];
+        tcount[blockIdx.x] = t;
     }
+}
+
+// (the heads go through LDS: written straight from the ranks, a wave's stores
+// scattered over ~2 KB, the emit took 1.03 ms at 2^28)
+__global__ __launch_bounds__(kTPB) void k_run_emit(const uint32_t* __restrict__ skeys, uint64_t n,
+                                                   const u64* __restrict__ toff, int* __restrict__ dk,
+                                                   uint32_t* __restrict__ rs) {
+    __shared__ uint32_t s_w[kTPB / 64];
+    __shared__ uint32_t s_dk[kRunTile], s_rs[kRunTile];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t i0 = (uint64_t)blockIdx.x * kRunTile + (uint64_t)threadIdx.x * kRunPer;
+    uint32_t k[kRunPer];
+    const uint32_t bits = i0 < n ? run_heads16(skeys, n, i0, k) : 0u;
+    const uint32_t c = (uint32_t)__popc(bits);
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t at = incl - c, tot = 0;
+    for (int w = 0; w < kTPB / 64; w++) {
+        if (w < wave) at += s_w[w];
+        tot += s_w[w];
+    }
+#pragma unroll
+    for (int m = 0; m < kRunPer; m++) {
+        if (bits & (1u << m)) {
+            s_dk[at] = k[m] ^ 0x80000000u;
+            s_rs[at] = (uint32_t)(i0 + m);
+            at++;
+        }
+    }
+    __syncthreads();
+    const u64 r0 = toff[blockIdx.x];
+    for (uint32_t x = threadIdx.x; x < tot; x += kTPB) {
+        dk[r0 + x] = (int)s_dk[x];
+        rs[r0 + x] = s_rs[x];
+    }
+    if (i0 < n && n - i0 <= (uint64_t)kRunPer) rs[r0 + tot] = (uint32_t)n;  // the block holding row n-1
 }
 
 // The table payload of run r: (start << 4) | length for runs shorter than 15 rows
@@ -1381,25 +1448,26 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
                const DevState* s) {
     const char* e = getenv("MQ_JOIN_RUNS");  // "0": the global-CAS run table (A/B, tests)
     if (e && e[0] == '0') return 1;
-    uint32_t* head = (uint32_t*)pool_alloc(n * 4);
-    u64* rank = (u64*)pool_alloc(n * 8);
-    u64* scratch = (u64*)pool_alloc(scan_scratch_elems(n) * 8);
+    const uint64_t ntiles = ceil_div(n, kRunTile);
+    uint32_t* tcount = (uint32_t*)pool_alloc(ntiles * 4);
+    u64* toff = (u64*)pool_alloc(ntiles * 8);
+    u64* scratch = (u64*)pool_alloc(scan_scratch_elems(ntiles) * 8);
     auto fail = [&](int rc) {
-        pool_free(head);
-        pool_free(rank);
+        pool_free(tcount);
+        pool_free(toff);
         pool_free(scratch);
         return rc;
     };
-    if (!head || !rank || !scratch) return fail(set_err(MQ_ENOMEM, "join: run buffers"));
-    hipLaunchKernelGGL(k_run_flags, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, skeys, n, head);
-    int rc = scan_exclusive<uint32_t>(head, rank, n, scratch, st);
+    if (!tcount || !toff || !scratch) return fail(set_err(MQ_ENOMEM, "join: run buffers"));
+    hipLaunchKernelGGL(k_run_count, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, skeys, n, tcount);
+    int rc = scan_exclusive<uint32_t>(tcount, toff, ntiles, scratch, st);
     if (rc) return fail(rc);
     u64 last = 0;
-    uint32_t lasth = 0;
-    HIPCHK(hipMemcpyAsync(&last, rank + (n - 1), 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&lasth, head + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    uint32_t lastc = 0;
+    HIPCHK(hipMemcpyAsync(&last, toff + (ntiles - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&lastc, tcount + (ntiles - 1), 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const uint64_t R = last + lasth;
+    const uint64_t R = last + lastc;
     int* dk = (int*)pool_alloc(R * 4);
     int* rid = (int*)pool_alloc(R * 4);
     uint32_t* rs = nullptr;
@@ -1408,7 +1476,7 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
         pool_free(rid);
         return fail(rc ? rc : set_err(MQ_ENOMEM, "join: run keys"));
     }
-    hipLaunchKernelGGL(k_run_compact, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, skeys, n, head, rank, dk, rs, rid);
+    hipLaunchKernelGGL(k_run_emit, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, skeys, n, toff, dk, rs);
     hipLaunchKernelGGL(k_run_payload, dim3(stream_grid(s, R)), dim3(kTPB), 0, st, rs, R, n <= (1ull << 28), rid);
     if (hipGetLastError() != hipSuccess) rc = set_err(MQ_EHIP, "join: run compaction");
     uint32_t flag = 0;
