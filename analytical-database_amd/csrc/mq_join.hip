@@ -4,19 +4,22 @@
 // (build position, probe position) in probe-major order and, for one probe row,
 // in build-insertion order.
 //
-// Build (one of two paths):
-//   * unique keys (the common FK case, and config 5): every build row CAS-inserts
-//     one 64-bit word {key, build position} into an open-addressing table (linear
-//     probing, power-of-two size >= 2 x rows, all-ones = empty). A second sighting
-//     of a key (or a row equal to the empty word) raises a flag and the build
-//     restarts on the general path.
-//   * duplicate keys: a stable LSD radix sort of (key, position) pairs makes each
-//     key's rows one contiguous run in insertion order; run heads insert
-//     key -> run start and run tails store the run length.
-// Probe: one lookup per probe row -> (start, len) (unique table: the build
-// position itself, len 0/1); an exclusive scan of len gives each probe row's
-// output offset; the write kernel copies the run.
-// No CPU work per row anywhere; the host only reads back the duplicate flag and M.
+// Build:
+//   * unique keys (the FK case, and config 5): one 64-bit word {key, build
+//     position} per slot of an open-addressing table (4-slot buckets, linear
+//     probing inside 8192-slot windows, all-ones = empty). Above 2^16 rows the
+//     rows are radix-partitioned by window and each window is built in LDS by one
+//     block (k_win_build), which also leaves overflow marks in full buckets' slot
+//     order. A second sighting of a key, or the empty word, raises a flag.
+//   * duplicate keys (a sampled duplicate check decides up front for 2^20 rows and
+//     up, else the flag): a stable LSD radix sort of (key, position) makes each
+//     key's rows one run in insertion order; the runs' distinct keys go into the
+//     same windowed table with the run (start, length) packed as payload.
+// Probe: one 32-byte bucket read per probe row; continuations past a full bucket
+// ride along in later steps through a per-wave LDS queue. Unique table: a payload
+// and one hit word per 64 rows, then a scan of the hit words; runs: each row's
+// (start, length), then a scan of the lengths. The write kernels copy the pairs.
+// No CPU work per row anywhere; the host reads back only the flags and M.
 
 #include <hip/hip_runtime.h>
 
@@ -34,7 +37,7 @@ using namespace mqi;
 constexpr int kTPB = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kTPB * kScanItems;  // 4096
-constexpr int kSortItems = 16;  // 8: 36.3 ms, 32: 40.5 ms for the 1e9-row index (16: 31.2)
+constexpr int kSortItems = 16;  // words per thread of a sort tile (8 and 32 measured slower)
 constexpr int kSortTile = kTPB * kSortItems;  // 4096
 constexpr int kRadix = 256;
 constexpr int kSortTPB = 512;  // sort tile = kSortTPB x kSortItems words (radix_sort_tiles)
