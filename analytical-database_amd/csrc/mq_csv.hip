@@ -34,6 +34,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -219,12 +220,15 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-    }
+// Inclusive sum over the wave by DPP (row shifts within 16 lanes, then the row
+// broadcasts of lanes 15 and 31): 6 adds instead of 6 ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return v;
 }
 
@@ -619,6 +623,154 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
     return (int32_t)(neg ? 0u - v : v);
 }
 
+// ---- pass 2, token-parallel form (the usual text): every row is ncols tokens
+// [-]digits{0..10}, ',' between them and '\n' after the last, no line over 1023
+// bytes. Then token t of the chunk is the text between separators t and t+1 of the
+// chunk's list, counted from the '\n' that ends the previous chunk's last row, and
+// it belongs to row t / ncols, column t % ncols. So:
+//   * every lane classifies 68 staged bytes: a byte below '-' (0x2D) is a candidate
+//     separator ('\n' and ',' are; digits and '-' are not): 4 ops a word, and the
+//     flag bytes become a bit mask by v_dot4 with weights 1, 2, 4, 8 (16, ..., 128);
+//   * the candidates' LDS offsets are listed in text order (one block scan of the
+//     counts); wave 0 also finds the first '\n' of the chunk (entry f0);
+//   * lane i takes tokens i, i + S, ... with S the largest multiple of ncols up to
+//     256, so its column is fixed: one pointer, one min and one max per lane. The
+//     token's bytes are its two list entries apart; the 12 bytes ending at the
+//     separator are read from LDS, bytes before the digits become '0', and the
+//     value is digits4 of three words (next_token_nl's arithmetic).
+// Each token checks its own separator byte exactly (',' or, for the last column,
+// '\n') and its digits; together with the candidate list (every ',' and '\n' is a
+// candidate) that proves the chunk is R rows of the fast form. Anything else (a
+// space, '+', '\r', a missing or extra token, 11+ digits, a NUL) makes the block
+// return false before anything but its own rows' columns was written; the row-wise
+// parse then rewrites those rows.
+constexpr int kTokSeg = (kChunk + kHalo) / kTPB;  // 68 bytes classified per lane
+constexpr int kTokMaxCols = 16;
+static_assert(kTokSeg % 4 == 0 && kTokSeg >= 64 && kTokSeg < 64 + 32, "classification in words");
+
+__device__ __forceinline__ uint32_t below_2d(uint32_t x) {  // 0x80 in each byte < 0x2D
+    return ~(((x | 0x80808080u) - 0x2D2D2D2Du) | x) & 0x80808080u;
+}
+
+__device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __restrict__ list,
+                                   uint32_t* s_u, int* s_f0, int* s_mm, uint4* s_lead, uint64_t r0, uint32_t R,
+                                   int ncols, int32_t* const* __restrict__ cols) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int base = kPre + tid * kTokSeg;
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(s + base);
+    constexpr int kW = kTokSeg / 4;
+    uint32_t f[kW];
+#pragma unroll
+    for (int k = 0; k < kW; k++) f[k] = below_2d(d[k]);
+    unsigned long long m = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const uint32_t lo = __builtin_amdgcn_udot4(f[4 * g + 1], 0x80402010u,
+                                                   __builtin_amdgcn_udot4(f[4 * g], 0x08040201u, 0u, false), false);
+        const uint32_t hi = __builtin_amdgcn_udot4(f[4 * g + 3], 0x80402010u,
+                                                   __builtin_amdgcn_udot4(f[4 * g + 2], 0x08040201u, 0u, false), false);
+        m |= (unsigned long long)((lo | (hi << 8)) >> 7) << (16 * g);
+    }
+    uint32_t mt = 0;  // the words past the first 64 bytes
+#pragma unroll
+    for (int k = 16; k < kW; k++) mt |= (__builtin_amdgcn_udot4(f[k], 0x08040201u, 0u, false) >> 7) << (4 * (k - 16));
+    const bool pre = tid == 0 && s[kPre - 1] == '\n';  // byte cs-1: a row starts at cs
+    if (tid == 0) *s_f0 = INT_MAX;
+    if (tid < 13) {  // s_lead[z]: byte masks of a 12-byte window that clear its first z bytes
+        const uint32_t z8 = 8u * (uint32_t)tid;
+        const uint64_t m01 = z8 >= 64u ? 0ull : (~0ull << z8);
+        s_lead[tid] = make_uint4((uint32_t)m01, (uint32_t)(m01 >> 32),
+                                 z8 >= 96u ? 0u : (uint32_t)(0xFFFFFFFFull << (z8 > 64u ? z8 - 64u : 0u)), 0u);
+    }
+    uint32_t ntot;
+    uint32_t o = block_excl_sum((uint32_t)(__popcll(m) + __popc(mt) + (pre ? 1 : 0)), s_u, &ntot);
+    if (ntot > (uint32_t)kList) return false;
+    int first_nl = INT_MAX;
+    if (pre) first_nl = (int)o, list[o++] = (uint16_t)(kPre - 1);
+    // (three 32-bit loops: a 64-bit find-first and clear cost twice the VALU)
+    uint32_t mw[3] = {(uint32_t)m, (uint32_t)(m >> 32), mt};
+#pragma unroll
+    for (int h = 0; h < 3; h++) {
+        uint32_t x = mw[h];
+        while (x) {
+            const int p = base + 32 * h + __builtin_ctz(x);
+            if (wave == 0 && first_nl == INT_MAX && s[p] == '\n') first_nl = (int)o;
+            list[o++] = (uint16_t)p;
+            x &= x - 1;
+        }
+    }
+    if (wave == 0) {
+        const int f = wave_min_i(first_nl);
+        if (lane == 0 && f != INT_MAX) atomicMin(s_f0, f);
+    }
+    __syncthreads();
+    const int f0 = *s_f0;
+    const uint32_t T = R * (uint32_t)ncols;
+    if (f0 == INT_MAX || (uint64_t)f0 + T >= ntot) return false;
+
+    const uint32_t S = (uint32_t)(kTPB - kTPB % ncols);
+    bool bad = false;
+    int mn = INT_MAX, mx = INT_MIN;
+    int col = 0;
+    if ((uint32_t)tid < S) {
+        col = tid % ncols;
+        const uint32_t expect = col == ncols - 1 ? (uint32_t)'\n' : (uint32_t)',';
+        gint32* cp = global_ptr(cols[col]) + r0;
+        const uint32_t rstep = S / (uint32_t)ncols;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
+        const uint16_t* lt = list + f0;
+        uint32_t rr = (uint32_t)tid / (uint32_t)ncols;
+        for (uint32_t t = (uint32_t)tid; t < T; t += S, rr += rstep) {
+            const uint32_t pb = lt[t], pe = lt[t + 1];  // the separators before / after the token
+            const uint32_t L = pe - pb - 1u;
+            const uint32_t neg = s[pb + 1] == '-' ? 1u : 0u;  // (L == 0: that byte is the separator)
+            const uint32_t Ld = L - neg;                        // digits
+            const uint4 mk = s_lead[12u - min(Ld, 12u)];       // keeps the last Ld bytes of 12
+            const uint32_t b = pe - 12u;                        // >= kPre - 12
+            const uint32_t a2 = b >> 2, r2 = pe & 3u;
+            const uint32_t e0 = w[a2], e1 = w[a2 + 1], e2 = w[a2 + 2], e3 = w[a2 + 3];
+            // digit values: byte ^ '0' (no borrows: a digit byte is 0x30 | d), the bytes
+            // before the digits cleared; a byte that is not a digit gives a value > 9
+            const uint32_t d0 = (__builtin_amdgcn_alignbyte(e1, e0, r2) ^ 0x30303030u) & mk.x;
+            const uint32_t d1 = (__builtin_amdgcn_alignbyte(e2, e1, r2) ^ 0x30303030u) & mk.y;
+            const uint32_t d2 = (__builtin_amdgcn_alignbyte(e3, e2, r2) ^ 0x30303030u) & mk.z;
+            const uint32_t nd = ((d0 + 0x76767676u) | d0 | (d1 + 0x76767676u) | d1 | (d2 + 0x76767676u) | d2) &
+                                0x80808080u;
+            bad |= (s[pe] != expect) | (Ld > 10u) | (nd != 0u);
+            // 12 digits (at most the last 10 nonzero): pairs by v_dot4, then
+            // ((p1 * 10^4 + B) * 10^4 + C) mod 2^32 in 24-bit mads
+            const uint32_t p1 = __builtin_amdgcn_udot4(d0, 0x010A0000u, 0u, false) & 0xFFu;
+            const uint32_t hb = __builtin_amdgcn_udot4(d1, 0x0000010Au, 0u, false) & 0xFFu;
+            const uint32_t lb = __builtin_amdgcn_udot4(d1, 0x010A0000u, 0u, false) & 0xFFu;
+            const uint32_t hc = __builtin_amdgcn_udot4(d2, 0x0000010Au, 0u, false) & 0xFFu;
+            const uint32_t lc = __builtin_amdgcn_udot4(d2, 0x010A0000u, 0u, false) & 0xFFu;
+            uint32_t hi = p1 * 10000u + hb * 100u + lb;  // < 2^24
+            asm volatile("" : "+v"(hi));                 // (keeps the next product 24-bit)
+            const uint32_t v = (hi & 0xFFFFFFu) * 10000u + (hc * 100u + lc);
+            const int32_t y = (int32_t)(neg ? 0u - v : v);
+            cp[rr] = y;
+            mn = min(mn, y);
+            mx = max(mx, y);
+        }
+    }
+    if (__syncthreads_or(bad)) return false;
+    if (64 % ncols == 0) {  // lanes l and l + ncols hold one column
+        for (int o2 = 32; o2 >= ncols; o2 >>= 1) {
+            mn = min(mn, __shfl_xor(mn, o2, 64));
+            mx = max(mx, __shfl_xor(mx, o2, 64));
+        }
+        if (lane < ncols) {
+            atomicMin(&s_mm[2 * col], mn);
+            atomicMax(&s_mm[2 * col + 1], mx);
+        }
+    } else if ((uint32_t)tid < S) {
+        atomicMin(&s_mm[2 * col], mn);
+        atomicMax(&s_mm[2 * col + 1], mx);
+    }
+    return true;
+}
+
 // ---- pass 2: parse. One block per chunk. The chunk's row starts stay as one
 // 64-bit mask per thread segment plus the exclusive prefix of their counts; lane i
 // takes pieces i, i+256, ... and finds piece i's byte by a binary search over the
@@ -629,13 +781,15 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
                                                      const long long* __restrict__ prev, int ncols,
                                                      int32_t* const* __restrict__ cols,
                                                      int2* __restrict__ partial, uint16_t* __restrict__ nf,
-                                                     unsigned* flags) {
+                                                     unsigned* flags, uint64_t rows, int tok) {
     __shared__ __attribute__((aligned(16))) uint8_t s[kLds + 32];  // + token_fast's over-read
     __shared__ unsigned long long s_mask[kTPB];
     __shared__ uint16_t s_list[kList];
     __shared__ uint32_t s_off[kTPB];
     __shared__ long long s_w[kWaves];
     __shared__ uint32_t s_u[kWaves];
+    __shared__ int s_f0;
+    __shared__ uint4 s_lead[13];
     extern __shared__ int s_mm[];  // 2 * ncols: min, max
     const uint64_t c = xcd_tile(blockIdx.x, gridDim.x), cs = c * kChunk;  // XCD-contiguous chunks: halo reads and shared column lines meet in one L2
     const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
@@ -647,6 +801,16 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
         s_mm[2 * j + 1] = INT_MIN;
     }
     __syncthreads();
+    if (tok && !lmode && !nf && ncols <= kTokMaxCols) {
+        const uint64_t rb = row_base[c];
+        const uint64_t R = (c + 1 < gridDim.x ? row_base[c + 1] : rows) - rb;
+        if (parse_chunk_tokens(s, s_list, s_u, &s_f0, s_mm, s_lead, rb, (uint32_t)R, ncols, cols)) {
+            __syncthreads();
+            for (int j = tid; j < ncols; j += kTPB)
+                partial[c * (uint64_t)ncols + j] = make_int2(s_mm[2 * j], s_mm[2 * j + 1]);
+            return;
+        }
+    }
     unsigned long long st = real_starts(s, cs, ce, tid);
     const uint64_t a = cs + (uint64_t)tid * kSeg;
     if (lmode) {
@@ -727,26 +891,57 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
 // min/max per column over the chunk partials (one block per column); zfill[j]
 // set = the fix-up wrote 0s into column j (rows before its first token), which
 // count as values like every other row.
-__global__ __launch_bounds__(kTPB) void k_csv_minmax(const int2* __restrict__ partial, uint64_t nch,
-                                                      int ncols, const unsigned* __restrict__ zfill,
-                                                      int32_t* __restrict__ out) {
-    __shared__ int s_a[kWaves], s_b[kWaves];
-    const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    int mn = INT_MAX, mx = INT_MIN;
-    for (uint64_t c = tid; c < nch; c += kTPB) {
-        const int2 v = partial[c * (uint64_t)ncols + j];
-        mn = min(mn, v.x);
-        mx = max(mx, v.y);
+__global__ __launch_bounds__(kTPB) void k_csv_minmax_init(int ncols, const unsigned* __restrict__ zfill,
+                                                           int32_t* __restrict__ out) {
+    for (int j = threadIdx.x; j < ncols; j += kTPB) {
+        const bool z = zfill && zfill[j];
+        out[2 * j] = z ? 0 : INT_MAX;
+        out[2 * j + 1] = z ? 0 : INT_MIN;
     }
-    if (zfill && zfill[j]) mn = min(mn, 0), mx = max(mx, 0);
-    mn = wave_min_i(mn);
-    mx = wave_max_i(mx);
-    if (lane == 0) s_a[tid >> 6] = mn, s_b[tid >> 6] = mx;
+}
+
+// Fold of the per-chunk partials (flat [chunk][column] int2) into out, which
+// k_csv_minmax_init seeded: each block a contiguous range of the flat array (one
+// read, coalesced), per column in registers when kTPB % ncols == 0 (a thread's
+// column is then fixed), else through LDS atomics; one global atomic per column
+// and block. (One block per column read 583K strided partials each: 2.4 ms at 1e9
+// rows.)
+__global__ __launch_bounds__(kTPB) void k_csv_minmax(const int2* __restrict__ partial, uint64_t nch,
+                                                      int ncols, uint64_t per, int32_t* __restrict__ out) {
+    extern __shared__ int s_mm[];  // 2 * ncols
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint64_t tot = nch * (uint64_t)ncols;
+    const uint64_t i0 = (uint64_t)blockIdx.x * per, i1 = i0 + per < tot ? i0 + per : tot;
+    if (kTPB % ncols == 0) {
+        int mn = INT_MAX, mx = INT_MIN;
+        for (uint64_t i = i0 + (uint64_t)tid; i < i1; i += kTPB) {
+            const int2 v = partial[i];
+            mn = min(mn, v.x);
+            mx = max(mx, v.y);
+        }
+        const int col = (int)((i0 + (uint64_t)tid) % (uint64_t)ncols);  // per % ncols == 0
+        for (int o = 32; o >= ncols; o >>= 1) {  // lanes l and l ^ o share the column
+            mn = min(mn, __shfl_xor(mn, o, 64));
+            mx = max(mx, __shfl_xor(mx, o, 64));
+        }
+        if (ncols > 64 || lane < ncols) {
+            atomicMin(&out[2 * col], mn);
+            atomicMax(&out[2 * col + 1], mx);
+        }
+        return;
+    }
+    for (int j = tid; j < ncols; j += kTPB) s_mm[2 * j] = INT_MAX, s_mm[2 * j + 1] = INT_MIN;
     __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < kWaves; w++) mn = min(mn, s_a[w]), mx = max(mx, s_b[w]);
-        out[2 * j] = mn;
-        out[2 * j + 1] = mx;
+    for (uint64_t i = i0 + (uint64_t)tid; i < i1; i += kTPB) {
+        const int2 v = partial[i];
+        const int col = (int)(i % (uint64_t)ncols);
+        atomicMin(&s_mm[2 * col], v.x);
+        atomicMax(&s_mm[2 * col + 1], v.y);
+    }
+    __syncthreads();
+    for (int j = tid; j < ncols; j += kTPB) {
+        atomicMin(&out[2 * j], s_mm[2 * j]);
+        atomicMax(&out[2 * j + 1], s_mm[2 * j + 1]);
     }
 }
 
@@ -852,13 +1047,15 @@ int launch_count(const char* text, uint64_t n, const CsvWs& w, bool lng, hipStre
     return MQ_OK;
 }
 
-int launch_parse(const char* text, uint64_t n, int ncols, const CsvWs& w, uint16_t* nf, hipStream_t st) {
+int launch_parse(const char* text, uint64_t n, int ncols, uint64_t rows, const CsvWs& w, uint16_t* nf,
+                 hipStream_t st) {
     const uint64_t nch = nchunks_of(n);
     const size_t dyn = (size_t)ncols * 8;
+    static const int tok = !(getenv("MQ_CSV_TOKENS") && getenv("MQ_CSV_TOKENS")[0] == '0');  // 0: row-wise only (A/B)
     if (aligned16(text))
-        hipLaunchKernelGGL((k_csv_parse<true>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags);
+        hipLaunchKernelGGL((k_csv_parse<true>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags, rows, tok);
     else
-        hipLaunchKernelGGL((k_csv_parse<false>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags);
+        hipLaunchKernelGGL((k_csv_parse<false>), dim3((unsigned)nch), dim3(kTPB), dyn, st, text, n, w.row_base, w.prev, ncols, w.colptr, w.partial, nf, w.flags, rows, tok);
     LAUNCHCHK("k_csv_parse");
     return MQ_OK;
 }
@@ -947,7 +1144,7 @@ int mq_csv_parse_int32(const char* d_text, uint64_t n, int ncols, int32_t* const
     }
     const uint64_t nch = nchunks_of(n);
     HIPCHK(hipMemcpyAsync(w.colptr, d_cols, (size_t)ncols * 8, hipMemcpyHostToDevice, st));
-    if ((rc = launch_parse(d_text, n, ncols, w, nullptr, st))) return rc;
+    if ((rc = launch_parse(d_text, n, ncols, rows, w, nullptr, st))) return rc;
     unsigned flags[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(flags, w.flags, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -964,7 +1161,7 @@ int mq_csv_parse_int32(const char* d_text, uint64_t n, int ncols, int32_t* const
         long long* carry = reinterpret_cast<long long*>(p + b_nf + b_t);
         zfill = reinterpret_cast<unsigned*>(p + b_nf + 2 * b_t);
         HIPCHK(hipMemsetAsync(zfill, 0, (size_t)ncols * 4, st));
-        if ((rc = launch_parse(d_text, n, ncols, w, nf, st))) return rc;
+        if ((rc = launch_parse(d_text, n, ncols, rows, w, nf, st))) return rc;
         hipLaunchKernelGGL(k_fill_tile_last, dim3((unsigned)ntiles), dim3(kTPB), 0, st, nf, rows, ncols, tl);
         LAUNCHCHK("k_fill_tile_last");
         hipLaunchKernelGGL(k_fill_carry, dim3((unsigned)ncols), dim3(1024), 0, st, tl, ntiles, ncols, carry);
@@ -973,9 +1170,18 @@ int mq_csv_parse_int32(const char* d_text, uint64_t n, int ncols, int32_t* const
                            w.colptr, carry, zfill);
         LAUNCHCHK("k_fill_apply");
     }
-    hipLaunchKernelGGL(k_csv_minmax, dim3((unsigned)ncols), dim3(kTPB), 0, st, w.partial, nch, ncols,
-                       zfill, d_minmax);
-    LAUNCHCHK("k_csv_minmax");
+    hipLaunchKernelGGL(k_csv_minmax_init, dim3(1), dim3(kTPB), 0, st, ncols, zfill, d_minmax);
+    LAUNCHCHK("k_csv_minmax_init");
+    {
+        const uint64_t tot = nch * (uint64_t)ncols;
+        uint64_t per = (tot + 1023) / 1024;                            // <= 1024 blocks
+        per = (per + 8ull * kTPB - 1) / (8ull * kTPB) * (8ull * kTPB);  // 8 partials a thread at least
+        per = (per + ncols - 1) / ncols * ncols;                       // whole chunks: a thread's column is fixed
+        const unsigned g = (unsigned)((tot + per - 1) / per);
+        hipLaunchKernelGGL(k_csv_minmax, dim3(g), dim3(kTPB), (size_t)ncols * 8, st, w.partial, nch, ncols, per,
+                           d_minmax);
+        LAUNCHCHK("k_csv_minmax");
+    }
     if (scratch) {
         HIPCHK(hipStreamSynchronize(st));
         pool_free(scratch);

@@ -101,6 +101,65 @@ def test_load_multichunk_vs_oracle(lib, refcpu, long_every, ragged):
     assert np.array_equal(cols, want) and np.array_equal(mm, want_mm)
 
 
+_TOKENS = ["0", "-0", "", "-", "7", "-7", "0000000000", "4294967295", "9999999999", "-9999999999",
+           "2147483647", "-2147483648", "123456789", "-12345", "00042"]
+_IRREGULAR = [" 5", "+5", "5 ", "12345678901", "1-2", "5\r", "\t9"]
+
+
+def _token_text(seed: int, lines: int, ncols: int, irregular_every: int) -> bytes:
+    """Rows of ncols tokens of 0-10 digits (k_csv_parse's token-parallel form), with
+    every irregular_every-th row made irregular (isspace, '+', junk, 11 digits,
+    a missing or an extra token) so that its chunk takes the row-wise parse."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(lines):
+        k = ncols
+        toks = []
+        for _ in range(k):
+            r = rng.random()
+            if r < 0.15:
+                toks.append(_TOKENS[int(rng.integers(len(_TOKENS)))])
+            else:
+                toks.append(str(int(rng.integers(-10 ** int(rng.integers(1, 10)), 10 ** int(rng.integers(1, 11))))))
+        if irregular_every and i % irregular_every == irregular_every - 1:
+            kind = int(rng.integers(3))
+            if kind == 0:
+                toks[int(rng.integers(ncols))] = _IRREGULAR[int(rng.integers(len(_IRREGULAR)))]
+            elif kind == 1 and ncols > 1:
+                toks = toks[:-1]
+            else:
+                toks.append("31")
+        out.append(",".join(toks) + "\n")
+    return "".join(out).encode()
+
+
+@pytest.mark.parametrize("ncols", [1, 2, 3, 4, 5, 7, 8, 16, 17])
+@pytest.mark.parametrize("irregular_every", [0, 701])
+def test_load_token_parallel_vs_oracle(lib, refcpu, ncols, irregular_every):
+    """The token-parallel parse (every row ncols tokens of [-]digits{0..10}) and its
+    per-chunk fall-back to the row-wise parse, against the oracle."""
+    data = _token_text(100 + ncols, max(4000, 600_000 // (ncols * 7)), ncols, irregular_every)
+    assert len(data) > 16 * 16384
+    for offset in (0, 5):
+        d = text_dev(data, offset)
+        cols, mm = gpu_load(lib, d.ptr, len(data), ncols)
+        want, want_mm = refcpu.load_csv(data, ncols)
+        assert np.array_equal(cols, want), (ncols, irregular_every, offset)
+        assert np.array_equal(mm, want_mm), (ncols, irregular_every, offset)
+
+
+def test_load_token_parallel_short_tokens(lib, refcpu):
+    """One-digit tokens: more separators per chunk than the token list holds (the
+    row-wise parse), and the text's end without a final '\n'."""
+    rng = np.random.default_rng(9)
+    rows = ["%d,%d,%d" % tuple(rng.integers(0, 10, 3)) for _ in range(50_000)]
+    data = ("\n".join(rows)).encode()
+    d = text_dev(data)
+    cols, mm = gpu_load(lib, d.ptr, len(data), 3)
+    want, want_mm = refcpu.load_csv(data, 3)
+    assert np.array_equal(cols, want) and np.array_equal(mm, want_mm)
+
+
 def _format(L, dcols, rows):
     ncols = len(dcols)
     ws = Dev(L.mq_format_csv_workspace_bytes(rows, ncols))
