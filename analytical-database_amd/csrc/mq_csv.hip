@@ -47,13 +47,14 @@ using namespace mqi;
 
 constexpr int kTPB = 256;
 constexpr int kWaves = kTPB / 64;
-constexpr int kChunk = 16384;            // text bytes per block
+constexpr int kChunk = 16384;            // text bytes per block (12 KB chunks measured 5 % slower)
 constexpr int kSeg = kChunk / kTPB;      // 64 bytes per thread
+static_assert(kSeg % 16 == 0 && kSeg <= 64 && kChunk % 4096 == 0, "segments of 16-byte pieces");
 constexpr int kPre = 16;                 // LDS bytes before the chunk (byte cs-1 at kPre-1)
 constexpr int kHalo = 1024;              // after the chunk: a piece has <= 1023 bytes
 constexpr int kLds = kPre + kChunk + kHalo;
 constexpr int kPiece = 1023;             // fgets(line, 1024)
-constexpr int kList = 4096;              // piece starts listed in LDS (else searched)
+constexpr int kList = 4096;              // piece / token starts listed in LDS
 constexpr int kRegCols = 8;              // columns whose min/max live in lane registers
 constexpr int kMaxCols = 1024;
 constexpr int kFillTile = 1024;          // rows per tile in the missing-token fix-up
@@ -176,7 +177,7 @@ __device__ __forceinline__ uint32_t nl4(uint32_t w) {
     return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
 }
 
-// Real starts of this thread's 64-byte segment [a, a+64): bit k <=> a+k starts a
+// Real starts of this thread's segment [a, a+kSeg): bit k <=> a+k starts a
 // line (byte a+k-1 is '\n'); bytes at or past ce are masked off.
 __device__ __forceinline__ unsigned long long real_starts(const uint8_t* s, uint64_t cs, uint64_t ce,
                                                           int tid) {
@@ -189,9 +190,10 @@ __device__ __forceinline__ unsigned long long real_starts(const uint8_t* s, uint
               << (q * 16);
     }
     unsigned long long st = (nl << 1) | (s[off - 1] == '\n' ? 1ull : 0ull);
+    if (kSeg < 64) st &= (1ull << (kSeg & 63)) - 1;  // (bit kSeg is the next segment's)
     const uint64_t a = cs + (uint64_t)tid * kSeg;
     if (a >= ce) return 0;
-    if (ce - a < 64) st &= (1ull << (ce - a)) - 1;
+    if (ce - a < (uint64_t)kSeg) st &= (1ull << (ce - a)) - 1;
     return st;
 }
 
@@ -265,14 +267,14 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t x, uint32_t* s_w, ui
 // Row starts of the segment, in long mode: the real starts plus, inside a line that
 // is longer than 1023 bytes, every 1023rd byte after its start (fgets pieces).
 // ls_in = last real start before the segment (global). Between two real starts of
-// one 64-byte segment there is no room for 1023 bytes, so only the part before
+// one segment there is no room for 1023 bytes, so only the part before
 // the first real start can hold a piece start.
 __device__ __forceinline__ unsigned long long piece_starts(unsigned long long real, uint64_t a,
                                                            long long ls_in, uint64_t ce) {
     if (ls_in < 0 || a >= ce) return real;
     const uint64_t q = (a - (uint64_t)ls_in) % kPiece;
     const uint64_t p = q == 0 ? 0 : kPiece - q;  // first piece boundary at or after a
-    const int rf = real ? __builtin_ctzll(real) : 64;
+    const int rf = real ? __builtin_ctzll(real) : kSeg;
     if (p < (uint64_t)rf && a + p < ce) real |= 1ull << p;
     return real;
 }
@@ -356,9 +358,10 @@ __global__ __launch_bounds__(kTPB) void k_csv_count_stream(const char* __restric
     const uint64_t c = blockIdx.x, cs = c * kChunk;
     const uint64_t ce = cs + kChunk < n ? cs + kChunk : n;
     const int tid = threadIdx.x, lane = tid & 63;
-    uint32_t w[4][4];
+    constexpr int kQ = kChunk / 4096;
+    uint32_t w[kQ][4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {  // 4 x 16 B per lane, 4 KB apart: coalesced
+    for (int q = 0; q < kQ; q++) {  // kQ x 16 B per lane, 4 KB apart: coalesced
         const uint64_t g = cs + (uint64_t)q * 4096 + (uint64_t)tid * 16;
         if (VEC && g + 16 <= ce) {
             const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(text + g));
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_count_stream(const char* __restric
     uint32_t cntl = 0;
     bool nolf_block = false;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < kQ; q++) {
         const uint32_t m = nl4(w[q][0]) | (nl4(w[q][1]) << 4) | (nl4(w[q][2]) << 8) | (nl4(w[q][3]) << 12);
         cntl += __popc(m);
         // 32 lanes x 16 B = one aligned 512-byte block; count only blocks wholly in the text
@@ -646,7 +649,7 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
 // parse then rewrites those rows.
 constexpr int kTokSeg = (kChunk + kHalo) / kTPB;  // 68 bytes classified per lane
 constexpr int kTokMaxCols = 16;
-static_assert(kTokSeg % 4 == 0 && kTokSeg >= 64 && kTokSeg < 64 + 32, "classification in words");
+static_assert((kChunk + kHalo) % kTPB == 0 && kTokSeg % 4 == 0 && kTokSeg < 64 + 32, "classification in words");
 
 __device__ __forceinline__ uint32_t below_2d(uint32_t x) {  // 0x80 in each byte < 0x2D
     return ~(((x | 0x80808080u) - 0x2D2D2D2Du) | x) & 0x80808080u;
@@ -663,15 +666,20 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
     uint32_t f[kW];
 #pragma unroll
     for (int k = 0; k < kW; k++) f[k] = below_2d(d[k]);
+    // flag bytes -> bits: v_dot4 with weights 1, 2, 4, 8 (and 16, ..., 128 for the
+    // next word) gives 128 x the bits of two words
     unsigned long long m = 0;
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
+    for (int g = 0; g < kW / 4 && g < 4; g++) {
         const uint32_t lo = __builtin_amdgcn_udot4(f[4 * g + 1], 0x80402010u,
                                                    __builtin_amdgcn_udot4(f[4 * g], 0x08040201u, 0u, false), false);
         const uint32_t hi = __builtin_amdgcn_udot4(f[4 * g + 3], 0x80402010u,
                                                    __builtin_amdgcn_udot4(f[4 * g + 2], 0x08040201u, 0u, false), false);
         m |= (unsigned long long)((lo | (hi << 8)) >> 7) << (16 * g);
     }
+#pragma unroll
+    for (int k = kW / 4 * 4; k < kW && k < 16; k++)
+        m |= (unsigned long long)(__builtin_amdgcn_udot4(f[k], 0x08040201u, 0u, false) >> 7) << (4 * k);
     uint32_t mt = 0;  // the words past the first 64 bytes
 #pragma unroll
     for (int k = 16; k < kW; k++) mt |= (__builtin_amdgcn_udot4(f[k], 0x08040201u, 0u, false) >> 7) << (4 * (k - 16));
@@ -783,9 +791,14 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
                                                      int2* __restrict__ partial, uint16_t* __restrict__ nf,
                                                      unsigned* flags, uint64_t rows, int tok) {
     __shared__ __attribute__((aligned(16))) uint8_t s[kLds + 32];  // + token_fast's over-read
-    __shared__ unsigned long long s_mask[kTPB];
-    __shared__ uint16_t s_list[kList];
-    __shared__ uint32_t s_off[kTPB];
+    // the start list, or (more starts than it holds) the per-segment masks and
+    // prefix it is searched in: one is written per chunk, so they share LDS (26 KB
+    // a block: 6 blocks per CU instead of 5)
+    __shared__ __attribute__((aligned(16))) unsigned long long s_lu[kList * 2 / 8];
+    static_assert(kTPB * 12 <= kList * 2, "masks + prefix fit the list's bytes");
+    uint16_t* const s_list = reinterpret_cast<uint16_t*>(s_lu);
+    unsigned long long* const s_mask = s_lu;
+    uint32_t* const s_off = reinterpret_cast<uint32_t*>(s_lu + kTPB);
     __shared__ long long s_w[kWaves];
     __shared__ uint32_t s_u[kWaves];
     __shared__ int s_f0;
@@ -819,9 +832,10 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
     }
     uint32_t nst;
     const uint32_t o = block_excl_sum((uint32_t)__popcll(st), s_u, &nst);
-    s_off[tid] = o;
-    s_mask[tid] = st;
-    if (nst <= (uint32_t)kList) {  // the usual case: an explicit start list
+    if (nst > (uint32_t)kList) {
+        s_off[tid] = o;
+        s_mask[tid] = st;
+    } else {  // the usual case: an explicit start list
         uint32_t q = o;
         for (unsigned long long m = st; m; m &= m - 1) s_list[q++] = (uint16_t)(tid * kSeg + __builtin_ctzll(m));
     }
