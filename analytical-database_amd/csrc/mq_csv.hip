@@ -564,18 +564,22 @@ __device__ __forceinline__ uint32_t nondigit_first(uint32_t w) {
     return ((y + 0x76767676u) | y) & 0x80808080u;
 }
 
-// a * b + c on the low 24 bits of a (b < 2^24): the mask is free, it lets the
-// compiler pick v_mul_u32_u24 (full rate) instead of widening the product to
-// v_mad_u64_u32 / v_mul_lo_u32 (quarter rate).
-__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) { return (a & 0xFFFFFFu) * b + c; }
-
-// Four ASCII digits of a word (byte 0 the most significant) -> 0..9999, by two
-// v_dot4_u32_u8 (the accumulator removes 48 x the weights) and one 24-bit mad.
-__device__ __forceinline__ uint32_t digits4(uint32_t x) {
-    constexpr uint32_t kMinus48x11 = 0u - 48u * 11u;
-    const uint32_t hi = __builtin_amdgcn_udot4(x, 0x0000010Au, kMinus48x11, false);  // 10 b0 + b1
-    const uint32_t lo = __builtin_amdgcn_udot4(x, 0x010A0000u, kMinus48x11, false);  // 10 b2 + b3
-    return mad24(hi, 100u, lo);
+// The value mod 2^32 of 12 ASCII digits (x0 byte 0 the most significant) whose
+// first two are '0' (at most 10 significant digits): digit pairs by v_dot4 on
+// byte ^ '0', then ((p1 * 10^4 + B) * 10^4 + C) in 24-bit multiplies (a chain of
+// (a & 0xFFFFFF) * b + c compiled to quarter-rate 64-bit mads).
+__device__ __forceinline__ uint32_t digits12_d(uint32_t d0, uint32_t d1, uint32_t d2) {
+    const uint32_t p1 = __builtin_amdgcn_udot4(d0, 0x010A0000u, 0u, false) & 0xFFu;
+    const uint32_t hb = __builtin_amdgcn_udot4(d1, 0x0000010Au, 0u, false) & 0xFFu;
+    const uint32_t lb = __builtin_amdgcn_udot4(d1, 0x010A0000u, 0u, false) & 0xFFu;
+    const uint32_t hc = __builtin_amdgcn_udot4(d2, 0x0000010Au, 0u, false) & 0xFFu;
+    const uint32_t lc = __builtin_amdgcn_udot4(d2, 0x010A0000u, 0u, false) & 0xFFu;
+    uint32_t hi = p1 * 10000u + hb * 100u + lb;  // < 2^24
+    asm volatile("" : "+v"(hi));                 // (keeps the next product 24-bit)
+    return (hi & 0xFFFFFFu) * 10000u + (hc * 100u + lc);
+}
+__device__ __forceinline__ uint32_t digits12(uint32_t x0, uint32_t x1, uint32_t x2) {
+    return digits12_d(x0 ^ 0x30303030u, x1 ^ 0x30303030u, x2 ^ 0x30303030u);
 }
 
 // Index of the lowest set bit, or 0xFFFFFFFF for 0 (v_ffbl_b32 as it is).
@@ -590,7 +594,7 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) { return (uint32_t)__builti
 //     after an optional '-' is the end e (min3 over the three words' ffbl);
 //   * the 12 bytes ENDING at k+e are read again, so the digits sit right-aligned;
 //     the bytes before them become '0' (one bitfield insert per word) and the value
-//     is digits4 of the three words combined by 24-bit mads, mod 2^32: strtol
+//     is digits12 of the three words, mod 2^32: strtol
 //     saturates only past 18 digits, so (int)strtol is the low 32 bits.
 __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, int& k, int kend,
                                                  bool& more) {
@@ -620,7 +624,7 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
     const uint32_t x0 = (__builtin_amdgcn_alignbyte(e1, e0, r2) & m0) | (0x30303030u & ~m0);
     const uint32_t x1 = (__builtin_amdgcn_alignbyte(e2, e1, r2) & m1) | (0x30303030u & ~m1);
     const uint32_t x2 = (__builtin_amdgcn_alignbyte(e3, e2, r2) & m2) | (0x30303030u & ~m2);
-    const uint32_t v = mad24(mad24(digits4(x0), 100u, 0u), 1000000u, mad24(digits4(x1), 10000u, digits4(x2)));
+    const uint32_t v = digits12(x0, x1, x2);
     more = c == ',';
     k += e + (more ? 1 : 0);
     return (int32_t)(neg ? 0u - v : v);
@@ -640,7 +644,7 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
 //     256, so its column is fixed: one pointer, one min and one max per lane. The
 //     token's bytes are its two list entries apart; the 12 bytes ending at the
 //     separator are read from LDS, bytes before the digits become '0', and the
-//     value is digits4 of three words (next_token_nl's arithmetic).
+//     value is digits12 of three words (next_token_nl's arithmetic).
 // Each token checks its own separator byte exactly (',' or, for the last column,
 // '\n') and its digits; together with the candidate list (every ',' and '\n' is a
 // candidate) that proves the chunk is R rows of the fast form. Anything else (a
@@ -746,16 +750,7 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
             const uint32_t nd = ((d0 + 0x76767676u) | d0 | (d1 + 0x76767676u) | d1 | (d2 + 0x76767676u) | d2) &
                                 0x80808080u;
             bad |= (s[pe] != expect) | (Ld > 10u) | (nd != 0u);
-            // 12 digits (at most the last 10 nonzero): pairs by v_dot4, then
-            // ((p1 * 10^4 + B) * 10^4 + C) mod 2^32 in 24-bit mads
-            const uint32_t p1 = __builtin_amdgcn_udot4(d0, 0x010A0000u, 0u, false) & 0xFFu;
-            const uint32_t hb = __builtin_amdgcn_udot4(d1, 0x0000010Au, 0u, false) & 0xFFu;
-            const uint32_t lb = __builtin_amdgcn_udot4(d1, 0x010A0000u, 0u, false) & 0xFFu;
-            const uint32_t hc = __builtin_amdgcn_udot4(d2, 0x0000010Au, 0u, false) & 0xFFu;
-            const uint32_t lc = __builtin_amdgcn_udot4(d2, 0x010A0000u, 0u, false) & 0xFFu;
-            uint32_t hi = p1 * 10000u + hb * 100u + lb;  // < 2^24
-            asm volatile("" : "+v"(hi));                 // (keeps the next product 24-bit)
-            const uint32_t v = (hi & 0xFFFFFFu) * 10000u + (hc * 100u + lc);
+            const uint32_t v = digits12_d(d0, d1, d2);
             const int32_t y = (int32_t)(neg ? 0u - v : v);
             cp[rr] = y;
             mn = min(mn, y);
