@@ -36,6 +36,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "mq_common.h"
@@ -688,7 +689,7 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
 #pragma unroll
     for (int k = 16; k < kW; k++) mt |= (__builtin_amdgcn_udot4(f[k], 0x08040201u, 0u, false) >> 7) << (4 * (k - 16));
     const bool pre = tid == 0 && s[kPre - 1] == '\n';  // byte cs-1: a row starts at cs
-    if (tid == 0) *s_f0 = INT_MAX;
+    if (tid == 0) s_f0[0] = INT_MAX, s_f0[1] = 0;  // first '\n' entry, "not the fast form"
     if (tid < 13) {  // s_lead[z]: byte masks of a 12-byte window that clear its first z bytes
         const uint32_t z8 = 8u * (uint32_t)tid;
         const uint64_t m01 = z8 >= 64u ? 0ull : (~0ull << z8);
@@ -701,17 +702,22 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
     int first_nl = INT_MAX;
     if (pre) first_nl = (int)o, list[o++] = (uint16_t)(kPre - 1);
     // (three 32-bit loops: a 64-bit find-first and clear cost twice the VALU)
-    uint32_t mw[3] = {(uint32_t)m, (uint32_t)(m >> 32), mt};
+    // (wave 0 also looks for the first '\n'; the other waves' loops skip the test)
+    const uint32_t mw[3] = {(uint32_t)m, (uint32_t)(m >> 32), mt};
+    auto emit = [&](auto find_nl) {
 #pragma unroll
-    for (int h = 0; h < 3; h++) {
-        uint32_t x = mw[h];
-        while (x) {
-            const int p = base + 32 * h + __builtin_ctz(x);
-            if (wave == 0 && first_nl == INT_MAX && s[p] == '\n') first_nl = (int)o;
-            list[o++] = (uint16_t)p;
-            x &= x - 1;
+        for (int h = 0; h < 3; h++) {
+            uint32_t x = mw[h];
+            while (x) {
+                const int p = base + 32 * h + __builtin_ctz(x);
+                if (decltype(find_nl)::value && first_nl == INT_MAX && s[p] == '\n') first_nl = (int)o;
+                list[o++] = (uint16_t)p;
+                x &= x - 1;
+            }
         }
-    }
+    };
+    if (wave == 0) emit(std::true_type{});
+    else emit(std::false_type{});
     if (wave == 0) {
         const int f = wave_min_i(first_nl);
         if (lane == 0 && f != INT_MAX) atomicMin(s_f0, f);
@@ -726,13 +732,16 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
     int mn = INT_MAX, mx = INT_MIN;
     int col = 0;
     if ((uint32_t)tid < S) {
-        col = tid % ncols;
+        // tid / ncols by a 16-bit reciprocal (exact for tid < 256, ncols <= 16),
+        // not the ~20-instruction integer division
+        const uint32_t magic = (65536u + (uint32_t)ncols - 1u) / (uint32_t)ncols;
+        uint32_t rr = ((uint32_t)tid * magic) >> 16;
+        col = tid - (int)rr * ncols;
         const uint32_t expect = col == ncols - 1 ? (uint32_t)'\n' : (uint32_t)',';
         gint32* cp = global_ptr(cols[col]) + r0;
         const uint32_t rstep = S / (uint32_t)ncols;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
         const uint16_t* lt = list + f0;
-        uint32_t rr = (uint32_t)tid / (uint32_t)ncols;
         for (uint32_t t = (uint32_t)tid; t < T; t += S, rr += rstep) {
             const uint32_t pb = lt[t], pe = lt[t + 1];  // the separators before / after the token
             const uint32_t L = pe - pb - 1u;
@@ -757,17 +766,10 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
             mx = max(mx, y);
         }
     }
-    if (__syncthreads_or(bad)) return false;
-    if (64 % ncols == 0) {  // lanes l and l + ncols hold one column
-        for (int o2 = 32; o2 >= ncols; o2 >>= 1) {
-            mn = min(mn, __shfl_xor(mn, o2, 64));
-            mx = max(mx, __shfl_xor(mx, o2, 64));
-        }
-        if (lane < ncols) {
-            atomicMin(&s_mm[2 * col], mn);
-            atomicMax(&s_mm[2 * col + 1], mx);
-        }
-    } else if ((uint32_t)tid < S) {
+    if (bad) s_f0[1] = 1;  // (__syncthreads_or costs ~26 VALU a wave)
+    __syncthreads();
+    if (s_f0[1]) return false;
+    if ((uint32_t)tid < S) {  // LDS atomics (a shuffle tree cost ~50 VALU a wave)
         atomicMin(&s_mm[2 * col], mn);
         atomicMax(&s_mm[2 * col + 1], mx);
     }
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
     uint32_t* const s_off = reinterpret_cast<uint32_t*>(s_lu + kTPB);
     __shared__ long long s_w[kWaves];
     __shared__ uint32_t s_u[kWaves];
-    __shared__ int s_f0;
+    __shared__ int s_f0[2];
     __shared__ uint4 s_lead[13];
     extern __shared__ int s_mm[];  // 2 * ncols: min, max
     const uint64_t c = xcd_tile(blockIdx.x, gridDim.x), cs = c * kChunk;  // XCD-contiguous chunks: halo reads and shared column lines meet in one L2
@@ -812,7 +814,7 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
     if (tok && !lmode && !nf && ncols <= kTokMaxCols) {
         const uint64_t rb = row_base[c];
         const uint64_t R = (c + 1 < gridDim.x ? row_base[c + 1] : rows) - rb;
-        if (parse_chunk_tokens(s, s_list, s_u, &s_f0, s_mm, s_lead, rb, (uint32_t)R, ncols, cols)) {
+        if (parse_chunk_tokens(s, s_list, s_u, s_f0, s_mm, s_lead, rb, (uint32_t)R, ncols, cols)) {
             __syncthreads();
             for (int j = tid; j < ncols; j += kTPB)
                 partial[c * (uint64_t)ncols + j] = make_int2(s_mm[2 * j], s_mm[2 * j + 1]);
