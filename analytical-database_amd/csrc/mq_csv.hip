@@ -163,9 +163,29 @@ __device__ __forceinline__ void store_chunk(const char* __restrict__ text, uint6
     }
 }
 
+#ifndef MQ_CSV_STAGE_FAST
+#define MQ_CSV_STAGE_FAST 1
+#endif
 template <bool VEC>
 __device__ __forceinline__ void stage_chunk(const char* __restrict__ text, uint64_t n, uint64_t cs,
                                             uint8_t* s) {
+    if (MQ_CSV_STAGE_FAST && VEC && cs >= (uint64_t)kPre && cs - kPre + kLds <= n) {
+        // an interior chunk (all but the first and the last ones): every piece is a
+        // whole 16-byte load, no per-piece bounds tests (~40 VALU and 5 branches a lane)
+        const v4u* src = reinterpret_cast<const v4u*>(text + (cs - kPre));
+        v4u pv[kPf];
+#pragma unroll
+        for (int q = 0; q < kPf; q++) {
+            const int i = threadIdx.x + q * kTPB;
+            if (q < kPf - 1 || i < kPieces) pv[q] = __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int q = 0; q < kPf; q++) {
+            const int i = threadIdx.x + q * kTPB;
+            if (q < kPf - 1 || i < kPieces) *reinterpret_cast<v4u*>(s + i * 16) = pv[q];
+        }
+        return;
+    }
     uint4 pf[kPf];
     prefetch_chunk<VEC>(text, n, cs, pf);
     store_chunk<VEC>(text, n, cs, pf, s);
@@ -570,11 +590,12 @@ __device__ __forceinline__ uint32_t nondigit_first(uint32_t w) {
 // byte ^ '0', then ((p1 * 10^4 + B) * 10^4 + C) in 24-bit multiplies (a chain of
 // (a & 0xFFFFFF) * b + c compiled to quarter-rate 64-bit mads).
 __device__ __forceinline__ uint32_t digits12_d(uint32_t d0, uint32_t d1, uint32_t d2) {
-    const uint32_t p1 = __builtin_amdgcn_udot4(d0, 0x010A0000u, 0u, false) & 0xFFu;
-    const uint32_t hb = __builtin_amdgcn_udot4(d1, 0x0000010Au, 0u, false) & 0xFFu;
-    const uint32_t lb = __builtin_amdgcn_udot4(d1, 0x010A0000u, 0u, false) & 0xFFu;
-    const uint32_t hc = __builtin_amdgcn_udot4(d2, 0x0000010Au, 0u, false) & 0xFFu;
-    const uint32_t lc = __builtin_amdgcn_udot4(d2, 0x010A0000u, 0u, false) & 0xFFu;
+    // (each pair is <= 99 for digits, so no masking: the callers have checked them)
+    const uint32_t p1 = __builtin_amdgcn_udot4(d0, 0x010A0000u, 0u, false);
+    const uint32_t hb = __builtin_amdgcn_udot4(d1, 0x0000010Au, 0u, false);
+    const uint32_t lb = __builtin_amdgcn_udot4(d1, 0x010A0000u, 0u, false);
+    const uint32_t hc = __builtin_amdgcn_udot4(d2, 0x0000010Au, 0u, false);
+    const uint32_t lc = __builtin_amdgcn_udot4(d2, 0x010A0000u, 0u, false);
     uint32_t hi = p1 * 10000u + hb * 100u + lb;  // < 2^24
     asm volatile("" : "+v"(hi));                 // (keeps the next product 24-bit)
     return (hi & 0xFFFFFFu) * 10000u + (hc * 100u + lc);
@@ -654,6 +675,12 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
 // parse then rewrites those rows.
 constexpr int kTokSeg = (kChunk + kHalo) / kTPB;  // 68 bytes classified per lane
 constexpr int kTokMaxCols = 16;
+#ifndef MQ_CSV_NEGW
+#define MQ_CSV_NEGW 0  // A/B: a token's '-' from its window words instead of an LDS byte read
+#endif
+#ifndef MQ_CSV_MASKA
+#define MQ_CSV_MASKA 0  // A/B: the lead masks computed instead of read from s_lead
+#endif
 static_assert((kChunk + kHalo) % kTPB == 0 && kTokSeg % 4 == 0 && kTokSeg < 64 + 32, "classification in words");
 
 __device__ __forceinline__ uint32_t below_2d(uint32_t x) {  // 0x80 in each byte < 0x2D
@@ -664,7 +691,6 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
                                    uint32_t* s_u, int* s_f0, int* s_mm, uint4* s_lead, uint64_t r0, uint32_t R,
                                    int ncols, int32_t* const* __restrict__ cols) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int base = kPre + tid * kTokSeg;
     const uint32_t* d = reinterpret_cast<const uint32_t*>(s + base);
     constexpr int kW = kTokSeg / 4;
@@ -689,7 +715,7 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
 #pragma unroll
     for (int k = 16; k < kW; k++) mt |= (__builtin_amdgcn_udot4(f[k], 0x08040201u, 0u, false) >> 7) << (4 * (k - 16));
     const bool pre = tid == 0 && s[kPre - 1] == '\n';  // byte cs-1: a row starts at cs
-    if (tid == 0) s_f0[0] = INT_MAX, s_f0[1] = 0;  // first '\n' entry, "not the fast form"
+    if (tid == 0) s_f0[1] = 0;  // "not the fast form"
     if (tid < 13) {  // s_lead[z]: byte masks of a 12-byte window that clear its first z bytes
         const uint32_t z8 = 8u * (uint32_t)tid;
         const uint64_t m01 = z8 >= 64u ? 0ull : (~0ull << z8);
@@ -699,33 +725,23 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
     uint32_t ntot;
     uint32_t o = block_excl_sum((uint32_t)(__popcll(m) + __popc(mt) + (pre ? 1 : 0)), s_u, &ntot);
     if (ntot > (uint32_t)kList) return false;
-    int first_nl = INT_MAX;
-    if (pre) first_nl = (int)o, list[o++] = (uint16_t)(kPre - 1);
+    if (pre) list[o++] = (uint16_t)(kPre - 1);
     // (three 32-bit loops: a 64-bit find-first and clear cost twice the VALU)
-    // (wave 0 also looks for the first '\n'; the other waves' loops skip the test)
     const uint32_t mw[3] = {(uint32_t)m, (uint32_t)(m >> 32), mt};
-    auto emit = [&](auto find_nl) {
 #pragma unroll
-        for (int h = 0; h < 3; h++) {
-            uint32_t x = mw[h];
-            while (x) {
-                const int p = base + 32 * h + __builtin_ctz(x);
-                if (decltype(find_nl)::value && first_nl == INT_MAX && s[p] == '\n') first_nl = (int)o;
-                list[o++] = (uint16_t)p;
-                x &= x - 1;
-            }
-        }
-    };
-    if (wave == 0) emit(std::true_type{});
-    else emit(std::false_type{});
-    if (wave == 0) {
-        const int f = wave_min_i(first_nl);
-        if (lane == 0 && f != INT_MAX) atomicMin(s_f0, f);
+    for (int h = 0; h < 3; h++) {
+        for (uint32_t x = mw[h]; x; x &= x - 1) list[o++] = (uint16_t)(base + 32 * h + __builtin_ctz(x));
     }
     __syncthreads();
-    const int f0 = *s_f0;
+    // f0 = the first '\n' of the list. In the fast form a row has at most ncols <= 16
+    // separators, so it is among the first 64 entries; every wave finds it by one
+    // ballot (a search inside the list loop held wave 0, and the block, ~1000 cycles).
+    const bool isnl = (uint32_t)lane < ntot && s[list[lane]] == '\n';
+    const unsigned long long bnl = __ballot(isnl);
     const uint32_t T = R * (uint32_t)ncols;
-    if (f0 == INT_MAX || (uint64_t)f0 + T >= ntot) return false;
+    if (!bnl) return false;
+    const int f0 = __builtin_ctzll(bnl);
+    if ((uint64_t)f0 + T >= ntot) return false;
 
     const uint32_t S = (uint32_t)(kTPB - kTPB % ncols);
     bool bad = false;
@@ -738,30 +754,48 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
         uint32_t rr = ((uint32_t)tid * magic) >> 16;
         col = tid - (int)rr * ncols;
         const uint32_t expect = col == ncols - 1 ? (uint32_t)'\n' : (uint32_t)',';
-        gint32* cp = global_ptr(cols[col]) + r0;
+        gint32* op = global_ptr(cols[col]) + r0 + rr;  // this lane's next row of its column
         const uint32_t rstep = S / (uint32_t)ncols;
         const uint32_t* w = reinterpret_cast<const uint32_t*>(s);
         const uint16_t* lt = list + f0;
-        for (uint32_t t = (uint32_t)tid; t < T; t += S, rr += rstep) {
-            const uint32_t pb = lt[t], pe = lt[t + 1];  // the separators before / after the token
+        // (pointer steps: no separate token / row counters in the loop)
+        for (const uint16_t *q = lt + tid, *qe = lt + T; q < qe; q += S, op += rstep) {
+            const uint32_t pb = q[0], pe = q[1];  // the separators before / after the token
             const uint32_t L = pe - pb - 1u;
-            const uint32_t neg = s[pb + 1] == '-' ? 1u : 0u;  // (L == 0: that byte is the separator)
-            const uint32_t Ld = L - neg;                        // digits
-            const uint4 mk = s_lead[12u - min(Ld, 12u)];       // keeps the last Ld bytes of 12
-            const uint32_t b = pe - 12u;                        // >= kPre - 12
-            const uint32_t a2 = b >> 2, r2 = pe & 3u;
+            const uint32_t a2 = (pe - 12u) >> 2, r2 = pe & 3u;  // the 12 bytes before pe, and pe
             const uint32_t e0 = w[a2], e1 = w[a2 + 1], e2 = w[a2 + 2], e3 = w[a2 + 3];
+            const uint32_t x0 = __builtin_amdgcn_alignbyte(e1, e0, r2), x1 = __builtin_amdgcn_alignbyte(e2, e1, r2),
+                           x2 = __builtin_amdgcn_alignbyte(e3, e2, r2);
+#if MQ_CSV_NEGW
+            // byte pb + 1 is byte 12 - L of the window (L in 1..11; else no valid negative)
+            const uint32_t jn = 12u - L;
+            const uint32_t cn = jn < 4u ? __builtin_amdgcn_perm(x1, x0, jn) : __builtin_amdgcn_perm(x2, x1, jn - 4u);
+            const uint32_t neg = ((L - 1u < 11u) & ((cn & 0xFFu) == (uint32_t)'-')) ? 1u : 0u;
+#else
+            const uint32_t neg = s[pb + 1] == '-' ? 1u : 0u;  // (L == 0: that byte is the separator)
+#endif
+            const uint32_t Ld = L - neg;  // digits
+#if MQ_CSV_MASKA
+            const uint32_t z8 = 8u * (12u - min(Ld, 12u));  // leading bits that are not digits
+            const uint32_t m0 = z8 >= 32u ? 0u : ~0u << z8;
+            const uint32_t m1 = z8 >= 64u ? 0u : z8 <= 32u ? ~0u : ~0u << (z8 - 32u);
+            const uint32_t m2 = z8 >= 96u ? 0u : z8 <= 64u ? ~0u : ~0u << (z8 - 64u);
+            const uint4 mk = make_uint4(m0, m1, m2, 0u);
+#else
+            const uint4 mk = s_lead[12u - min(Ld, 12u)];  // keeps the last Ld bytes of 12
+#endif
             // digit values: byte ^ '0' (no borrows: a digit byte is 0x30 | d), the bytes
             // before the digits cleared; a byte that is not a digit gives a value > 9
-            const uint32_t d0 = (__builtin_amdgcn_alignbyte(e1, e0, r2) ^ 0x30303030u) & mk.x;
-            const uint32_t d1 = (__builtin_amdgcn_alignbyte(e2, e1, r2) ^ 0x30303030u) & mk.y;
-            const uint32_t d2 = (__builtin_amdgcn_alignbyte(e3, e2, r2) ^ 0x30303030u) & mk.z;
+            const uint32_t d0 = (x0 ^ 0x30303030u) & mk.x;
+            const uint32_t d1 = (x1 ^ 0x30303030u) & mk.y;
+            const uint32_t d2 = (x2 ^ 0x30303030u) & mk.z;
+            const uint32_t sep = __builtin_amdgcn_alignbyte(e3, e3, r2) & 0xFFu;  // byte pe
             const uint32_t nd = ((d0 + 0x76767676u) | d0 | (d1 + 0x76767676u) | d1 | (d2 + 0x76767676u) | d2) &
                                 0x80808080u;
-            bad |= (s[pe] != expect) | (Ld > 10u) | (nd != 0u);
+            bad |= (sep != expect) | (Ld > 10u) | (nd != 0u);
             const uint32_t v = digits12_d(d0, d1, d2);
             const int32_t y = (int32_t)(neg ? 0u - v : v);
-            cp[rr] = y;
+            *op = y;
             mn = min(mn, y);
             mx = max(mx, y);
         }
