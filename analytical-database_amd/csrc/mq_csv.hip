@@ -269,7 +269,9 @@ __device__ __forceinline__ long long block_excl_max(long long x, long long seed,
     return carry > ex ? carry : ex;
 }
 
-// Exclusive sum over the block's threads; *total receives the block sum.
+// Exclusive sum over the block's threads; *total receives the block sum. TRAIL = false
+// drops the closing barrier (s_w is not written again before the caller's next one).
+template <bool TRAIL = true>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t x, uint32_t* s_w, uint32_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t inc = wave_incl_sum(x, lane);
@@ -280,7 +282,7 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t x, uint32_t* s_w, ui
         if (w < wave) carry += s_w[w];
         tot += s_w[w];
     }
-    __syncthreads();
+    if (TRAIL) __syncthreads();
     *total = tot;
     return carry + inc - x;
 }
@@ -723,8 +725,12 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
                                  z8 >= 96u ? 0u : (uint32_t)(0xFFFFFFFFull << (z8 > 64u ? z8 - 64u : 0u)), 0u);
     }
     uint32_t ntot;
-    uint32_t o = block_excl_sum((uint32_t)(__popcll(m) + __popc(mt) + (pre ? 1 : 0)), s_u, &ntot);
-    if (ntot > (uint32_t)kList) return false;
+    // (no closing barrier: the list barrier below orders the reads of s_u)
+    uint32_t o = block_excl_sum<false>((uint32_t)(__popcll(m) + __popc(mt) + (pre ? 1 : 0)), s_u, &ntot);
+    if (ntot > (uint32_t)kList) {
+        __syncthreads();  // (the row-wise parse writes s_u next)
+        return false;
+    }
     if (pre) list[o++] = (uint16_t)(kPre - 1);
     // (three 32-bit loops: a 64-bit find-first and clear cost twice the VALU)
     const uint32_t mw[3] = {(uint32_t)m, (uint32_t)(m >> 32), mt};
@@ -800,14 +806,15 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
             mx = max(mx, y);
         }
     }
-    if (bad) s_f0[1] = 1;  // (__syncthreads_or costs ~26 VALU a wave)
-    __syncthreads();
-    if (s_f0[1]) return false;
+    // min/max go to LDS before the one barrier that also publishes the flag (a chunk
+    // that fails re-initialises them for the row-wise parse)
     if ((uint32_t)tid < S) {  // LDS atomics (a shuffle tree cost ~50 VALU a wave)
         atomicMin(&s_mm[2 * col], mn);
         atomicMax(&s_mm[2 * col + 1], mx);
     }
-    return true;
+    if (bad) s_f0[1] = 1;  // (__syncthreads_or costs ~26 VALU a wave)
+    __syncthreads();
+    return s_f0[1] == 0;
 }
 
 // ---- pass 2: parse. One block per chunk. The chunk's row starts stay as one
@@ -849,10 +856,13 @@ __global__ __launch_bounds__(kTPB) void k_csv_parse(const char* __restrict__ tex
         const uint64_t rb = row_base[c];
         const uint64_t R = (c + 1 < gridDim.x ? row_base[c + 1] : rows) - rb;
         if (parse_chunk_tokens(s, s_list, s_u, s_f0, s_mm, s_lead, rb, (uint32_t)R, ncols, cols)) {
-            __syncthreads();
-            for (int j = tid; j < ncols; j += kTPB)
+            for (int j = tid; j < ncols; j += kTPB)  // (after the flag barrier: every atomic is in)
                 partial[c * (uint64_t)ncols + j] = make_int2(s_mm[2 * j], s_mm[2 * j + 1]);
             return;
+        }
+        for (int j = tid; j < ncols; j += kTPB) {  // (ordered before the row-wise atomics by its scan)
+            s_mm[2 * j] = INT_MAX;
+            s_mm[2 * j + 1] = INT_MIN;
         }
     }
     unsigned long long st = real_starts(s, cs, ce, tid);
