@@ -677,12 +677,6 @@ __device__ __forceinline__ int32_t next_token_nl(const uint8_t* __restrict__ s, 
 // parse then rewrites those rows.
 constexpr int kTokSeg = (kChunk + kHalo) / kTPB;  // 68 bytes classified per lane
 constexpr int kTokMaxCols = 16;
-#ifndef MQ_CSV_NEGW
-#define MQ_CSV_NEGW 0  // A/B: a token's '-' from its window words instead of an LDS byte read
-#endif
-#ifndef MQ_CSV_MASKA
-#define MQ_CSV_MASKA 0  // A/B: the lead masks computed instead of read from s_lead
-#endif
 static_assert((kChunk + kHalo) % kTPB == 0 && kTokSeg % 4 == 0 && kTokSeg < 64 + 32, "classification in words");
 
 __device__ __forceinline__ uint32_t below_2d(uint32_t x) {  // 0x80 in each byte < 0x2D
@@ -772,24 +766,9 @@ __device__ bool parse_chunk_tokens(const uint8_t* __restrict__ s, uint16_t* __re
             const uint32_t e0 = w[a2], e1 = w[a2 + 1], e2 = w[a2 + 2], e3 = w[a2 + 3];
             const uint32_t x0 = __builtin_amdgcn_alignbyte(e1, e0, r2), x1 = __builtin_amdgcn_alignbyte(e2, e1, r2),
                            x2 = __builtin_amdgcn_alignbyte(e3, e2, r2);
-#if MQ_CSV_NEGW
-            // byte pb + 1 is byte 12 - L of the window (L in 1..11; else no valid negative)
-            const uint32_t jn = 12u - L;
-            const uint32_t cn = jn < 4u ? __builtin_amdgcn_perm(x1, x0, jn) : __builtin_amdgcn_perm(x2, x1, jn - 4u);
-            const uint32_t neg = ((L - 1u < 11u) & ((cn & 0xFFu) == (uint32_t)'-')) ? 1u : 0u;
-#else
             const uint32_t neg = s[pb + 1] == '-' ? 1u : 0u;  // (L == 0: that byte is the separator)
-#endif
             const uint32_t Ld = L - neg;  // digits
-#if MQ_CSV_MASKA
-            const uint32_t z8 = 8u * (12u - min(Ld, 12u));  // leading bits that are not digits
-            const uint32_t m0 = z8 >= 32u ? 0u : ~0u << z8;
-            const uint32_t m1 = z8 >= 64u ? 0u : z8 <= 32u ? ~0u : ~0u << (z8 - 32u);
-            const uint32_t m2 = z8 >= 96u ? 0u : z8 <= 64u ? ~0u : ~0u << (z8 - 64u);
-            const uint4 mk = make_uint4(m0, m1, m2, 0u);
-#else
             const uint4 mk = s_lead[12u - min(Ld, 12u)];  // keeps the last Ld bytes of 12
-#endif
             // digit values: byte ^ '0' (no borrows: a digit byte is 0x30 | d), the bytes
             // before the digits cleared; a byte that is not a digit gives a value > 9
             const uint32_t d0 = (x0 ^ 0x30303030u) & mk.x;
