@@ -47,6 +47,9 @@ int radix_sort_pairs(const int* keys, const int* vals, uint64_t n, uint32_t** ke
 // (int32, may be NULL) and positions (size_t rows, may be NULL). Synchronises.
 int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* positions, hipStream_t st);
 
+// Frees the calling thread's pinned upload staging of shared_select (mq_shared.hip).
+void shared_staging_release();
+
 // Caching device allocator for per-call scratch (join tables and partitions,
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
 // idle blocks are released by mq_trim(). A freed block may be handed out again at

@@ -98,9 +98,10 @@ __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long
 // In-kernel combine (replaces the k_final launch on the fused paths). Arrival
 // counters: 8 shards (blockIdx % 8, one per XCD under round-robin placement, so no
 // word takes more than 1/8 of the arrivals) + a top counter. Zero at module load;
-// the last arriver resets them, so consecutive launches on a stream reuse a slot
-// without a memset. Slots rotate on the host so concurrent launches on different
-// streams do not share counters (up to kArriveSlots in flight).
+// the last arriver resets them, so consecutive launches on a stream reuse a block
+// without a memset. Each (device, stream) owns its own counter block
+// (arrive_counters): launches on one stream run in order, so they can share it,
+// and launches on different streams never do, however many are in flight.
 // Ordering without an L2 writeback: the partial is stored write-through (sc1),
 // `s_waitcnt vmcnt(0)` waits for those stores to be acknowledged before the
 // arrival add is issued, and the last block reads the partials with sc1 loads.
@@ -111,16 +112,14 @@ __device__ __forceinline__ void block_store_partial(unsigned long long cnt, long
 // chain) and saves a launch on small ones.
 // Each counter sits on its own 4 KiB line: atomics on one line serialise at about
 // 12 ns each (2048 arrivals on one line measured +45 us per launch).
-constexpr int kArriveSlots = 16;
 constexpr int kArriveStride = 1024;  // uints = 4 KiB
-__device__ unsigned int g_arrive[kArriveSlots][9 * kArriveStride];
+constexpr size_t kArriveBytes = 9 * kArriveStride * sizeof(unsigned int);
 
 // Called by every block after block_store_partial; true in the last block to
 // arrive, which then sees every block's partial.
-__device__ __forceinline__ bool block_arrive_last(uint32_t nblocks, uint32_t slot) {
+__device__ __forceinline__ bool block_arrive_last(uint32_t nblocks, unsigned int* ctr) {
     __shared__ int s_last;
     if (threadIdx.x == 0) {
-        unsigned int* ctr = g_arrive[slot];
         const uint32_t shard = blockIdx.x & 7u;
         const uint32_t shard_n = (nblocks - shard + 7u) / 8u;  // blocks b < nblocks, b % 8 == shard
         __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0): partial stores acked
@@ -239,7 +238,7 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
                                                const int* __restrict__ aux, uint64_t n,
                                                uint64_t rows_per_block, Pred pred,
                                                Partial* __restrict__ part,
-                                               mq_agg* __restrict__ out, uint32_t slot) {
+                                               mq_agg* __restrict__ out, unsigned int* __restrict__ arrive) {
     const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
     uint64_t end = start + rows_per_block;
     if (end > n) end = n;
@@ -332,7 +331,7 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
     // out != nullptr: the last block to finish folds all partials (no k_final launch)
     if (out) {
         block_store_partial<true>(cnt, sum, mn, mx, part);
-        if (block_arrive_last(gridDim.x, slot)) block_combine(part, gridDim.x, out);
+        if (block_arrive_last(gridDim.x, arrive)) block_combine(part, gridDim.x, out);
     } else {
         block_store_partial(cnt, sum, mn, mx, part);
     }
@@ -1277,7 +1276,7 @@ __global__ __launch_bounds__(kTPB, 6) void k_scan_gather(const int* __restrict__
                                                          const int* __restrict__ aux, uint64_t n,
                                                          uint64_t rows_per_block, Pred pred,
                                                          Partial* __restrict__ part,
-                                                         mq_agg* __restrict__ out, uint32_t slot) {
+                                                         mq_agg* __restrict__ out, unsigned int* __restrict__ arrive) {
     __shared__ uint32_t s_buf[kWaves][kGBuf];
     const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
     uint64_t end = start + rows_per_block;
@@ -1367,7 +1366,7 @@ __global__ __launch_bounds__(kTPB, 6) void k_scan_gather(const int* __restrict__
     const unsigned long long c_lane = lane == 0 ? cnt : 0ull;
     if (out) {
         block_store_partial<true>(c_lane, sumv, mnv, mxv, part);
-        if (block_arrive_last(gridDim.x, slot)) block_combine(part, gridDim.x, out);
+        if (block_arrive_last(gridDim.x, arrive)) block_combine(part, gridDim.x, out);
     } else {
         block_store_partial(c_lane, sumv, mnv, mxv, part);
     }
@@ -1600,24 +1599,62 @@ const void* scan_fn(bool vec) {
                : reinterpret_cast<const void*>(&k_scan<MODE, false>);
 }
 
+// The arrival counters of block_arrive_last for launches on stream st of the
+// current device: one zeroed 36 KiB block per (device, stream), made on first use
+// (the zeroing memset is queued on st ahead of the first launch that uses it).
+// Launches on one stream run in order and the last arriver of each resets the
+// counters, so every launch on that stream finds them zero; launches on different
+// streams use different blocks, so any number of them may be in flight. (A fixed
+// pool of slots handed out in rotation let >16 concurrent launches, e.g. row shards
+// on one device, share counters and fold wrong partials.) The per-thread default
+// stream is one stream per thread, so its blocks are keyed by thread as well.
+unsigned int* arrive_counters(hipStream_t st) {
+    struct Key {
+        int dev;
+        hipStream_t st;
+        std::thread::id th;
+    };
+    struct Entry {
+        Key k;
+        unsigned int* ctr;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> tab;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::thread::id th = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+    std::lock_guard<std::mutex> lk(mu);
+    for (const Entry& e : tab)
+        if (e.k.dev == dev && e.k.st == st && e.k.th == th) return e.ctr;
+    void* p = nullptr;
+    if (hipMalloc(&p, kArriveBytes) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kArriveBytes, st) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    tab.push_back(Entry{Key{dev, st, th}, static_cast<unsigned int*>(p)});
+    return static_cast<unsigned int*>(p);
+}
+
 // Launch k_scan<MODE> over n rows; returns the number of blocks (partials) via *g_out.
 // out != nullptr folds the partials inside the launch (block_arrive_last).
 template <int MODE>
 int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
                 mq_agg* out, hipStream_t st, const DevState* s, uint32_t* g_out,
                 uint64_t* rpb_out = nullptr) {
-    static std::atomic<uint32_t> next_slot{0};
-    const uint32_t slot = out ? next_slot.fetch_add(1, std::memory_order_relaxed) % kArriveSlots : 0;
+    unsigned int* arrive = nullptr;
+    if (out && !(arrive = arrive_counters(st)))
+        return set_err(MQ_ENOMEM, "arrival counters for the stream could not be allocated");
     const bool vec = aligned16(col);
     uint32_t g;
     uint64_t rpb;
     geometry(s, n, scan_fn<MODE>(vec), &g, &rpb);
     if (vec)
         hipLaunchKernelGGL((k_scan<MODE, true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
-                           part, out, slot);
+                           part, out, arrive);
     else
         hipLaunchKernelGGL((k_scan<MODE, false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
-                           part, out, slot);
+                           part, out, arrive);
     LAUNCHCHK("k_scan");
     *g_out = g;
     if (rpb_out) *rpb_out = rpb;
@@ -1628,17 +1665,17 @@ int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Part
 // in-kernel into *out.
 int launch_gather(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
                   mq_agg* out, hipStream_t st, const DevState* s) {
-    static std::atomic<uint32_t> next_slot{0};
-    const uint32_t slot = next_slot.fetch_add(1, std::memory_order_relaxed) % kArriveSlots;
+    unsigned int* arrive = arrive_counters(st);
+    if (!arrive) return set_err(MQ_ENOMEM, "arrival counters for the stream could not be allocated");
     const bool vec = aligned16(col);
     const void* fn = vec ? (const void*)&k_scan_gather<true> : (const void*)&k_scan_gather<false>;
     uint32_t g;
     uint64_t rpb;
     geometry(s, n, fn, &g, &rpb);
     if (vec)
-        hipLaunchKernelGGL((k_scan_gather<true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, slot);
+        hipLaunchKernelGGL((k_scan_gather<true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, arrive);
     else
-        hipLaunchKernelGGL((k_scan_gather<false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, slot);
+        hipLaunchKernelGGL((k_scan_gather<false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p, part, out, arrive);
     LAUNCHCHK("k_scan_gather");
     return MQ_OK;
 }
@@ -1951,6 +1988,27 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
         if (c + kStageBufs < nchunks && (rc = issue(c + kStageBufs))) return rc;
     }
     return MQ_OK;
+}
+
+// mq_thread_release (mq_device.h): the calling thread's pinned staging buffers and
+// their events, on every device it staged through. A thread that exits without it
+// leaks them (thread_local storage is not freed by the runtime).
+void mq_thread_release(void) {
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (int d = 0; d < kMaxDev; d++) {
+        Staging& S = g_staging[d];
+        if (!S.ready) continue;
+        if (hipSetDevice(d) != hipSuccess) continue;
+        for (int i = 0; i < kStageBufs; i++) {
+            (void)hipEventSynchronize(S.ev[i]);
+            (void)hipEventDestroy(S.ev[i]);
+            (void)hipHostFree(S.buf[i]);
+        }
+        S = Staging{};
+    }
+    if (have_cur) (void)hipSetDevice(cur);
+    mqi::shared_staging_release();
 }
 
 // The mirror of the staged D2H: the pool copies chunk c into pinned buffer c % 4

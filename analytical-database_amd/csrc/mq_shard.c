@@ -60,7 +60,8 @@ typedef struct Shard {
 static Shard g_sh[MAXS];
 static int g_G = -1;        /* shard count; 1 = off */
 static size_t g_min_rows;
-static int g_started;
+static int g_started;       /* 1 = workers up, -1 = start failed (one device from then on) */
+static int g_live;          /* workers running: g_sh[0 .. g_live) */
 
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t g_go = PTHREAD_COND_INITIALIZER, g_done = PTHREAD_COND_INITIALIZER;
@@ -96,6 +97,11 @@ static void configure(void) {
     for (int g = 0; g < G; g++) {
         g_sh[g].idx = g;
         g_sh[g].dev = nd > 0 ? devs[g % nd] : (primary + g) % count;
+        if (G > 1 && (g_sh[g].dev < 0 || g_sh[g].dev >= count)) { /* as mq_shard_config refuses */
+            fprintf(stderr, "libmq: MQ_DEVICES names device %d of %d; row shards off\n", g_sh[g].dev, count);
+            G = 1;
+            break;
+        }
     }
     const char* m = getenv("MQ_SHARD_MIN_ROWS");
     g_min_rows = m ? (size_t)strtoull(m, NULL, 10) : ((size_t)1 << 24);
@@ -127,18 +133,18 @@ static int run_all(void (*fn)(Shard*, void*), void* arg) {
     pthread_mutex_lock(&g_mu);
     g_fn = fn;
     g_arg = arg;
-    g_pending = g_G;
+    g_pending = g_live;
     g_gen++;
     pthread_cond_broadcast(&g_go);
     while (g_pending) pthread_cond_wait(&g_done, &g_mu);
     pthread_mutex_unlock(&g_mu);
     double x = 0; /* the shards copy in parallel: the task's transfer time is the longest */
-    for (int g = 0; g < g_G; g++) {
+    for (int g = 0; g < g_live; g++) {
         if (g_sh[g].xfer > x) x = g_sh[g].xfer;
         g_sh[g].xfer = 0;
     }
     shim_xfer_add(x);
-    for (int g = 0; g < g_G; g++)
+    for (int g = 0; g < g_live; g++)
         if (g_sh[g].rc) return g_sh[g].rc;
     return 0;
 }
@@ -150,6 +156,17 @@ static void t_init(Shard* s, void* arg) {
     s->rc = mq_malloc(&s->small, 4096);
 }
 
+static void t_stop(Shard* s, void* a);
+
+/* Stop every running worker (each frees its stream, scratch and pinned staging). */
+static void stop_workers(void) {
+    if (g_live > 0) run_all(t_stop, NULL);
+    g_live = 0;
+}
+
+/* Start the G workers and bind each to its device. On any failure the workers
+ * already running are stopped again and row shards stay off for the process: the
+ * operators then run on one device (shard_wants() is 0). */
 static int start(Status* st) {
     if (g_started == 1) return 0;
     if (g_started == -1) return shim_fail(st, "row shards (earlier)", MQ_ENODEV);
@@ -158,15 +175,21 @@ static int start(Status* st) {
     pthread_mutex_unlock(&g_mu);
     for (int g = 0; g < g_G; g++) {
         g_sh[g].gen0 = gen0;
+        g_sh[g].quit = 0;
         if (pthread_create(&g_sh[g].th, NULL, worker, &g_sh[g]) != 0) {
+            stop_workers();
             g_started = -1;
+            fprintf(stderr, "libmq: shard worker start failed; row shards off\n");
             return shim_fail(st, "shard worker start", MQ_EINVAL);
         }
         pthread_detach(g_sh[g].th);
+        g_live = g + 1;
     }
     int rc = run_all(t_init, NULL);
     if (rc) {
+        stop_workers();
         g_started = -1;
+        fprintf(stderr, "libmq: shard device init failed (%s); row shards off\n", mq_last_error());
         return shim_fail(st, "shard device init", rc);
     }
     g_started = 1;
@@ -178,10 +201,19 @@ int shard_count(void) {
     return g_G;
 }
 
+/* Whether an operator on column c fans out over the row shards. Starts the workers
+ * on first use; a failed start turns shards off, and the operator (this one and every
+ * later one) runs on the one-device path instead of failing. */
 int shard_wants(const Column* c) {
     configure();
-    return g_G > 1 && c && c->row_count >= g_min_rows && c->row_count >= (size_t)g_G &&
-           c->row_count <= (size_t)INT32_MAX;
+    if (!(g_G > 1 && c && c->row_count >= g_min_rows && c->row_count >= (size_t)g_G &&
+          c->row_count <= (size_t)INT32_MAX))
+        return 0;
+    if (g_started == 0) {
+        Status tmp;
+        (void)start(&tmp);
+    }
+    return g_started == 1;
 }
 
 /* Per-shard scratch on the worker's device (grow-only, pool memory). */
@@ -706,9 +738,12 @@ void shard_stats(mq_residency* out) {
 
 static void t_stop(Shard* s, void* a) {
     (void)a;
-    t_trim(s, NULL);
-    mq_stream_destroy(s->stream);
+    if (s->stream) { /* a worker whose t_init failed early has nothing on its device */
+        t_trim(s, NULL);
+        mq_stream_destroy(s->stream);
+    }
     mq_free(s->small);
+    mq_thread_release(); /* the worker's pinned staging (it exits after this task) */
     s->stream = s->small = NULL;
     s->quit = 1;
 }
@@ -716,10 +751,8 @@ static void t_stop(Shard* s, void* a) {
 /* mq_shard_config (mq_query.h): drop every sharded copy, stop the workers, then take
  * the new layout (G <= 0: back to the environment's). */
 int mq_shard_config(int shards, const int* devices, int ndev, uint64_t min_rows) {
-    if (g_started == 1) {
-        shard_release_all();
-        run_all(t_stop, NULL);
-    }
+    if (g_started == 1) shard_release_all();
+    stop_workers();
     g_started = 0;
     g_G = -1;
     if (shards <= 0) return MQ_OK;

@@ -908,6 +908,30 @@ Staging& staging_slot(int dev, int which) {
     static thread_local Staging st[kMaxDev][2];
     return st[dev][which];
 }
+}  // namespace
+
+namespace mqi {
+// Frees the calling thread's pinned staging on every device (mq_thread_release).
+void shared_staging_release() {
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (int d = 0; d < kMaxDev; d++)
+        for (int w = 0; w < 2; w++) {
+            Staging& S = staging_slot(d, w);
+            if (!S.p && !S.ev) continue;
+            if (hipSetDevice(d) != hipSuccess) continue;
+            if (S.ev) {
+                (void)hipEventSynchronize(S.ev);
+                (void)hipEventDestroy(S.ev);
+            }
+            if (S.p) (void)hipHostFree(S.p);
+            S = Staging{};
+        }
+    if (have_cur) (void)hipSetDevice(cur);
+}
+}  // namespace mqi
+
+namespace {
 int staging_get(int which, size_t bytes, char** p) {
     int dev;
     int rc = current_device(&dev);

@@ -109,6 +109,7 @@ _SIGS = {
     "mq_memcpy_d2h_staged": (_int, [_vp, _vp, _sz, _vp]),
     "mq_stream_create": (_int, [C.POINTER(_vp)]),
     "mq_stream_destroy": (_int, [_vp]),
+    "mq_thread_release": (None, []),
     "mq_fetch_at": (_int, [_vp, _i32, _vp, _u64, _vp, _vp]),
     "mq_memset": (_int, [_vp, _int, _sz, _vp]),
     "mq_stream_sync": (_int, [_vp]),

@@ -65,6 +65,11 @@ int mq_stream_destroy(void* stream);
 /* Release the device scratch libmq keeps cached between calls (join tables and
  * partition buffers, probe arrays); the next call allocates afresh. */
 void mq_trim(void);
+/* Free the calling thread's pinned host staging buffers (the staged D2H/H2D ring
+ * and shared_select's upload staging) on every device. A thread that stops using
+ * libmq calls it before it exits (the row-shard workers do); later staged copies
+ * on the thread allocate afresh. */
+void mq_thread_release(void);
 /* The same caching allocator for callers (the query layer keeps result shadows
  * and column copies in it): a freed block may be handed out again at once, so
  * free only what no queued work still uses. mq_pool_free also accepts pointers

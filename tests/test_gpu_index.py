@@ -205,3 +205,45 @@ def test_index_build_1e9_properties(lib):
     seen = np.zeros(n, dtype=np.bool_)
     seen[ps.astype(np.int64)] = True
     assert seen.all()
+
+
+def _qs_cases():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "quicksort_goldens.json")
+    for c in json.load(open(path)):
+        marks = [pytest.mark.big] if c["n"] > (1 << 24) else []
+        yield pytest.param(c, marks=marks, id=f"2^{c['log2n']}_s{c['seed']}_m{c['modulus']}")
+
+
+@pytest.mark.parametrize("case", list(_qs_cases()))
+def test_index_build_lomuto_full_size(lib, refcpu, case):
+    """the exact tie order at the sizes build_index applies it to
+    (up to MQ_INDEX_EXACT_MAX = 2^27 rows), against the reference's own quicksort
+    (tests/golden/quicksort_goldens.json, made by the `quicksort` symbol of the
+    reference's index.c, make_quicksort_goldens.py). Both entry points:
+    mq_index_build_lomuto, and mq_index_build_ref (the build_index policy: radix sort,
+    tie check, then the Lomuto restatement) with exact_max = 2^27. Up to 2^24 rows the
+    arrays are also compared element by element with the restatement
+    rc_index_build_lomuto (refcpu.c, itself pinned to the same symbol)."""
+    n = case["n"]
+    col = Dev(n * 4)
+    mq.check(lib.mq_gen_uniform(col.ptr, n, case["seed"], case["modulus"], None))
+    h = col.get(np.int32, n)
+    assert f"{refcpu.fnv1a64(h):016x}" == case["col_fnv"]
+    v, p = Dev(n * 4), Dev(n * 8)
+    mq.check(lib.mq_index_build_lomuto(col.ptr, n, v.ptr, p.ptr, None), "mq_index_build_lomuto")
+    hv, hp = v.get(np.int32, n), p.get(np.uint64, n)
+    assert f"{refcpu.fnv1a64(hv):016x}" == case["values_fnv"]
+    assert f"{refcpu.fnv1a64(hp):016x}" == case["positions_fnv"]
+    if n <= (1 << 24):
+        wv, wp = refcpu.index_build_lomuto(h)
+        assert np.array_equal(hv, wv) and np.array_equal(hp, wp)
+    del hv, hp
+    ex = C.c_int(-1)
+    mq.check(lib.mq_memset(v.ptr, 0, n * 4, None))
+    mq.check(lib.mq_memset(p.ptr, 0, n * 8, None))
+    mq.check(lib.mq_index_build_ref(col.ptr, n, v.ptr, p.ptr, 1 << 27, C.byref(ex), None))
+    assert ex.value == 1
+    assert f"{refcpu.fnv1a64(v.get(np.int32, n)):016x}" == case["values_fnv"]
+    assert f"{refcpu.fnv1a64(p.get(np.uint64, n)):016x}" == case["positions_fnv"]

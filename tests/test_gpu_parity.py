@@ -139,6 +139,58 @@ def test_select_sum_in_kernel_combine_repeated(lib, refcpu):
             assert (a.count, a.sum) == want[n], (r, n)
 
 
+def test_select_sum_in_kernel_combine_32_streams(lib, refcpu):
+    """the in-kernel combine's arrival counters belong to the
+    launch's stream, so launches in flight on many streams at once never share them
+    (a pool of 16 slots handed out in rotation did). 32 streams, each with its own
+    workspace, queue 6 mq_select_sum launches back to back and alternate with the
+    fused fetch + aggregate (mq_select_fetch_agg, the other in-kernel combine); no
+    host sync until every launch is queued; every result equals the oracle."""
+    nstreams, reps = 32, 6
+    sizes = [1024 * 5 + 3, 1 << 18, 1_000_003, 4_000_037]
+    data = {n: _data(n, 2000 + n) for n in sizes}
+    aux = {n: _data(n, 3000 + n) for n in sizes}
+    devs = {n: Dev.of(d) for n, d in data.items()}
+    dauxs = {n: Dev.of(a) for n, a in aux.items()}
+    want, want_aux = {}, {}
+    for n, d in data.items():
+        p = refcpu.select_scan(d, -5, 5)
+        want[n] = (len(p), int(d[p].astype(np.int64).sum()))
+        a = aux[n][p]
+        want_aux[n] = (len(a), int(a.astype(np.int64).sum()), int(a.min()), int(a.max()))
+    streams = []
+    for _ in range(nstreams):
+        sp = C.c_void_p()
+        mq.check(lib.mq_stream_create(C.byref(sp)))
+        streams.append(sp.value)
+    big = max(sizes)
+    ws = [Dev(lib.mq_scan_workspace_bytes(big)) for _ in range(nstreams)]
+    outs = [[Dev(32) for _ in range(reps)] for _ in range(nstreams)]
+    hl, l, hh, h = mq.bounds(-5, 5)
+    plan = []
+    for r in range(reps):
+        for s in range(nstreams):
+            n = sizes[(s + r) % len(sizes)]
+            fused = (s + r) % 3 == 0
+            if fused:
+                mq.check(lib.mq_select_fetch_agg(devs[n].ptr, dauxs[n].ptr, n, hl, l, hh, h,
+                                                 outs[s][r].ptr, ws[s].ptr, ws[s].nbytes, streams[s]))
+            else:
+                mq.check(lib.mq_select_sum(devs[n].ptr, n, hl, l, hh, h, outs[s][r].ptr,
+                                           ws[s].ptr, ws[s].nbytes, streams[s]))
+            plan.append((s, r, n, fused))
+    for sp in streams:
+        mq.check(lib.mq_stream_sync(sp))
+    for s, r, n, fused in plan:
+        a = mq.MqAgg.from_buffer_copy(outs[s][r].get(np.uint8, 32).tobytes())
+        if fused:
+            assert (a.count, a.sum, a.min, a.max) == want_aux[n], (s, r, n)
+        else:
+            assert (a.count, a.sum) == want[n], (s, r, n)
+    for sp in streams:
+        mq.check(lib.mq_stream_destroy(sp))
+
+
 @pytest.mark.parametrize("n", [0, 7, 4097, 200_003, 3_000_017])
 def test_select_result_payload_vs_oracle(lib, refcpu, n, pos_impl):
     rng = np.random.default_rng(n + 1)

@@ -87,3 +87,28 @@ def test_lomuto_restatement_equals_reference_quicksort(refcpu, name, col):
     v, p = refcpu.index_build_lomuto(col)
     assert np.array_equal(v, rv), name
     assert np.array_equal(p, rp), name
+
+
+def _qs_goldens():
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "quicksort_goldens.json")
+    return [c for c in json.load(open(path)) if c["log2n"] == 22]
+
+
+@pytest.mark.parametrize("case", _qs_goldens(), ids=lambda c: f"s{c['seed']}_m{c['modulus']}")
+def test_lomuto_restatement_2e22_vs_reference_quicksort(refcpu, case):
+    """rc_index_build_lomuto (the iterative restatement the GPU
+    tests compare with) against the reference's own quicksort at 2^22 rows: the
+    goldens that symbol produced (make_quicksort_goldens.py) and, where libdbm.so is
+    built, a fresh run of the symbol itself on the seed-42 column."""
+    n = case["n"]
+    col = refcpu.gen_uniform(n, case["seed"], case["modulus"])
+    assert f"{refcpu.fnv1a64(col):016x}" == case["col_fnv"]
+    v, p = refcpu.index_build_lomuto(col)
+    assert f"{refcpu.fnv1a64(v):016x}" == case["values_fnv"]
+    assert f"{refcpu.fnv1a64(p):016x}" == case["positions_fnv"]
+    assert int(np.count_nonzero(v[1:] == v[:-1])) == case["ties"]
+    import refload
+    if case["seed"] == 42 and refload.have():
+        rv, rp = refload.quicksort(col)
+        assert np.array_equal(v, rv) and np.array_equal(p, rp)
