@@ -217,9 +217,13 @@ static int h2d(void* d, const void* h, size_t bytes) {
     return rc;
 }
 
+/* The transfer clock starts once the stream is idle, so mq_transfer_seconds counts
+ * the copies alone, not the kernels they wait for. */
 static int d2h(void* h, const void* d, size_t bytes) {
+    int rc = mq_stream_sync(g_stream);
+    if (rc) return rc;
     double t0 = now_s();
-    int rc = mq_memcpy_d2h(h, d, bytes, g_stream);
+    rc = mq_memcpy_d2h(h, d, bytes, g_stream);
     g_xfer_s += now_s() - t0;
     return rc;
 }
@@ -227,8 +231,10 @@ static int d2h(void* h, const void* d, size_t bytes) {
 /* D2H into memory that will be write-guarded: through pinned staging, so the
  * guard's mprotect does not stall the GPU (mq_memcpy_d2h_staged). */
 static int d2h_staged(void* h, const void* d, size_t bytes) {
+    int rc = mq_stream_sync(g_stream);
+    if (rc) return rc;
     double t0 = now_s();
-    int rc = mq_memcpy_d2h_staged(h, d, bytes, g_stream);
+    rc = mq_memcpy_d2h_staged(h, d, bytes, g_stream);
     g_xfer_s += now_s() - t0;
     return rc;
 }

@@ -239,8 +239,10 @@ static int ensure(Shard* s, size_t rows) {
  * buffers) when the payload will be write-guarded, see mq_memcpy_d2h_staged. */
 static int download(Shard* s, void* host, const void* dev, size_t bytes, int staged) {
     if (!bytes) return 0;
+    int rc = mq_stream_sync(s->stream); /* the transfer clock counts the copy alone */
+    if (rc) return rc;
     double t0 = shim_now();
-    int rc = staged ? mq_memcpy_d2h_staged(host, dev, bytes, s->stream) : mq_memcpy_d2h(host, dev, bytes, s->stream);
+    rc = staged ? mq_memcpy_d2h_staged(host, dev, bytes, s->stream) : mq_memcpy_d2h(host, dev, bytes, s->stream);
     s->xfer += shim_now() - t0;
     return rc;
 }

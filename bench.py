@@ -289,6 +289,7 @@ def main() -> None:
         extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold,
                            cpu=not args.no_cpu)
 
+    bad = []
     if rank == 0:
         ms_step = 1e3 * elapsed / args.steps
         gbs = 4.0 * n / (k_mean_ms * 1e-3) / 1e9
@@ -324,9 +325,33 @@ def main() -> None:
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(n)
+        bad = parity_failures(out)
+        out["parity_failures"] = bad
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    # fail loudly: a wrong combined count/sum on any rank, or any
+    # extra leg's parity check false on rank 0, makes the run exit non-zero after the
+    # JSON line is out
+    if parity is False or (rank == 0 and bad):
+        print(f"bench.py: parity FAILED: {'headline' if parity is False else ''} {bad}", file=sys.stderr)
+        sys.exit(1)
+
+
+def parity_failures(out: dict) -> list:
+    """Paths of every parity flag in the record that is False (headline and extras)."""
+    bad = []
+
+    def walk(x, path):
+        if isinstance(x, dict):
+            for k, v in x.items():
+                p = f"{path}/{k}"
+                if (k.startswith("parity") or k in ("ok", "identical")) and v is False:
+                    bad.append(p)
+                walk(v, p)
+
+    walk(out, "")
+    return bad
 
 
 def achievable_read_peak(lib, mq, torch, stream, col, ws, launches: int = 20) -> dict:
@@ -349,6 +374,30 @@ def achievable_read_peak(lib, mq, torch, stream, col, ws, launches: int = 20) ->
     med = statistics.median(ms)
     return {"kernel": "k_stream_read", "gbs": nbytes.value / (med * 1e-3) / 1e9,
             "bytes": nbytes.value, "ms_median": med}
+
+
+def pcie_probe(torch, dev, stream, nbytes: int = 256 << 20, reps: int = 5) -> dict:
+    """The host link's rate on this box: hipMemcpy of a 256 MB
+    pinned host buffer to and from HBM (torch pinned tensors, copies on `stream`),
+    median of `reps` after one warm-up. The drop-in API's transfers (api_leg) are
+    judged against these."""
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = {"bytes": nbytes}
+    with torch.cuda.stream(stream):
+        for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)),
+                         ("d2h", lambda: h.copy_(d, non_blocking=True))):
+            ts = []
+            for i in range(reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                if i:
+                    ts.append(time.perf_counter() - t0)
+            out[f"{name}_gbs"] = nbytes / statistics.median(ts) / 1e9
+    del h, d
+    return out
 
 
 def print_leg(lib, mq, torch, dev, stream, pos, k, cpu: bool = True) -> dict:
@@ -491,6 +540,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
     out["config5_many_to_many"] = join_dup_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
     out["load_csv_config3_table"] = load_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["index_build"] = index_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
+    out["pcie_probe"] = pcie_probe(torch, dev, stream)
     out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
     return out
 
@@ -530,10 +580,11 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
     mq.check(lib.mq_column_upload(C.byref(col1)), "upload col1")
     t_up = time.perf_counter() - t0
     lo_c, hi_c = C.c_int(lo), C.c_int(hi)
-    times = {"select_column": [], "fetch_column": [], "average": []}
+    times = {"select_column": [], "fetch_column": [], "average": [], "free_results": []}
+    xfers = []
     avg = None
     k = 0
-    for rep in range(4):
+    for rep in range(5):
         st = mq.Status(0, None)
         lib.mq_transfer_seconds(1)
         t0 = time.perf_counter()
@@ -547,15 +598,23 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
         xfer = lib.mq_transfer_seconds(0)
         k = rp.contents.num_tuples
         avg = C.cast(ra.contents.payload, C.POINTER(C.c_double))[0]
+        t4 = time.perf_counter()
         for r in (rp, rf, ra):
             _libc.free(r.contents.payload)
             _libc.free(r)
+        t5 = time.perf_counter()
         if rep:
             times["select_column"].append(t1 - t0)
             times["fetch_column"].append(t2 - t1)
             times["average"].append(t3 - t2)
+            times["free_results"].append(t5 - t4)
+            xfers.append((xfer, t3 - t0))
     med = {f"ms_{name}": 1e3 * statistics.median(v) for name, v in times.items()}
-    chain_s = sum(med.values()) / 1e3
+    chain_s = (med["ms_select_column"] + med["ms_fetch_column"] + med["ms_average"]) / 1e3
+    # transfer share of the same reps: the median rep by chain time, its D2H seconds
+    # (counted from an idle stream, so kernels are not in them)
+    xfers.sort(key=lambda x: x[1])
+    x_med, wall_med = xfers[len(xfers) // 2]
     want = next((r for r in gold["config3"] if r["n"] == n and r["low"] == lo and r["high"] == hi), None)
     resid = mq.residency(lib)
     lib.mq_release_all()
@@ -563,10 +622,13 @@ def api_leg(lib, mq, n, lo, hi, gold) -> dict:
            "residency": {"column_uploads": resid["column_uploads"], "guards_live": resid["guards_live"],
                          "result_uploads": resid["result_uploads"]},
            "upload_gbs": 8.0 * n / t_up / 1e9, **med, "ms_chain": 1e3 * chain_s,
-           "rows_per_s_chain": n / chain_s, "ms_transfer_last_chain": 1e3 * xfer,
+           "rows_per_s_chain": n / chain_s, "ms_transfer_median_chain": 1e3 * x_med,
+           "ms_wall_median_chain": 1e3 * wall_med,
+           "d2h_payload_gbs": 8.0 * k / x_med / 1e9 if x_med > 0 else None,
            "note": "PCIe-inclusive: each operator returns malloc'd host payloads (client_context.c "
-                   "frees them); the chain runs on HBM-resident columns after the one-off upload "
-                   "(memfd-backed columns, write-guarded)"}
+                   "frees them; ms_free_results is that free, outside the chain); the chain runs on "
+                   "HBM-resident columns after the one-off upload (memfd-backed columns, write-guarded); "
+                   "ms_transfer_median_chain and ms_wall_median_chain come from the same rep"}
     if want is not None:
         res["parity"] = (k, avg) == (want["k"], want["avg"])
     return res
@@ -609,19 +671,28 @@ def shared_leg(lib, mq, torch, dev, stream, col, n) -> dict:
             sws = lib.mq_scan_workspace_bytes(n)
             ws2 = torch.empty(sws, dtype=torch.uint8, device=dev)
             cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            one = torch.empty(n, dtype=torch.int32, device=dev)  # capacity n: any K fits
             ts = []
             for _ in range(3):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for j in range(q):
                     mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, int(lows[j]), 1, int(highs[j]),
-                                                     outs[j].data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
+                                                     one.data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
             t2 = statistics.median(ts)
-            del outs, ws, ws2
+            # parity: every query's K and positions equal the ordered select's (itself
+            # pinned to the 1e9 goldens), compared on the device
+            ok = True
+            for j in range(q):
+                mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, int(lows[j]), 1, int(highs[j]),
+                                                 one.data_ptr(), cnt.data_ptr(), ws2.data_ptr(), sws, sp))
+                kj = int(cnt.item())
+                ok = ok and kj == int(k[j]) and torch.equal(outs[j][:kj], one[:kj])
+            del outs, one, ws, ws2
         res[f"q{q}"] = {"ms_shared": 1e3 * t1, "ms_q_separate_selects": 1e3 * t2,
-                        "rows_x_queries_per_s": n * q / t1, "k_total": int(sum(k))}
+                        "rows_x_queries_per_s": n * q / t1, "k_total": int(sum(k)), "parity": bool(ok)}
     return res
 
 
@@ -830,6 +901,45 @@ def load_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
     return res
 
 
+def exact_index_leg(lib, mq, torch, dev, stream, logn: int = 27) -> dict:
+    """build_index's exact path at its size limit: the §8(c)
+    uniform column of 2^27 rows (seed 42, values in [0, 2^27): 49M tied neighbours),
+    sorted in the reference quicksort's own order. ms_lomuto = mq_index_build_lomuto
+    (the level-synchronous Lomuto restatement, one host sync per recursion depth);
+    ms_build_index = mq_index_build_ref as build_index runs it (radix sort, tie
+    check, then the Lomuto restatement); ms_radix = the radix sort alone. Parity: the
+    FNV of values and positions equal the goldens the reference's own quicksort made
+    (tests/golden/quicksort_goldens.json)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu  # checker only (FNV)
+    n = 1 << logn
+    sp = mq.stream_of(stream)
+    gold = [c for c in json.load(open(os.path.join(ROOT, "tests", "golden", "quicksort_goldens.json")))
+            if c["n"] == n and c["seed"] == 42 and c["modulus"] == n]
+    with torch.cuda.stream(stream):
+        c = torch.empty(n, dtype=torch.int32, device=dev)
+        mq.check(lib.mq_gen_uniform(c.data_ptr(), n, 42, n, sp), "gen")
+        v = torch.empty(n, dtype=torch.int32, device=dev)
+        p = torch.empty(n, dtype=torch.int64, device=dev)
+        ms_radix = _events_ms(torch, stream, lambda: mq.check(
+            lib.mq_index_build(c.data_ptr(), n, v.data_ptr(), p.data_ptr(), sp), "index_build"), 2)
+        ms_lomuto = _events_ms(torch, stream, lambda: mq.check(
+            lib.mq_index_build_lomuto(c.data_ptr(), n, v.data_ptr(), p.data_ptr(), sp), "lomuto"), 2)
+        ok_l = bool(gold) and (f"{refcpu.fnv1a64(v.cpu().numpy()):016x}", f"{refcpu.fnv1a64(p.cpu().numpy()):016x}") == \
+            (gold[0]["values_fnv"], gold[0]["positions_fnv"])
+        ex = C.c_int(-1)
+        ms_ref = _events_ms(torch, stream, lambda: mq.check(
+            lib.mq_index_build_ref(c.data_ptr(), n, v.data_ptr(), p.data_ptr(), n, C.byref(ex), sp), "ref"), 2)
+        ok_r = bool(gold) and ex.value == 1 and \
+            (f"{refcpu.fnv1a64(v.cpu().numpy()):016x}", f"{refcpu.fnv1a64(p.cpu().numpy()):016x}") == \
+            (gold[0]["values_fnv"], gold[0]["positions_fnv"])
+        del c, v, p
+    return {"rows": n, "ms_lomuto": ms_lomuto, "ms_build_index": ms_ref, "ms_radix": ms_radix,
+            "rows_per_s_build_index": n / (ms_ref * 1e-3), "parity": ok_l and ok_r,
+            "ties": gold[0]["ties"] if gold else None,
+            "path": "exact tie order (the reference quicksort's), as build_index applies it up to 2^27 rows"}
+
+
 def index_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
     """the sorted index of the 1e9-row column (mq_index_build:
     stable radix sort of (value, row) -> values + size_t positions). Parity: gather
@@ -848,8 +958,10 @@ def index_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
         del v, p, g
     res = {"rows": n, "ms": ms, "rows_per_s": n / (ms * 1e-3), "parity": ok,
            "hbm_bytes_design": 4 * 20 * n,
+           "path": "mq_index_build: the stable radix sort alone (equal values in ascending row order)",
            "note": "4 LSD passes of 8 bits: histogram (4N read) + scatter (8N read + 8N write) each, "
                    "+ key flip and emit"}
+    res["exact_2e27"] = exact_index_leg(lib, mq, torch, dev, stream)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refload  # the reference's quicksort, baseline only
     if cpu and refload.have():
