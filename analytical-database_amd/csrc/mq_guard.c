@@ -105,20 +105,38 @@ static void install(void) {
 }
 
 static void on_segv(int sig, siginfo_t* si, void* uc) {
+    /* the address this thread last returned for without an armed guard: a second
+     * fault there in a row is not a race with another handler, so it is handed on */
+    static __thread uintptr_t t_retry;
     const uintptr_t a = (uintptr_t)si->si_addr;
-    int hit = 0;
+    int hit = 0, covered = 0;
     if (si->si_code == SEGV_ACCERR) {
         const int hw = atomic_load_explicit(&g_hw, memory_order_acquire);
         for (int i = 0; i < hw; i++) {
             Guard* g = &g_guard[i];
-            if (atomic_load_explicit(&g->state, memory_order_acquire) != G_ARMED) continue;
-            if (a < g->lo || a >= g->hi) continue;
+            const int state = atomic_load_explicit(&g->state, memory_order_acquire);
+            if (state == G_FREE || a < g->lo || a >= g->hi) continue;
+            if (state != G_ARMED) {
+                covered = 1;
+                continue;
+            }
             mprotect((void*)g->lo, g->hi - g->lo, g->prot);
             atomic_store_explicit(&g->state, G_DIRTY, memory_order_release);
             hit = 1;
         }
     }
-    if (hit) return;
+    if (hit) {
+        t_retry = 0;
+        return;
+    }
+    /* Another thread's fault on the same guard (or a release) already gave the pages
+     * their protection back between this fault and the scan: re-execute the store
+     * once. A slot of any live state covering the address says so. */
+    if (covered && t_retry != a) {
+        t_retry = a;
+        return;
+    }
+    t_retry = 0;
     /* not ours: hand it on as if we were not here */
     if (g_prev.sa_flags & SA_SIGINFO) {
         if (g_prev.sa_sigaction) {
@@ -228,8 +246,15 @@ void mq_guard_forget_range(uintptr_t addr, size_t bytes) {
 }
 
 int mq_guard_chunk_ok(const void* p) {
-    /* glibc chunk header: the size word before p has IS_MMAPPED (0x2) set */
-    return p && (((const size_t*)p)[-1] & 2) != 0;
+    /* glibc's mmapped chunk: the header (prev_size, size) sits at the start of its own
+     * mapping, so p is 16 bytes past a page boundary, and the size word has IS_MMAPPED
+     * (0x2) set and counts whole pages. A block from another allocator (a preloaded
+     * malloc) almost never looks like that; one that does not is never guarded. */
+    if (!p) return 0;
+    const uintptr_t chunk = (uintptr_t)p - 2 * sizeof(size_t);
+    const size_t sz = ((const size_t*)p)[-1];
+    return (chunk & (page() - 1)) == 0 && (sz & 2) != 0 && ((sz & ~(size_t)7) & (page() - 1)) == 0 &&
+           (sz & ~(size_t)7) >= page();
 }
 
 uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {

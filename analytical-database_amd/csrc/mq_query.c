@@ -183,7 +183,7 @@ static int ready(Status* st) {
      * is what lets a write guard cover them; glibc's dynamic threshold would
      * otherwise rise to the last freed size (up to 32 MB) and serve them from the
      * heap. Affects only where large blocks of this process come from. */
-    mallopt(M_MMAP_THRESHOLD, (int)SHADOW_MIN_BYTES);
+    if (mq_guard_enabled()) mallopt(M_MMAP_THRESHOLD, (int)SHADOW_MIN_BYTES); /* not needed unguarded */
     g_stream = mq_default_stream();
     if (!g_stream) {
         g_ready = -1;

@@ -185,3 +185,53 @@ print(lib.mq_guard_arm(a.ctypes.data, a.nbytes, 0))
     cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
                         env=env)
     assert cp.stdout.strip() == "0", cp.stderr[-2000:]
+
+
+def test_chunk_check_needs_glibc_mmapped_header(lib):
+    """a CHUNK guard is armed only on what looks exactly like glibc's
+    mmapped chunk (header at a page start, IS_MMAPPED set, whole pages), so a block
+    from another allocator whose size word merely has bit 1 set is refused."""
+    base = libc.mmap(None, 4 * PAGE, mmap.PROT_READ | mmap.PROT_WRITE,
+                     mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS, -1, 0)
+    try:
+        words = (C.c_size_t * (PAGE // 8)).from_address(base)
+        words[7] = (3 * PAGE) | 2   # size word of a fake chunk at base + 48: not page-aligned
+        assert lib.mq_guard_arm(base + 64, 2 * PAGE, mq.MQ_GUARD_CHUNK) == 0
+        words[1] = 1000 | 2         # at the page start, but not a whole number of pages
+        assert lib.mq_guard_arm(base + 16, 2 * PAGE, mq.MQ_GUARD_CHUNK) == 0
+    finally:
+        libc.munmap(base, 4 * PAGE)
+
+
+def test_concurrent_first_writes_into_one_guard():
+    """several threads store into the same guarded pages at once; every
+    fault after the first finds the guard no longer armed and must re-execute its
+    store instead of handing the signal on (which would kill the process)."""
+    code = f"""
+import ctypes as C, mmap, os, sys, threading
+sys.path.insert(0, {os.path.join(os.path.dirname(__file__))!r})
+from refapi import mq
+import numpy as np
+lib = mq.load()
+libc = C.CDLL(None)
+libc.memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+for rep in range(200):
+    fd = os.memfd_create("x"); os.ftruncate(fd, 1 << 20)
+    m = mmap.mmap(fd, 1 << 20); os.close(fd)
+    a = np.frombuffer(m, dtype=np.uint8)
+    h = lib.mq_guard_arm(a.ctypes.data, a.nbytes, 0)
+    assert h
+    go = threading.Barrier(8)
+    def w(i):
+        go.wait()
+        libc.memset(a.ctypes.data + i * 4096, i + 1, 64)
+    ts = [threading.Thread(target=w, args=(i,)) for i in range(8)]
+    [t.start() for t in ts]; [t.join() for t in ts]
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 0
+    assert all(a[i * 4096] == i + 1 for i in range(8))
+    lib.mq_guard_release(h)
+    del a; m.close()
+print("ok", flush=True)
+"""
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert cp.returncode == 0 and "ok" in cp.stdout, (cp.returncode, cp.stderr[-2000:])
