@@ -38,6 +38,13 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <cerrno>
+#include <sys/mman.h>
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
 #include "mq_common.h"
 #include "mq_device.h"
 #include "mq_scan_common.h"
@@ -1954,7 +1961,112 @@ struct CopyPool {
     }
 };
 thread_local CopyPool g_copy;
+
+// Background population of a fresh host destination (a Result payload the caller
+// will free()): first touch of fresh pages costs more than the DMA that fills them
+// (tools/pcie_probe, payload_probe: 40 MB take 0.9 ms to fault in with 4 threads and
+// huge pages, 0.71 ms to cross the link). F threads populate it ahead of the staged
+// copy with MADV_POPULATE_WRITE (content unchanged; a range that is no longer mapped
+// just fails), in 8 MB chunks split into F slices taken in chunk order, so the copy of
+// chunk c waits only until chunk c is in. One pool per calling thread, like CopyPool.
+struct FaultPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable go;
+    char* base = nullptr;
+    size_t bytes = 0, nchunks = 0;
+    std::vector<std::atomic<int>> done;  // finished slices per chunk
+    std::atomic<size_t> next{0};
+    std::atomic<int> busy{0};
+    unsigned long gen = 0;
+    int F = 0;
+    bool quit = false;
+    std::atomic<bool> usable{true};
+
+    void start() {
+        const char* e = getenv("MQ_FAULT_THREADS");
+        F = e ? atoi(e) : 8;
+        if (F < 0) F = 0;
+        if (F > 16) F = 16;
+        for (int i = 0; i < F; i++) th.emplace_back([this] { loop(); });
+    }
+    void work() {
+        const size_t pg = 4096;
+        for (;;) {
+            const size_t piece = next.fetch_add(1, std::memory_order_relaxed);
+            if (piece >= nchunks * (size_t)F) return;
+            const size_t c = piece / (size_t)F, sl = piece % (size_t)F;
+            const size_t c0 = c * kStageBytes, clen = bytes - c0 < kStageBytes ? bytes - c0 : kStageBytes;
+            const size_t a = c0 + clen * sl / (size_t)F, b = c0 + clen * (sl + 1) / (size_t)F;
+            const uintptr_t pa = ((uintptr_t)base + a + pg - 1) & ~(uintptr_t)(pg - 1);
+            const uintptr_t pb = ((uintptr_t)base + b) & ~(uintptr_t)(pg - 1);
+            if (pb > pa && madvise((void*)pa, pb - pa, MADV_POPULATE_WRITE) != 0 && errno == EINVAL)
+                usable.store(false, std::memory_order_relaxed);
+            done[c].fetch_add(1, std::memory_order_release);
+        }
+    }
+    void loop() {
+        unsigned long seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                go.wait(lk, [&] { return quit || gen != seen; });
+                if (quit) return;
+                seen = gen;
+            }
+            work();
+            busy.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    // wait for the job in flight, if any
+    void finish() {
+        while (busy.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+        base = nullptr;
+        bytes = nchunks = 0;
+    }
+    void begin(void* p, size_t n) {
+        if (th.empty() && F == 0 && gen == 0) start();
+        finish();
+        if (F == 0 || !usable.load(std::memory_order_relaxed) || n < ((size_t)4 << 20)) return;
+        base = static_cast<char*>(p);
+        bytes = n;
+        nchunks = (n + kStageBytes - 1) / kStageBytes;
+        if (done.size() < nchunks) done = std::vector<std::atomic<int>>(nchunks);
+        for (size_t c = 0; c < nchunks; c++) done[c].store(0, std::memory_order_relaxed);
+        next.store(0, std::memory_order_relaxed);
+        busy.store(F, std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            gen++;
+        }
+        go.notify_all();
+    }
+    // chunk c of [dst, dst + n) is populated (or no job covers it)
+    void wait_chunk(const void* dst, size_t n, size_t c) {
+        if (!base || dst != base || n != bytes || c >= nchunks) return;
+        while (done[c].load(std::memory_order_acquire) < F) std::this_thread::yield();
+    }
+    bool covers(const void* dst, size_t n) const { return base && dst == base && n == bytes; }
+    ~FaultPool() {
+        finish();
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        go.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+thread_local FaultPool g_fault;
 }  // namespace
+
+// mq_host_prefault (mq_device.h): start populating [p, p + bytes) on the calling
+// thread's fault pool; the next mq_memcpy_d2h_staged into exactly that range waits for
+// each chunk's population before copying into it.
+void mq_host_prefault(void* p, size_t bytes) {
+    static const bool on = !(getenv("MQ_PREFAULT") && getenv("MQ_PREFAULT")[0] == '0');
+    if (on && p && bytes) g_fault.begin(p, bytes);
+}
 
 int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream) {
     if (bytes == 0) return MQ_OK;
@@ -1980,13 +2092,16 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
     };
     for (size_t c = 0; c < nchunks && c < (size_t)kStageBufs; c++)
         if ((rc = issue(c))) return rc;
+    if (!g_fault.covers(dst, bytes)) mq_host_prefault(dst, bytes);
     for (size_t c = 0; c < nchunks; c++) {
         const int b = (int)(c % kStageBufs);
         HIPCHK(hipEventSynchronize(S.ev[b]));
         const size_t off = c * kStageBytes, len = bytes - off < kStageBytes ? bytes - off : kStageBytes;
+        g_fault.wait_chunk(dst, bytes, c);
         g_copy.copy(static_cast<char*>(dst) + off, S.buf[b], len);
         if (c + kStageBufs < nchunks && (rc = issue(c + kStageBufs))) return rc;
     }
+    g_fault.finish();
     return MQ_OK;
 }
 

@@ -26,6 +26,7 @@
 #include <fcntl.h>
 #include <limits.h>
 #include <malloc.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -348,8 +349,8 @@ static int grow(void** buf, size_t* have, size_t need) {
 }
 
 /* Register a device copy of a column's rows (made here: owned) and guard the host
- * rows it mirrors. */
-static ColEntry* col_put(Column* c, void* dev) {
+ * rows it mirrors (armed here unless the caller armed it already: guard != ~0). */
+static ColEntry* col_put_armed(Column* c, void* dev, uint64_t guard) {
     ColEntry* e = col_find(c);
     if (e) col_drop(e);
     if (g_ncols == MAX_COLS) {
@@ -359,9 +360,36 @@ static ColEntry* col_put(Column* c, void* dev) {
         col_drop(&g_cols[victim]);
     }
     const size_t bytes = c->row_count * sizeof(int32_t);
-    const uint64_t guard = bytes ? mq_guard_arm(c->data, bytes, MQ_GUARD_FILE) : 0;
+    if (guard == ~(uint64_t)0) guard = bytes ? mq_guard_arm(c->data, bytes, MQ_GUARD_FILE) : 0;
     g_cols[g_ncols++] = (ColEntry){c, c->data, c->row_count, dev, 1, guard, g_op};
     return &g_cols[g_ncols - 1];
+}
+
+static ColEntry* col_put(Column* c, void* dev) { return col_put_armed(c, dev, ~(uint64_t)0); }
+
+/* Arming a guard is one mprotect over the whole column, 11-22 ms per GB of a file
+ * mapping (tools/payload_probe); it runs on a thread of its own while the upload
+ * copies. The staged upload only reads the rows, so read-only pages do not disturb it,
+ * and no store can reach them meanwhile: the caller is inside this operator. */
+typedef struct {
+    const void* p;
+    size_t bytes;
+    uint64_t guard;
+} ArmArg;
+
+static void* arm_thread(void* a) {
+    ArmArg* x = (ArmArg*)a;
+    x->guard = mq_guard_arm(x->p, x->bytes, MQ_GUARD_FILE);
+    return NULL;
+}
+
+static int arm_async_on(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MQ_GUARD_ASYNC");
+        v = !(e && e[0] == '0');
+    }
+    return v;
 }
 
 static int column_device(Column* c, const int32_t** d, Status* st) {
@@ -378,13 +406,24 @@ static int column_device(Column* c, const int32_t** d, Status* st) {
     void* dev = NULL;
     int rc = dev_alloc(&dev, bytes);
     if (rc) return fail(st, "column allocation", rc);
+    ArmArg arm = {c->data, bytes, ~(uint64_t)0};
+    pthread_t th;
+    const int async = bytes >= ((size_t)64 << 20) && mq_guard_enabled() && arm_async_on() &&
+                      pthread_create(&th, NULL, arm_thread, &arm) == 0;
     if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
+        if (async) {
+            pthread_join(th, NULL);
+            mq_guard_release(arm.guard);
+        }
         mq_pool_free(dev);
         return fail(st, "column upload", rc);
     }
+    TRACE("column h2d", t0);
+    if (async) pthread_join(th, NULL);
+    TRACE("column h2d + guard", t0);
     g_res.column_uploads++;
     g_res.column_bytes += bytes;
-    *d = (const int32_t*)col_put(c, dev)->dev;
+    *d = (const int32_t*)col_put_armed(c, dev, async ? arm.guard : ~(uint64_t)0)->dev;
     TRACE("column_device(upload)", t0);
     return 0;
 }
@@ -472,11 +511,9 @@ static Result* new_result(DataType t, size_t n, void* payload) {
  * malloc'd payload. When the payload can be guarded (glibc served it with mmap, so
  * free() unmaps it) an HBM shadow of it is kept for the operators that follow;
  * otherwise they upload it again. */
-static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
-    double t0 = now_s();
+static Result* int_result_into(int32_t* host, const void* d_src, size_t n, Status* st) {
+    double t0;
     const size_t bytes = n * sizeof(int32_t);
-    int32_t* host = (int32_t*)payload_alloc(bytes);
-    TRACE("payload_alloc", t0);
     /* small payloads are cheaper to upload again than to guard */
     const int keep = bytes >= SHADOW_MIN_BYTES && mq_guard_enabled() && mq_guard_chunk_ok(host);
     int rc;
@@ -511,6 +548,13 @@ static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
     TRACE("shadow put", t0);
     st->code = OK;
     return new_result(INT, n, host);
+}
+
+static Result* int_result_from_device(const void* d_src, size_t n, Status* st) {
+    double t0 = now_s();
+    int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
+    TRACE("payload_alloc", t0);
+    return int_result_into(host, d_src, n, st);
 }
 
 static int read_count(uint64_t* k, Status* st) {
@@ -690,12 +734,16 @@ Result* fetch_column(Column* column, Result* position_result, Status* ret_status
     if (column_device(column, &dcol, ret_status) || result_device(position_result, &dpos, ret_status) ||
         ensure_ws(k, ret_status))
         return NULL;
+    /* K is known before the gather runs: the payload's pages fault in while it does */
+    int32_t* host = (int32_t*)payload_alloc(k * sizeof(int32_t));
+    mq_host_prefault(host, k * sizeof(int32_t));
     int rc = mq_fetch(dcol, dpos, k, (int32_t*)g_scratch, g_stream);
     if (rc) {
         fail(ret_status, "fetch_column", rc);
+        free(host);
         return NULL;
     }
-    return int_result_from_device(g_scratch, k, ret_status);
+    return int_result_into(host, g_scratch, k, ret_status);
 }
 
 static int reduce_result(Result* r, mq_agg* a, Status* st) {

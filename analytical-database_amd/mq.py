@@ -107,6 +107,7 @@ _SIGS = {
     "mq_memcpy_d2h": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2d": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2h_staged": (_int, [_vp, _vp, _sz, _vp]),
+    "mq_host_prefault": (None, [_vp, _sz]),
     "mq_stream_create": (_int, [C.POINTER(_vp)]),
     "mq_stream_destroy": (_int, [_vp]),
     "mq_thread_release": (None, []),

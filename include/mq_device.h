@@ -55,6 +55,13 @@ int mq_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
  * registered with the driver, so it can be write-protected afterwards without
  * stalling later GPU work (a direct pageable D2H followed by mprotect does). */
 int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream);
+/* Start populating the fresh host pages of [p, p + bytes) in the background (helper
+ * threads of the calling thread, MADV_POPULATE_WRITE: content unchanged). The next
+ * mq_memcpy_d2h_staged into exactly that range copies each chunk as soon as its pages
+ * are in; it also starts this itself when nothing covers its range. Callers that know
+ * a result's size before its kernel runs start it first, so the page faults overlap
+ * the kernel. MQ_PREFAULT=0 disables it, MQ_FAULT_THREADS (default 8) sizes it. */
+void mq_host_prefault(void* p, size_t bytes);
 int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memset(void* dptr, int value, size_t bytes, void* stream);
 int mq_stream_sync(void* stream);
