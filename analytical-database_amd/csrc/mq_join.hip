@@ -865,6 +865,10 @@ __device__ __forceinline__ void probe_emit(uint64_t j, bool hit, uint32_t payloa
                                            const uint32_t* __restrict__ rs, uint32_t* __restrict__ cnt,
                                            bool packed) {
     if constexpr (RUNS) {
+        if (!cnt) {  // packed runs: the payload itself (0 = miss), decoded by the write
+            pstart[j] = hit ? payload : 0u;
+            return;
+        }
         uint32_t a = 0, L = 0;
         if (hit) {
             L = packed ? payload & 15u : 15u;
@@ -1152,6 +1156,67 @@ __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict_
         const int pp = p2[j];
         for (uint32_t t = 0; t < L; t++) {
             out1[o + t] = bpos[s + t];
+            out2[o + t] = pp;
+        }
+    }
+}
+
+// Packed runs (n1 <= 2^28): the probe stores each row's table payload as it is (0 for
+// a miss; a hit's payload is never 0: start << 4 | length with length >= 1, or
+// r << 4 | 15 for a long run, whose bounds are rs[r], rs[r + 1]). Then per 64-row word
+// the sum of the rows' run lengths, a scan over those n2/64 sums, and the write: each
+// wave takes one word, its lanes the word's 64 consecutive rows, and a row's output
+// offset is the word's offset plus the lengths of the rows below it (a wave prefix).
+// (Was: per row a start and a length from the probe and a scan of n2 lengths into
+// 8-byte offsets, 16 B more per probe row written and read again, plus the n2 scan.)
+__device__ __forceinline__ void run_decode(uint32_t pk, const uint32_t* __restrict__ rs, uint32_t* a, uint32_t* L) {
+    uint32_t l = pk & 15u, s = pk >> 4;
+    if (l == 15u) {
+        l = rs[s + 1] - rs[s];
+        s = rs[s];
+    }
+    *a = pk ? s : 0u;
+    *L = pk ? l : 0u;
+}
+
+__global__ __launch_bounds__(kTPB) void k_runs_count(const uint32_t* __restrict__ pk, uint64_t n2,
+                                                     const uint32_t* __restrict__ rs, uint32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (n2 + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6); w < nw; w += wstride) {
+        const uint64_t j = w * 64 + (uint64_t)lane;
+        uint32_t a, L;
+        run_decode(j < n2 ? pk[j] : 0u, rs, &a, &L);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+        if (lane == 0) cnt[w] = L;
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __restrict__ pk, uint64_t n2,
+                                                          const uint32_t* __restrict__ rs,
+                                                          const u64* __restrict__ woffs, const int* __restrict__ p2,
+                                                          const int* __restrict__ bpos, int* __restrict__ out1,
+                                                          int* __restrict__ out2) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (n2 + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64);
+    for (uint64_t w = (uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6); w < nw; w += wstride) {
+        const uint64_t j = w * 64 + (uint64_t)lane;
+        uint32_t a, L;
+        run_decode(j < n2 ? pk[j] : 0u, rs, &a, &L);
+        uint32_t incl = L;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (!L) continue;
+        const u64 o = woffs[w] + (u64)(incl - L);
+        const int pp = p2[j];
+        for (uint32_t t = 0; t < L; t++) {
+            out1[o + t] = bpos[a + t];
             out2[o + t] = pp;
         }
     }
@@ -1775,9 +1840,10 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     *h_m = 0;
     if (n2 == 0 || j->n1 == 0) return MQ_OK;
     const uint64_t nwords = (n2 + 63) / 64;
-    const bool words_scan = j->unique == 1;  // per 64-row hit word; else per row
+    const bool pruns = j->unique == 2 && j->packed;  // packed runs: per-word lengths
+    const bool words_scan = j->unique == 1 || pruns;  // per 64-row word; else per row
     j->pstart = (uint32_t*)pool_alloc(n2 * 4);
-    j->plen = (uint32_t*)pool_alloc(j->unique == 1 ? nwords * 12 : n2 * 4);
+    j->plen = (uint32_t*)pool_alloc(j->unique == 1 ? nwords * 12 : pruns ? nwords * 4 : n2 * 4);
     j->offs = (u64*)pool_alloc((words_scan ? nwords : n2) * 8);
     j->scan_scratch = (u64*)pool_alloc(scan_scratch_elems(words_scan ? nwords : n2) * 8);
     if (!j->pstart || !j->plen || !j->offs || !j->scan_scratch)
@@ -1787,7 +1853,14 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     const uint64_t nw = (n2 + 63) / 64;
     const uint64_t nscan = words_scan ? nw : n2;
     uint32_t* const cnt = j->unique == 1 ? j->plen + 2 * nw : j->plen;
-    if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
+    if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
+        auto kern = k_ht_probe_unique<true>;
+        hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks);
+        LAUNCHCHK("k_ht_probe_unique");
+        hipLaunchKernelGGL(k_runs_count, dim3(stream_grid(s, nw * 64)), dim3(kTPB), 0, st, j->pstart, n2, j->rs, cnt);
+        LAUNCHCHK("k_runs_count");
+    } else if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks);
@@ -1827,6 +1900,12 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                            reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
         LAUNCHCHK("k_join_write_hits");
+        return MQ_OK;
+    }
+    if (j->unique == 2 && j->packed) {
+        hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
+                           (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
+        LAUNCHCHK("k_join_write_runs");
         return MQ_OK;
     }
     hipLaunchKernelGGL(k_join_write, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
