@@ -254,6 +254,8 @@ constexpr int kPairCap = 512;
 constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
 constexpr int kBucketsP = kBuckets / 2;  // k_ssp_count's bucket table (LDS)
 constexpr int kCoarse = 16384;           // k_ssp_count's coverage bitmap cells
+constexpr int kCells = 4096;             // k_ssk_count's cell table (u16 per cell, 8 KB of LDS)
+constexpr uint32_t kRingK = 320;         // k_ssk_count's queued rows per wave (< 64 + a 256-row tile)
 constexpr uint32_t kRing = 320;          // k_ssp_count's queued rows per wave (< 64 + a 256-row tile)
 // Pairs of one 1024-row wave-group held in LDS until the next group's loads are
 // issued, then written with at most 4 straight-line coalesced stores: vmcnt retires
@@ -268,6 +270,7 @@ struct EiMeta {
     int shift;      // bucket width 2^shift
     int bmin, bmax; // first / last bound
     int cshift;     // coverage cell width 2^cshift
+    int xshift;     // k_ssk_count's cell width 2^xshift
 };
 
 struct EiTables {  // device copies, filled by the host (ss_count)
@@ -277,6 +280,9 @@ struct EiTables {  // device copies, filled by the host (ss_count)
     const uint16_t* qlist;      // queries covering each EI, ascending
     const uint32_t* qab;        // per query: ea (low 16) | eb (high 16)
     const uint32_t* cov;        // kCoarse bits over [bmin, bmax]: a covered EI meets the cell
+    const uint16_t* cell;       // kCells entries over [bmin, bmax] (k_ssk_count): 0 = no covered
+                                // EI meets the cell; e + 1 (< 0x8000) = the cell lies in covered
+                                // EI e; 0x8000 | e0 = bounds inside, e(v) >= e0: search
 };
 
 __device__ __forceinline__ int ei_of(int32_t v, const EiMeta& M, const uint32_t* s_bkt,
@@ -732,6 +738,255 @@ __global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col,
     }
 }
 
+// The same single pass, k-major (round 3): lane l of a wave-tile holds rows l, l + 64,
+// l + 128, l + 192 (four coalesced dword loads instead of one dwordx4), so the rows of
+// one load are 64 consecutive rows and a row's place in the wave's queue is one
+// mbcnt of the ballot of "covered" (rows in row order, no per-lane prefix over four
+// rows). A covered row is found with one LDS read of the cell table (kCells u16 over
+// [bmin, bmax], ei_build), which also gives its EI unless a bound lies inside the
+// cell; such rows are queued with a flag and their EI found from the cell's first EI
+// by a short search. k_ssp_count spent 670 M VALU per pass at Q = 150 on its
+// per-row coverage test, per-lane prefix and queue writes (PMC); this pass does the
+// per-row work in fewer instructions (625 vs 720 M VALU before the cell table shrank
+// to 4096 cells, which let 4 blocks share a CU). Outputs identical.
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
+                                                    EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
+                                                    uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
+                                                    uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
+    __shared__ uint16_t s_cell[kCells];
+    __shared__ int32_t s_b[kEiMax];
+    __shared__ uint32_t s_qoff[kEiMax];
+    __shared__ uint32_t hist[kWaves][kEiMax];
+    __shared__ uint16_t s_ql[kQlCap];
+    __shared__ uint32_t s_pb[kWaves][kPb];
+    __shared__ int32_t s_qv[kWaves][kRingK];
+    __shared__ uint16_t s_qe[kWaves][kRingK];
+    __shared__ uint32_t s_qr[kWaves][kRingK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    {  // the cell table: 16 u16 per thread, loaded as two 16-byte words before any store
+        const uint4* g = reinterpret_cast<const uint4*>(T.cell);
+        uint4* d = reinterpret_cast<uint4*>(s_cell);
+        constexpr int kPer = kCells * 2 / 16 / kTPB;
+        uint4 u[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) u[k] = g[tid + k * kTPB];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) d[tid + k * kTPB] = u[k];
+    }
+    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
+    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
+    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t nql = s_qoff[M.m + 1];
+    const bool ql_lds = nql <= (uint32_t)kQlCap;
+    if (ql_lds)
+        for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
+    __syncthreads();
+    const uint32_t bmin = (uint32_t)M.bmin, xsh = (uint32_t)M.xshift, m = (uint32_t)M.m;
+    uint64_t s, e;
+    wave_chunk(n, rpb, wave, &s, &e);
+    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    uint32_t* list = pairs + wc * cap;
+    uint32_t* pb = s_pb[wave];
+    int32_t* qv = s_qv[wave];
+    uint16_t* qe = s_qe[wave];
+    uint32_t* qr = s_qr[wave];
+    uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0;
+    bool direct = false;
+    auto round = [&](uint32_t nr) {
+        const bool has = (uint32_t)lane < nr;
+        uint32_t qa = 0, qn = 0, r = 0;
+        if (has) {
+            const uint32_t slot = head + (uint32_t)lane;
+            const int32_t x = qv[slot];
+            const uint32_t ent = qe[slot];
+            r = qr[slot];
+            uint32_t ei = ent - 1u;
+            if (ent & 0x8000u) {  // bounds inside the cell: from its first EI on
+                ei = ent & 0x7FFFu;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (ei < m && s_b[ei] <= x) ei++;
+                if (ei < m && s_b[ei] <= x) {
+                    uint32_t lo = ei + 1, hi = m;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_b[mid] <= x) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    ei = lo;
+                }
+            }
+            qa = s_qoff[ei];
+            qn = s_qoff[ei + 1] - qa;
+            if (qn) atomicAdd(&hist[wave][ei], 1u);
+        }
+        head += nr;
+        uint32_t pre = 0, tot = 0;
+        if (!__ballot(qn > 1u)) {  // the usual case: at most one query per row
+            const unsigned long long bm = __ballot(qn != 0u);
+            pre = mbcnt64(bm);
+            tot = (uint32_t)__popcll(bm);
+        } else if (!__ballot(qn >= 8u)) {
+#pragma unroll
+            for (int bit = 0; bit < 3; bit++) {
+                const unsigned long long bm = __ballot((qn >> bit) & 1u);
+                pre += mbcnt64(bm) << bit;
+                tot += (uint32_t)__popcll(bm) << bit;
+            }
+        } else {
+            for (uint32_t t = 1;; t++) {
+                const unsigned long long bm = __ballot(qn >= t);
+                if (!bm) break;
+                pre += mbcnt64(bm);
+                tot += (uint32_t)__popcll(bm);
+            }
+        }
+        if (tot == 0) return;
+        if ((uint64_t)run + tot <= cap) {
+            direct = direct || fill + tot > kPb;
+            if (!direct) {
+                uint32_t at = fill + pre;
+                for (uint32_t i = 0; i < qn; i++)
+                    pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
+                fill += tot;
+            } else {
+                uint32_t at = run + pre;
+                for (uint32_t i = 0; i < qn; i++)
+                    list[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
+            }
+        }
+        run += tot;
+    };
+    auto drain = [&]() {  // full rounds while 64 rows are queued, the rest to the front
+        if (tail < 64u) return;
+        do {
+            round(64u);
+            __builtin_amdgcn_wave_barrier();
+        } while (tail - head >= 64u);
+        const uint32_t rest = tail - head;
+        int32_t mv = 0;
+        uint32_t mr = 0, me = 0;
+        if ((uint32_t)lane < rest) mv = qv[head + lane], me = qe[head + lane], mr = qr[head + lane];
+        __builtin_amdgcn_wave_barrier();
+        if ((uint32_t)lane < rest) qv[lane] = mv, qe[lane] = (uint16_t)me, qr[lane] = mr;
+        __builtin_amdgcn_wave_barrier();
+        head = 0;
+        tail = rest;
+    };
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
+    constexpr int kV = kSsUnroll * 4;
+    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
+        int v[kV];
+        const bool whole = t + kWaveTile * kSsUnroll <= e;
+        if (whole) {
+#pragma unroll
+            for (int i = 0; i < kV; i++) v[i] = __builtin_nontemporal_load(col + t + (uint64_t)i * 64 + lane);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kV; i++) {
+                const uint64_t row = t + (uint64_t)i * 64 + lane;
+                v[i] = row < e ? col[row] : 0;
+            }
+        }
+        {  // the previous group's pairs, behind this group's loads
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < (int)(kPb / 64); k++) {
+                const uint32_t i = (uint32_t)(k * 64 + lane);
+                __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, i < pend ? (int)((pend_at + i) * 4u) : (int)0x80000000u,
+                                                      0, 0);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint32_t grp_at = run;
+        fill = 0;
+        direct = false;
+        const uint32_t r0 = (uint32_t)(t - s) + (uint32_t)lane;
+        // per 256-row tile: its 4 row slots queued, then one drain (a drain per row slot
+        // inlined 16 copies of the round and overflowed the instruction cache)
+#pragma unroll
+        for (int u = 0; u < kSsUnroll; u++) {
+            uint32_t ent[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = u * 4 + k;
+                ent[k] = s_cell[min(((uint32_t)v[i] - bmin) >> xsh, (uint32_t)kCells - 1u)];
+            }
+            if (!whole) {  // (wave-uniform) rows past the chunk's end are not covered
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (r0 + (uint32_t)(u * 4 + k) * 64u >= (uint32_t)(e - s)) ent[k] = 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = u * 4 + k;
+                const bool cov = ent[k] != 0u;
+                const unsigned long long bm = __ballot(cov);
+                if (cov) {
+                    const uint32_t at = tail + mbcnt64(bm);
+                    qv[at] = v[i];
+                    qe[at] = (uint16_t)ent[k];
+                    qr[at] = r0 + (uint32_t)i * 64u;
+                }
+                tail += (uint32_t)__popcll(bm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            drain();
+        }
+        pend = fill;
+        pend_at = grp_at;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
+    __builtin_amdgcn_wave_barrier();
+    fill = 0;
+    direct = true;
+    while (tail != head) {
+        round(tail - head < 64u ? tail - head : 64u);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        npairs[wc] = run;
+        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* h = hist[wave];
+    const int ne = M.m + 2;
+    const int per = (ne + 63) / 64;
+    uint32_t loc = 0;
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) loc += h[j];
+    }
+    uint32_t incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    uint32_t acc = incl - loc;
+    __builtin_amdgcn_wave_barrier();
+    for (int i = 0; i < per; i++) {
+        const int j = lane * per + i;
+        if (j < ne) {
+            const uint32_t c = h[j];
+            h[j] = acc;
+            acc += c;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < q; i += 64) {
+        const uint32_t ab = T.qab[i];
+        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
+    }
+}
+
 constexpr int kSpChunk = 4096;                  // pairs sorted in LDS at a time
 constexpr int kSpPerWave = kSpChunk / kWaves;   // 1024: 16 rounds of 64
 constexpr int kSpRounds = kSpPerWave / 64;
@@ -864,8 +1119,9 @@ struct SsLayout {
 // EI tables in the workspace: bounds, bucket table, qoff, qab, then qlist
 constexpr size_t kEiBoundsB = (size_t)kEiMax * 4, kEiBucketB = (size_t)kBuckets * 4,
                  kEiQoffB = (size_t)kEiMax * 4, kEiQabB = (size_t)kMaxQ * 4,
-                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2, kEiCovB = (size_t)kCoarse / 8;
-constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB + kEiQlistB;
+                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2, kEiCovB = (size_t)kCoarse / 8,
+                 kEiCellB = (size_t)kCells * 2;
+constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB + kEiCellB + kEiQlistB;
 
 SsLayout ss_layout(uint64_t nwc, int q) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1053,7 +1309,29 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
             if (acc > 0 || (c > cmax && tail)) hcov[c >> 5] |= 1u << (c & 31);
         }
     }
-    *meta = EiMeta{m, shift, (int)bmin, (int)bmax, cshift};
+    // k_ssk_count's cell table: one u16 per cell of 2^xshift values from bmin (the last
+    // cell also takes every value below bmin and past the table, by the clamp)
+    int xshift = 0;
+    while (((bmax - bmin) >> xshift) >= kCells - 1) xshift++;
+    {
+        static thread_local uint16_t hcell[kCells];
+        static thread_local int cp[kEiMax + 1];  // covered EIs below e
+        cp[0] = 0;
+        for (int e = 0; e <= m; e++) cp[e + 1] = cp[e] + (hqoff[e + 1] > hqoff[e] ? 1 : 0);
+        int pl = 0, ph = 0;  // e(cell start), e(cell end): monotone over the cells
+        for (int c = 0; c < kCells - 1; c++) {
+            const long long cs = bmin + ((long long)c << xshift), ce = cs + (1ll << xshift) - 1;
+            while (pl < m && b[pl] <= cs) pl++;
+            if (ph < pl) ph = pl;
+            while (ph < m && b[ph] <= ce) ph++;
+            const bool any = cp[ph + 1] - cp[pl] > 0;  // a covered EI among [pl, ph]
+            hcell[c] = !any ? (uint16_t)0 : pl == ph ? (uint16_t)(pl + 1) : (uint16_t)(0x8000 | pl);
+        }
+        // past bmax's cell every value is in EI m; below bmin (wrapped) in EI 0
+        hcell[kCells - 1] = hqoff[m + 1] > hqoff[m] ? (uint16_t)0x8000 : (uint16_t)0;
+        std::memcpy(region + kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB, hcell, kEiCellB);
+    }
+    *meta = EiMeta{m, shift, (int)bmin, (int)bmax, cshift, xshift};
     size_t o = 0;
     std::memcpy(region + o, hb, (size_t)m * 4);
     o += kEiBoundsB;
@@ -1065,6 +1343,7 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
     o += kEiQabB;
     std::memcpy(region + o, hcov, kEiCovB);
     o += kEiCovB;
+    o += kEiCellB;  // the cell table, written above
     if (at) std::memcpy(region + o, hql, (size_t)at * 2);
     return MQ_OK;
 }
@@ -1082,6 +1361,8 @@ EiTables ei_tables(char* region) {
     o += kEiQabB;
     T.cov = reinterpret_cast<const uint32_t*>(region + o);
     o += kEiCovB;
+    T.cell = reinterpret_cast<const uint16_t*>(region + o);
+    o += kEiCellB;
     T.qlist = reinterpret_cast<const uint16_t*>(region + o);
     return T;
 }
@@ -1116,8 +1397,13 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     const bool vec = aligned16(d_col);
     const char* emin = getenv("MQ_SS_EI_MIN");  // A/B of the threshold
     const bool ei = qk >= (emin ? atoi(emin) : kEiMinQ) && getenv("MQ_SS_IMPL") == nullptr;  // MQ_SS_IMPL=ballot: A/B
-    const void* fn = ei ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
-                        : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
+    // the grid is sized for the kernel that reads the column: the k-major count pass of
+    // the single-pass EI path (its LDS allows 3 blocks a CU), else the write pass
+    static const bool filt = getenv("MQ_SS_COUNT") && strcmp(getenv("MQ_SS_COUNT"), "filter") == 0;
+    const bool kmajor = ei && !filt && getenv("MQ_SS_TWOPASS") == nullptr;
+    const void* fn = kmajor ? (vec ? (const void*)&k_ssk_count<true> : (const void*)&k_ssk_count<false>)
+                   : ei     ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
+                            : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
     uint32_t g = 1;
     uint64_t rpb = kGranule;
     if (n) geometry(s, n, fn, &g, &rpb, kGranule);
@@ -1132,7 +1418,7 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     std::memcpy(up + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1));
     std::memcpy(up + L.slot, hslot, sizeof(int) * q);
     std::memset(up + L.flag, 0, 4);
-    EiMeta meta{0, 0, 0, 0, 0};
+    EiMeta meta{0, 0, 0, 0, 0, 0};
     if (ei && (rc = ei_build(hp, qk, up + L.ei, &meta))) return rc;
     if ((rc = staging_put(0, w, L.outs, st))) return rc;
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
@@ -1144,13 +1430,24 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
             uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
             uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
             unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
-            if (vec)
-                hipLaunchKernelGGL(k_ssp_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                   nwc, pr, cap, npr, of);
-            else
-                hipLaunchKernelGGL(k_ssp_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                   nwc, pr, cap, npr, of);
-            LAUNCHCHK("k_ssp_count");
+            // MQ_SS_COUNT=filter keeps the coverage-bitmap pass (A/B)
+            if (filt) {
+                if (vec)
+                    hipLaunchKernelGGL(k_ssp_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                       nwc, pr, cap, npr, of);
+                else
+                    hipLaunchKernelGGL(k_ssp_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                       nwc, pr, cap, npr, of);
+                LAUNCHCHK("k_ssp_count");
+            } else {
+                if (vec)
+                    hipLaunchKernelGGL(k_ssk_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                       nwc, pr, cap, npr, of);
+                else
+                    hipLaunchKernelGGL(k_ssk_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
+                                       nwc, pr, cap, npr, of);
+                LAUNCHCHK("k_ssk_count");
+            }
         } else if (ei) {
             const EiTables T = ei_tables(w + L.ei);
             if (vec)
