@@ -22,6 +22,9 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "mq_common.h"
 #include "mq_device.h"
@@ -198,7 +201,8 @@ __global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V
                                                    const uint32_t* __restrict__ segc, const int32_t* __restrict__ lid,
                                                    const int32_t* __restrict__ rid, const uint32_t* __restrict__ J,
                                                    uint64_t n, int32_t* __restrict__ Vn, uint32_t* __restrict__ Pn,
-                                                   int32_t* __restrict__ SIDn, unsigned int* __restrict__ long_chain) {
+                                                   int32_t* __restrict__ SIDn, unsigned int* __restrict__ long_chain,
+                                                   uint8_t* __restrict__ segflag) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
         const int32_t sid = SID[i];
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V
                 }
                 if (!USE_F && q - g.lo < c) {  // long chain: doubling, then this kernel again
                     atomicOr(long_chain, 1u);
+                    segflag[sid] = 1;
                     continue;
                 }
                 if (q == g.lo + c) q = g.hi;        // the final swap with the pivot
@@ -309,7 +314,13 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
     int32_t* rid = b.get<int32_t>(smax);
     unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(n));
     unsigned long long* small = b.get<unsigned long long>(4);  // [S_next, long_chain | changed]
-    if (b.nb != 17) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
+    uint8_t* segflag = b.get<uint8_t>(smax);                    // ranges with a long chain
+    if (b.nb != 18) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
+    static const bool stats = getenv("MQ_LQ_STATS") != nullptr;  // per-level diagnostics (stderr)
+    std::vector<LSeg> hseg;
+    std::vector<uint32_t> hsegc;
+    std::vector<uint8_t> hflag;
+    int level = 0;
     unsigned int* flags = reinterpret_cast<unsigned int*>(small + 1);
     const uint32_t gn = stream_grid(s, n);
     hipLaunchKernelGGL(k_lq_init, dim3(gn), dim3(kTPB), 0, st, col, n, V[0], P[0], SID[0]);
@@ -333,14 +344,16 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
         hipLaunchKernelGGL(k_lq_less, dim3(gn), dim3(kTPB), 0, st, V[cur], SID[cur], seg[cur], EX, n, J);
         LAUNCHCHK("k_lq_less");
         HIPCHK(hipMemsetAsync(flags, 0, 8, st));
+        HIPCHK(hipMemsetAsync(segflag, 0, S, st));
         hipLaunchKernelGGL(k_lq_final<false>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
-                           segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags);
+                           segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags, segflag);
         LAUNCHCHK("k_lq_final");
         unsigned long long h[2];
         HIPCHK(hipMemcpyAsync(h, small, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        int jumps = 0;
         if ((uint32_t)h[1]) {  // a chain longer than kChainCap: double J, then place everyone again
-            for (int it = 0;; it++) {
+            for (int it = 0;; it++, jumps++) {
                 if (it > 40) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
                 HIPCHK(hipMemsetAsync(flags + 1, 0, 4, st));
                 hipLaunchKernelGGL(k_lq_jump, dim3(gn), dim3(kTPB), 0, st, SID[cur], seg[cur], segc, n, J, flags + 1);
@@ -351,9 +364,30 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
                 if (!ch) break;
             }
             hipLaunchKernelGGL(k_lq_final<true>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
-                               segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags);
+                               segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags, segflag);
             LAUNCHCHK("k_lq_final");
         }
+        if (stats) {
+            hseg.resize(S);
+            hsegc.resize(S);
+            hflag.resize(S);
+            HIPCHK(hipMemcpy(hseg.data(), seg[cur], S * sizeof(LSeg), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hsegc.data(), segc, S * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hflag.data(), segflag, S, hipMemcpyDeviceToHost));
+            uint64_t act = 0, big = 0, nbig = 0, nfl = 0, zfl = 0, efl = 0, maxm = 0;
+            for (uint64_t k = 0; k < S; k++) {
+                const uint64_t m = (uint64_t)hseg[k].hi - hseg[k].lo + 1;
+                act += m;
+                if (m > maxm) maxm = m;
+                if (m > 2048) big += m, nbig++;
+                if (hflag[k]) nfl++, efl += m, zfl += hsegc[k] == 0xFFFFFFFFu ? 0 : hsegc[k];
+            }
+            fprintf(stderr, "lq level %d: ranges %llu active %llu max %llu | >2048: %llu ranges %llu rows | long: %llu ranges, "
+                    "%llu rows, zones %llu, jumps %d\n", level, (unsigned long long)S, (unsigned long long)act,
+                    (unsigned long long)maxm, (unsigned long long)nbig, (unsigned long long)big, (unsigned long long)nfl,
+                    (unsigned long long)efl, (unsigned long long)zfl, jumps);
+        }
+        level++;
         S = h[0];
         cur ^= 1;
     }
