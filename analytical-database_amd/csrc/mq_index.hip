@@ -194,6 +194,47 @@ __global__ __launch_bounds__(kTPB) void k_lq_less(const int32_t* __restrict__ V,
 
 constexpr int kChainCap = 64;  // chain steps walked before pointer doubling takes over
 
+// One index of k_lq_final (below). Returns false when USE_F is false and the index
+// sits on a chain longer than kChainCap (it is placed later, after the doubling).
+template <bool USE_F>
+__device__ __forceinline__ bool lq_place(uint64_t i, const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
+                                         const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
+                                         const unsigned long long* __restrict__ EX, const uint32_t* __restrict__ segc,
+                                         const int32_t* __restrict__ lid, const int32_t* __restrict__ rid,
+                                         const uint32_t* __restrict__ J, int32_t* __restrict__ Vn,
+                                         uint32_t* __restrict__ Pn, int32_t* __restrict__ SIDn) {
+    const int32_t sid = SID[i];
+    const int32_t v = V[i];
+    const uint32_t row = P[i];
+    uint32_t q = (uint32_t)i;
+    int32_t ns = -1;
+    if (sid >= 0) {
+        const LSeg g = seg[sid];
+        const uint32_t c = segc[sid];
+        if (c == 0xFFFFFFFFu) {                 // all equal: last first, then in order
+            q = (uint32_t)i == g.hi ? g.lo : (uint32_t)i + 1;
+        } else if ((uint32_t)i == g.hi) {       // the pivot
+            q = g.lo + c;
+        } else if (v < V[g.hi]) {              // stable compaction of the "<" side
+            q = g.lo + ((uint32_t)EX[i] - (uint32_t)EX[g.lo]);
+            ns = lid[sid];
+        } else {                                // the >= side: follow the swaps
+            int steps = 0;
+            while (q - g.lo < c) {
+                q = J[q];
+                if (!USE_F && ++steps > kChainCap) break;
+            }
+            if (!USE_F && q - g.lo < c) return false;  // long chain: doubling, then placed again
+            if (q == g.lo + c) q = g.hi;        // the final swap with the pivot
+            ns = rid[sid];
+        }
+    }
+    Vn[q] = v;
+    Pn[q] = row;
+    SIDn[q] = ns;
+    return true;
+}
+
 template <bool USE_F>
 __global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
                                                    const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
@@ -205,64 +246,84 @@ __global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V
                                                    uint8_t* __restrict__ segflag) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        const int32_t sid = SID[i];
-        const int32_t v = V[i];
-        const uint32_t row = P[i];
-        uint32_t q = (uint32_t)i;
-        int32_t ns = -1;
-        if (sid >= 0) {
-            const LSeg g = seg[sid];
-            const uint32_t c = segc[sid];
-            if (c == 0xFFFFFFFFu) {                 // all equal: last first, then in order
-                q = (uint32_t)i == g.hi ? g.lo : (uint32_t)i + 1;
-            } else if ((uint32_t)i == g.hi) {       // the pivot
-                q = g.lo + c;
-            } else if (v < V[g.hi]) {              // stable compaction of the "<" side
-                q = g.lo + ((uint32_t)EX[i] - (uint32_t)EX[g.lo]);
-                ns = lid[sid];
-            } else {                                // the >= side: follow the swaps
-                int steps = 0;
-                while (q - g.lo < c) {
-                    q = J[q];
-                    if (!USE_F && ++steps > kChainCap) break;
-                }
-                if (!USE_F && q - g.lo < c) {  // long chain: doubling, then this kernel again
-                    atomicOr(long_chain, 1u);
-                    segflag[sid] = 1;
-                    continue;
-                }
-                if (q == g.lo + c) q = g.hi;        // the final swap with the pivot
-                ns = rid[sid];
-            }
+        if (!lq_place<USE_F>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn)) {
+            atomicOr(long_chain, 1u);
+            segflag[SID[i]] = 1;
         }
-        Vn[q] = v;
-        Pn[q] = row;
-        SIDn[q] = ns;
     }
 }
 
-// pointer doubling on J over each range's "<" zone [lo, lo + c): J[q] <- J[J[q]]
-// while J[q] is still inside the zone (in place: a concurrent update only moves a
-// pointer further along its own chain, never past the chain's end)
-__global__ __launch_bounds__(kTPB) void k_lq_jump(const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
-                                                  const uint32_t* __restrict__ segc, uint64_t n, uint32_t* J,
-                                                  unsigned int* __restrict__ changed) {
-    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+// Long chains are rare and sit in a few ranges (MQ_LQ_STATS at 2^27: their "<" zones
+// hold 20 % of the rows at the top levels and under 2 % below level 30), so the
+// doubling and the second placement run only over those ranges: per flagged range,
+// items of kZChunk indexes (of its zone for the doubling, of the whole range for the
+// placement), a block per item; a block finds its range by a binary search over the
+// items' prefix. (Was: both over all n rows, every doubling step and level: 0.42 ms
+// a pass, 44 % of the 2^27 build.)
+constexpr uint32_t kZChunk = 2048;
+
+__global__ __launch_bounds__(kTPB) void k_lq_items(const LSeg* __restrict__ seg, uint32_t S,
+                                                   const uint32_t* __restrict__ segc,
+                                                   const uint8_t* __restrict__ segflag, uint32_t* __restrict__ zi,
+                                                   uint32_t* __restrict__ fi) {
+    for (uint32_t s = blockIdx.x * kTPB + threadIdx.x; s < S; s += gridDim.x * kTPB) {
+        const bool f = segflag[s] != 0;
+        const uint32_t c = segc[s], m = seg[s].hi - seg[s].lo + 1;
+        zi[s] = f && c != 0xFFFFFFFFu ? (c + kZChunk - 1) / kZChunk : 0u;
+        fi[s] = f ? (m + kZChunk - 1) / kZChunk : 0u;
+    }
+}
+
+// the range of item b: the last s with off[s] <= b (off: exclusive prefix of items, S entries)
+__device__ __forceinline__ uint32_t lq_item_range(const unsigned long long* __restrict__ off, uint32_t S, uint64_t b) {
+    uint32_t lo = 0, hi = S;  // off[lo] <= b < off[hi] (off[S] taken as infinity)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kTPB) void k_lq_jump_z(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
+                                                    const unsigned long long* __restrict__ zoff, uint32_t S,
+                                                    uint32_t* J, unsigned int* __restrict__ changed) {
+    __shared__ uint32_t s_r;
+    if (threadIdx.x == 0) s_r = lq_item_range(zoff, S, blockIdx.x);
+    __syncthreads();
+    const uint32_t r = s_r;
+    const uint32_t lo = seg[r].lo, c = segc[r];
+    const uint32_t k = blockIdx.x - (uint32_t)zoff[r];
+    const uint32_t b = lo + k * kZChunk, e = min(lo + c, b + kZChunk);
     unsigned int any = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        const int32_t sid = SID[i];
-        if (sid < 0) continue;
-        const uint32_t lo = seg[sid].lo, c = segc[sid];
-        if (c == 0xFFFFFFFFu || (uint32_t)i - lo >= c) continue;
+    for (uint32_t i = b + threadIdx.x; i < e; i += kTPB) {
         const uint32_t f = J[i];
-        // J[i] == i: the first i - lo + 1 values are all below the pivot; no chain of
-        // a >= value passes there, and it would never converge
-        if (f != (uint32_t)i && f - lo < c) {
+        if (f != i && f - lo < c) {
             J[i] = J[f];
             any = 1;
         }
     }
-    if (any) atomicOr(changed, 1u);
+    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(changed, 1u);
+}
+
+__global__ __launch_bounds__(kTPB) void k_lq_final_z(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
+                                                     const int32_t* __restrict__ SID, const LSeg* __restrict__ seg,
+                                                     const unsigned long long* __restrict__ EX,
+                                                     const uint32_t* __restrict__ segc, const int32_t* __restrict__ lid,
+                                                     const int32_t* __restrict__ rid, const uint32_t* __restrict__ J,
+                                                     const unsigned long long* __restrict__ foff, uint32_t S,
+                                                     int32_t* __restrict__ Vn, uint32_t* __restrict__ Pn,
+                                                     int32_t* __restrict__ SIDn) {
+    __shared__ uint32_t s_r;
+    if (threadIdx.x == 0) s_r = lq_item_range(foff, S, blockIdx.x);
+    __syncthreads();
+    const uint32_t r = s_r;
+    const uint32_t lo = seg[r].lo, hi = seg[r].hi;
+    const uint32_t k = blockIdx.x - (uint32_t)foff[r];
+    const uint32_t b = lo + k * kZChunk;
+    const uint32_t e = hi + 1 - b < kZChunk ? hi + 1 : b + kZChunk;
+    for (uint32_t i = b + threadIdx.x; i < e; i += kTPB)
+        (void)lq_place<true>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn);
 }
 
 __global__ __launch_bounds__(kTPB) void k_lq_emit(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
@@ -284,7 +345,7 @@ __global__ __launch_bounds__(kTPB) void k_has_ties(const int32_t* __restrict__ v
 }
 
 struct LqBufs {
-    void* blk[24];
+    void* blk[32];
     int nb;
     ~LqBufs() {
         for (int i = 0; i < nb; i++) pool_free(blk[i]);
@@ -315,7 +376,11 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
     unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(n));
     unsigned long long* small = b.get<unsigned long long>(4);  // [S_next, long_chain | changed]
     uint8_t* segflag = b.get<uint8_t>(smax);                    // ranges with a long chain
-    if (b.nb != 18) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
+    uint32_t* zi = b.get<uint32_t>(smax);                       // per range: doubling items
+    uint32_t* fi = b.get<uint32_t>(smax);                       // per range: placement items
+    unsigned long long* zoff = b.get<unsigned long long>(smax);
+    unsigned long long* foff = b.get<unsigned long long>(smax);
+    if (b.nb != 22) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
     static const bool stats = getenv("MQ_LQ_STATS") != nullptr;  // per-level diagnostics (stderr)
     std::vector<LSeg> hseg;
     std::vector<uint32_t> hsegc;
@@ -352,20 +417,37 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
         HIPCHK(hipMemcpyAsync(h, small, 16, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         int jumps = 0;
-        if ((uint32_t)h[1]) {  // a chain longer than kChainCap: double J, then place everyone again
-            for (int it = 0;; it++, jumps++) {
+        if ((uint32_t)h[1]) {  // chains longer than kChainCap: double J, then place again, flagged ranges only
+            const uint32_t gs2 = stream_grid(s, S);
+            hipLaunchKernelGGL(k_lq_items, dim3(gs2), dim3(kTPB), 0, st, seg[cur], (uint32_t)S, segc, segflag, zi, fi);
+            LAUNCHCHK("k_lq_items");
+            if ((rc = scan_u32_exclusive(zi, zoff, S, scratch, st))) return rc;
+            if ((rc = scan_u32_exclusive(fi, foff, S, scratch, st))) return rc;
+            unsigned long long t[2];
+            uint32_t l[2];
+            HIPCHK(hipMemcpyAsync(&t[0], zoff + (S - 1), 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&t[1], foff + (S - 1), 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&l[0], zi + (S - 1), 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&l[1], fi + (S - 1), 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            const uint64_t nz = t[0] + l[0], nf = t[1] + l[1];
+            for (int it = 0; nz; it++, jumps++) {
                 if (it > 40) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
                 HIPCHK(hipMemsetAsync(flags + 1, 0, 4, st));
-                hipLaunchKernelGGL(k_lq_jump, dim3(gn), dim3(kTPB), 0, st, SID[cur], seg[cur], segc, n, J, flags + 1);
-                LAUNCHCHK("k_lq_jump");
+                hipLaunchKernelGGL(k_lq_jump_z, dim3((uint32_t)nz), dim3(kTPB), 0, st, seg[cur], segc, zoff,
+                                   (uint32_t)S, J, flags + 1);
+                LAUNCHCHK("k_lq_jump_z");
                 unsigned int ch = 0;
                 HIPCHK(hipMemcpyAsync(&ch, flags + 1, 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 if (!ch) break;
             }
-            hipLaunchKernelGGL(k_lq_final<true>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
-                               segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags, segflag);
-            LAUNCHCHK("k_lq_final");
+            if (nf) {
+                hipLaunchKernelGGL(k_lq_final_z, dim3((uint32_t)nf), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur],
+                                   seg[cur], EX, segc, lid, rid, J, foff, (uint32_t)S, V[cur ^ 1], P[cur ^ 1],
+                                   SID[cur ^ 1]);
+                LAUNCHCHK("k_lq_final_z");
+            }
         }
         if (stats) {
             hseg.resize(S);
