@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kTPB) void k_lq_less(const int32_t* __restrict__ V,
     }
 }
 
-constexpr int kChainCap = 64;  // chain steps walked before pointer doubling takes over
+constexpr int kChainCap = 64;  // chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
 
 // One index of k_lq_final (below). Returns false when USE_F is false and the index
 // sits on a chain longer than kChainCap (it is placed later, after the doubling).
@@ -202,7 +202,7 @@ __device__ __forceinline__ bool lq_place(uint64_t i, const int32_t* __restrict__
                                          const unsigned long long* __restrict__ EX, const uint32_t* __restrict__ segc,
                                          const int32_t* __restrict__ lid, const int32_t* __restrict__ rid,
                                          const uint32_t* __restrict__ J, int32_t* __restrict__ Vn,
-                                         uint32_t* __restrict__ Pn, int32_t* __restrict__ SIDn) {
+                                         uint32_t* __restrict__ Pn, int32_t* __restrict__ SIDn, int cap) {
     const int32_t sid = SID[i];
     const int32_t v = V[i];
     const uint32_t row = P[i];
@@ -222,7 +222,7 @@ __device__ __forceinline__ bool lq_place(uint64_t i, const int32_t* __restrict__
             int steps = 0;
             while (q - g.lo < c) {
                 q = J[q];
-                if (!USE_F && ++steps > kChainCap) break;
+                if (!USE_F && ++steps > cap) break;
             }
             if (!USE_F && q - g.lo < c) return false;  // long chain: doubling, then placed again
             if (q == g.lo + c) q = g.hi;        // the final swap with the pivot
@@ -243,10 +243,10 @@ __global__ __launch_bounds__(kTPB) void k_lq_final(const int32_t* __restrict__ V
                                                    const int32_t* __restrict__ rid, const uint32_t* __restrict__ J,
                                                    uint64_t n, int32_t* __restrict__ Vn, uint32_t* __restrict__ Pn,
                                                    int32_t* __restrict__ SIDn, unsigned int* __restrict__ long_chain,
-                                                   uint8_t* __restrict__ segflag) {
+                                                   uint8_t* __restrict__ segflag, int cap) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
-        if (!lq_place<USE_F>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn)) {
+        if (!lq_place<USE_F>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn, cap)) {
             atomicOr(long_chain, 1u);
             segflag[SID[i]] = 1;
         }
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kTPB) void k_lq_final_z(const int32_t* __restrict__
     const uint32_t b = lo + k * kZChunk;
     const uint32_t e = hi + 1 - b < kZChunk ? hi + 1 : b + kZChunk;
     for (uint32_t i = b + threadIdx.x; i < e; i += kTPB)
-        (void)lq_place<true>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn);
+        (void)lq_place<true>(i, V, P, SID, seg, EX, segc, lid, rid, J, Vn, Pn, SIDn, 0);
 }
 
 __global__ __launch_bounds__(kTPB) void k_lq_emit(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
@@ -386,6 +386,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
     std::vector<uint32_t> hsegc;
     std::vector<uint8_t> hflag;
     int level = 0;
+    static const int cap = getenv("MQ_LQ_CAP") ? atoi(getenv("MQ_LQ_CAP")) : kChainCap;
     unsigned int* flags = reinterpret_cast<unsigned int*>(small + 1);
     const uint32_t gn = stream_grid(s, n);
     hipLaunchKernelGGL(k_lq_init, dim3(gn), dim3(kTPB), 0, st, col, n, V[0], P[0], SID[0]);
@@ -411,7 +412,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
         HIPCHK(hipMemsetAsync(flags, 0, 8, st));
         HIPCHK(hipMemsetAsync(segflag, 0, S, st));
         hipLaunchKernelGGL(k_lq_final<false>, dim3(gn), dim3(kTPB), 0, st, V[cur], P[cur], SID[cur], seg[cur], EX,
-                           segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags, segflag);
+                           segc, lid, rid, J, n, V[cur ^ 1], P[cur ^ 1], SID[cur ^ 1], flags, segflag, cap);
         LAUNCHCHK("k_lq_final");
         unsigned long long h[2];
         HIPCHK(hipMemcpyAsync(h, small, 16, hipMemcpyDeviceToHost, st));
