@@ -192,7 +192,9 @@ __global__ __launch_bounds__(kTPB) void k_lq_less(const int32_t* __restrict__ V,
     }
 }
 
-constexpr int kChainCap = 64;  // chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
+// chain steps walked before pointer doubling takes over (MQ_LQ_CAP); 2^27 uniform rows:
+// 64 -> 288 ms, 128 -> 254, 256 -> 238, 512 -> 231 (the doubling only over flagged ranges)
+constexpr int kChainCap = 256;
 
 // One index of k_lq_final (below). Returns false when USE_F is false and the index
 // sits on a chain longer than kChainCap (it is placed later, after the doubling).
