@@ -33,6 +33,9 @@ uint32_t resident_grid(const DevState* s, uint64_t work_items, const void* fn);
 uint64_t scan_u32_scratch_elems(uint64_t n);
 int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st);
+// The same with u32 sums (n < 2^32 and a total below 2^32; in and out may alias).
+int scan_u32_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, unsigned long long* scratch,
+                           hipStream_t st);
 // The same over u64 elements (in and out may alias); scratch as above.
 int scan_u64_exclusive(const unsigned long long* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st);

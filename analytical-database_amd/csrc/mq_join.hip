@@ -78,8 +78,8 @@ __global__ __launch_bounds__(kTPB) void k_tile_sum(const Tin* in, uint64_t n, u6
 }
 
 // in and out may alias (every element is read into LDS before any is written).
-template <typename Tin>
-__global__ __launch_bounds__(kTPB) void k_tile_scan(const Tin* in, u64* out, uint64_t n,
+template <typename Tin, typename Tout = u64>
+__global__ __launch_bounds__(kTPB) void k_tile_scan(const Tin* in, Tout* out, uint64_t n,
                                                     const u64* offs) {
     __shared__ u64 tile[kScanTile];
     __shared__ u64 ws[kTPB / 64];
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kTPB) void k_tile_scan(const Tin* in, u64* out, uin
 #pragma unroll
     for (int k = 0; k < kScanItems; k++) {
         const uint64_t i = base + (uint64_t)k * kTPB + tid;
-        if (i < n) out[i] = tile[k * kTPB + tid];
+        if (i < n) out[i] = (Tout)tile[k * kTPB + tid];
     }
 }
 
@@ -134,11 +134,11 @@ uint64_t scan_scratch_elems(uint64_t n) {
     return total + 1;
 }
 
-template <typename Tin>
-int scan_exclusive(const Tin* in, u64* out, uint64_t n, u64* scratch, hipStream_t st) {
+template <typename Tin, typename Tout = u64>
+int scan_exclusive(const Tin* in, Tout* out, uint64_t n, u64* scratch, hipStream_t st) {
     if (n == 0) return MQ_OK;
     if (n <= (uint64_t)kScanTile) {
-        hipLaunchKernelGGL(k_tile_scan<Tin>, dim3(1), dim3(kTPB), 0, st, in, out, n,
+        hipLaunchKernelGGL((k_tile_scan<Tin, Tout>), dim3(1), dim3(kTPB), 0, st, in, out, n,
                            (const u64*)nullptr);
         LAUNCHCHK("k_tile_scan");
         return MQ_OK;
@@ -146,9 +146,9 @@ int scan_exclusive(const Tin* in, u64* out, uint64_t n, u64* scratch, hipStream_
     const uint64_t nb = ceil_div(n, kScanTile);
     hipLaunchKernelGGL(k_tile_sum<Tin>, dim3((uint32_t)nb), dim3(kTPB), 0, st, in, n, scratch);
     LAUNCHCHK("k_tile_sum");
-    int rc = scan_exclusive<u64>(scratch, scratch, nb, scratch + nb, st);
+    int rc = scan_exclusive<u64, u64>(scratch, scratch, nb, scratch + nb, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_tile_scan<Tin>, dim3((uint32_t)nb), dim3(kTPB), 0, st, in, out, n,
+    hipLaunchKernelGGL((k_tile_scan<Tin, Tout>), dim3((uint32_t)nb), dim3(kTPB), 0, st, in, out, n,
                        (const u64*)scratch);
     LAUNCHCHK("k_tile_scan");
     return MQ_OK;
@@ -1336,6 +1336,10 @@ uint64_t scan_u32_scratch_elems(uint64_t n) { return scan_scratch_elems(n); }
 int scan_u32_exclusive(const uint32_t* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st) {
     return scan_exclusive<uint32_t>(in, out, n, scratch, st);
+}
+int scan_u32_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, unsigned long long* scratch,
+                           hipStream_t st) {
+    return scan_exclusive<uint32_t, uint32_t>(in, out, n, scratch, st);
 }
 int scan_u64_exclusive(const unsigned long long* in, unsigned long long* out, uint64_t n,
                        unsigned long long* scratch, hipStream_t st) {
