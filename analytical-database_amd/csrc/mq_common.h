@@ -57,6 +57,9 @@ void shared_staging_release();
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
 // idle blocks are released by mq_trim(). A freed block may be handed out again at
 // once, so callers free only what no queued kernel still uses (sync first).
+// The reference's exact quicksort order (index.c:25-46) of col[0..n), n < 2^31, into
+// vout (values) and pout (size_t positions), either may be NULL (mq_lomuto.hip).
+int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, hipStream_t st, const DevState* s);
 void* pool_alloc(size_t bytes);
 void pool_free(void* p);
 

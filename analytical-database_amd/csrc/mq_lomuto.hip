@@ -1,0 +1,679 @@
+// mq_lomuto.hip — the reference's exact quicksort order on gfx950 (src/index.c:25-46).
+//
+// quicksort(low, high) partitions [low, high] around values[high] (Lomuto) and
+// recurses on both sides; disjoint ranges do not interact, so every range of one
+// recursion depth can be partitioned at once. One partition of a range with c values
+// below the pivot, restated without its sequential loop:
+//   * the k-th value below the pivot (index j_k, in index order) is swapped with
+//     index low + k, so it ends at low + k: the "<" side is a stable compaction;
+//   * a value >= the pivot moves only when it sits at low + k as the k-th "<" value
+//     is found (j_k is beyond it); it then jumps to j_k. From index x it therefore
+//     follows x -> J[x] -> J[J[x]] ... (J[low + k] = j_k) until the index leaves
+//     [low, low + c). Every step of every chain is one "<" value found while the
+//     ">=" block is not empty, so one partition's chains total at most c steps;
+//   * the final swap puts the pivot at low + c and the value that ended there at high.
+// A range whose values all equal its pivot would recurse one element per level
+// (O(n) depth); its outcome has a closed form: the last value first, then the others
+// in order (by induction over the partitions), so it finishes at once.
+//
+// Two phases:
+//   * large ranges (more than `small` indexes) are partitioned level by level over
+//     items of kItem indexes aligned to kItem (a block per item, 8 consecutive
+//     indexes per lane): count "<" / ">" per item, one scan over the items, the
+//     children, J, and the placement. Only the indexes of large ranges are read; a
+//     pivot, a child of one index and an all-equal range go straight to the output;
+//     a child of 2..small indexes joins the small list. A chain longer than kChainCap
+//     flags its range: J is pointer-doubled over that range's "<" zone and the range
+//     placed again.
+//   * each small range is finished by one wave with its values in LDS: the same
+//     partition with a ballot-ranked "<" side and chains walked in LDS, a stack of the
+//     sub-ranges above kTiny, and sub-ranges of 2..kTiny indexes run through the
+//     reference's own sequential partition by one lane each.
+// Values and row ids move as (int32, u32) pairs; the host reads one small record per
+// level. DESIGN.md §3.7 has the cost.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "mq_common.h"
+#include "mq_device.h"
+
+namespace {
+
+using namespace mqi;
+
+constexpr int kTPB = 256;
+constexpr uint32_t kItem = 2048;   // indexes per item: 256 lanes x 8
+constexpr uint32_t kEq = 0xFFFFFFFFu;
+constexpr int kTiny = 16;          // sub-ranges up to this size: one lane, sequential
+
+// chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
+constexpr int kChainCap = 256;
+
+struct LSeg {
+    uint32_t lo, hi;
+};
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// exclusive prefix of x over the 256 lanes of the block (sh: 4 words of LDS)
+__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t* sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < w; k++) pre += sh[k];
+    return pre + inc - x;
+}
+
+// The range of an item and the first index of the item's aligned chunk.
+struct ItemAt {
+    uint32_t r, base;
+    LSeg g;
+};
+__device__ __forceinline__ ItemAt item_at(uint32_t item, const uint32_t* __restrict__ imap,
+                                          const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff) {
+    ItemAt a;
+    a.r = imap[item];
+    a.g = seg[a.r];
+    a.base = (a.g.lo / kItem + (item - ioff[a.r])) * kItem;
+    return a;
+}
+
+__device__ __forceinline__ uint32_t items_of(uint32_t lo, uint32_t hi) { return hi / kItem - lo / kItem + 1; }
+
+// the last k < F with off[k] <= b (off ascending, off[0] = 0)
+__device__ __forceinline__ uint32_t upper_index(const uint32_t* __restrict__ off, uint32_t F, uint32_t b) {
+    uint32_t lo = 0, hi = F;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// the 8 values of this lane (indexes i0 .. i0+7 within [lo, hi]; others read as 0)
+template <typename T>
+__device__ __forceinline__ void load8(const T* __restrict__ a, uint32_t i0, uint32_t lo, uint32_t hi, T v[8]) {
+    if (i0 >= lo && i0 + 7 <= hi) {
+        const int4 x = *reinterpret_cast<const int4*>(a + i0);
+        const int4 y = *reinterpret_cast<const int4*>(a + i0 + 4);
+        v[0] = (T)x.x, v[1] = (T)x.y, v[2] = (T)x.z, v[3] = (T)x.w;
+        v[4] = (T)y.x, v[5] = (T)y.y, v[6] = (T)y.z, v[7] = (T)y.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = (i0 + k >= lo && i0 + k <= hi) ? a[i0 + k] : (T)0;
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void k_ld_init(const int32_t* __restrict__ col, uint64_t n, int32_t* __restrict__ V,
+                                                  uint32_t* __restrict__ P) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) {
+        V[i] = col[i];
+        P[i] = (uint32_t)i;
+    }
+}
+
+// per item: its range (the last r with ioff[r] <= item)
+__global__ __launch_bounds__(kTPB) void k_ld_imap(const uint32_t* __restrict__ ioff, uint32_t S, uint32_t NI,
+                                                  uint32_t* __restrict__ imap) {
+    for (uint32_t b = blockIdx.x * kTPB + threadIdx.x; b < NI; b += gridDim.x * kTPB) imap[b] = upper_index(ioff, S, b);
+}
+
+// per item: ("<" pivot) | (">" pivot) << 32 over its indexes, the pivot excluded; cnt[NI] = 0
+__global__ __launch_bounds__(kTPB) void k_ld_count(const int32_t* __restrict__ V, const LSeg* __restrict__ seg,
+                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
+                                                   uint32_t NI, unsigned long long* __restrict__ cnt) {
+    __shared__ unsigned long long s_acc;
+    const uint32_t item = blockIdx.x;
+    if (threadIdx.x == 0) s_acc = 0;
+    if (item == 0 && threadIdx.x == 0) cnt[NI] = 0;
+    const ItemAt a = item_at(item, imap, seg, ioff);
+    const int32_t piv = V[a.g.hi];
+    const uint32_t i0 = a.base + threadIdx.x * 8;
+    int32_t v[8];
+    load8(V, i0, a.g.lo, a.g.hi, v);
+    uint32_t lt = 0, gt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + k;
+        const bool ok = i >= a.g.lo && i < a.g.hi;
+        lt += ok && v[k] < piv;
+        gt += ok && v[k] > piv;
+    }
+    unsigned long long x = lt | ((unsigned long long)gt << 32);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_acc, x);
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[item] = s_acc;
+}
+
+// Per large range: c, all-equal, and its children: large ones (more than `small`
+// indexes) appended to the next level with their items (one packed atomic, so ranges
+// and their items keep one order), small ones (2..small) to the small list.
+__global__ __launch_bounds__(kTPB) void k_ld_children(const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff,
+                                                      uint32_t S, const unsigned long long* __restrict__ ex,
+                                                      uint32_t small, uint32_t dbuf, uint32_t* __restrict__ segc,
+                                                      LSeg* __restrict__ seg_next, uint32_t* __restrict__ ioff_next,
+                                                      unsigned long long* __restrict__ ctr, uint2* __restrict__ slist,
+                                                      unsigned int* __restrict__ nsmall) {
+    for (uint32_t r = blockIdx.x * kTPB + threadIdx.x; r < S; r += gridDim.x * kTPB) {
+        const LSeg g = seg[r];
+        const uint32_t f = ioff[r];
+        const unsigned long long tot = ex[f + items_of(g.lo, g.hi)] - ex[f];
+        const uint32_t c = (uint32_t)tot, gt = (uint32_t)(tot >> 32);
+        const bool eq = c == 0 && gt == 0;
+        segc[r] = eq ? kEq : c;
+        if (eq) continue;
+        const LSeg ch[2] = {{g.lo, g.lo + c - 1}, {g.lo + c + 1, g.hi}};
+        const uint32_t sz[2] = {c, g.hi - g.lo - c};
+        for (int k = 0; k < 2; k++) {
+            if (sz[k] > small) {
+                const uint32_t ni = items_of(ch[k].lo, ch[k].hi);
+                const unsigned long long old = atomicAdd(ctr, (1ull << 40) | ni);
+                const uint32_t idx = (uint32_t)(old >> 40);
+                seg_next[idx] = ch[k];
+                ioff_next[idx] = (uint32_t)(old & ((1ull << 40) - 1));
+            } else if (sz[k] >= 2) {
+                const unsigned int at = atomicAdd(nsmall, 1u);
+                slist[at] = make_uint2(ch[k].lo, ch[k].hi | (dbuf << 31));
+            }
+        }
+    }
+}
+
+// J[lo + rank] = index of the rank-th value below the pivot
+__global__ __launch_bounds__(kTPB) void k_ld_less(const int32_t* __restrict__ V, const LSeg* __restrict__ seg,
+                                                  const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
+                                                  const uint32_t* __restrict__ segc,
+                                                  const unsigned long long* __restrict__ ex, uint32_t* __restrict__ J) {
+    __shared__ uint32_t sh[4];
+    const uint32_t item = blockIdx.x;
+    const ItemAt a = item_at(item, imap, seg, ioff);
+    if (segc[a.r] == kEq) return;
+    const int32_t piv = V[a.g.hi];
+    const uint32_t i0 = a.base + threadIdx.x * 8;
+    int32_t v[8];
+    load8(V, i0, a.g.lo, a.g.hi, v);
+    uint32_t m = 0, nl = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const bool lt = i0 + k >= a.g.lo && i0 + k < a.g.hi && v[k] < piv;
+        m |= (uint32_t)lt << k;
+        nl += lt;
+    }
+    uint32_t rank = block_exscan(nl, sh) + ((uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]]);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (m >> k & 1) J[a.g.lo + rank++] = i0 + k;
+}
+
+// Placement of one item's indexes. Finals (the pivot, a child of one index, an
+// all-equal range) go to the output, the rest to the other buffer. The lane's 8
+// chains are walked together (their loads in flight at once). USE_F = false: a chain
+// longer than cap flags its range (appended once to flist) and leaves the index to
+// the second placement; USE_F = true (after the doubling): block b places item b -
+// foff[k] of flagged range flist[k].
+template <bool USE_F>
+__global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
+                                                   const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff,
+                                                   const uint32_t* __restrict__ imap, const uint32_t* __restrict__ segc,
+                                                   const unsigned long long* __restrict__ ex,
+                                                   const uint32_t* __restrict__ J, int32_t* __restrict__ Vd,
+                                                   uint32_t* __restrict__ Pd, int32_t* __restrict__ vout,
+                                                   unsigned long long* __restrict__ pout, uint32_t* __restrict__ segflag,
+                                                   uint32_t* __restrict__ flist, unsigned int* __restrict__ nflag,
+                                                   const uint32_t* __restrict__ foff, uint32_t F, int cap) {
+    __shared__ uint32_t sh[4];
+    uint32_t item;
+    ItemAt a;
+    if (USE_F) {
+        const uint32_t k = upper_index(foff, F, blockIdx.x);
+        a.r = flist[k];
+        item = ioff[a.r] + (blockIdx.x - foff[k]);
+        a.g = seg[a.r];
+        a.base = (a.g.lo / kItem + (blockIdx.x - foff[k])) * kItem;
+    } else {
+        item = blockIdx.x;
+        a = item_at(item, imap, seg, ioff);
+    }
+    const uint32_t lo = a.g.lo, hi = a.g.hi, c = segc[a.r];
+    const int32_t piv = V[hi];
+    const uint32_t i0 = a.base + threadIdx.x * 8;
+    int32_t v[8];
+    uint32_t p[8];
+    load8(V, i0, lo, hi, v);
+    load8(P, i0, lo, hi, p);
+    uint32_t nl = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) nl += c != kEq && i0 + k >= lo && i0 + k < hi && v[k] < piv;
+    uint32_t rank = block_exscan(nl, sh) + ((uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]]);
+    uint32_t q[8], fin = 0, walk = 0, live = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + k;
+        q[k] = i;
+        if (i < lo || i > hi) continue;
+        live |= 1u << k;
+        if (c == kEq) {                     // all equal: last first, then in order
+            q[k] = i == hi ? lo : i + 1;
+            fin |= 1u << k;
+        } else if (i == hi) {               // the pivot
+            q[k] = lo + c;
+            fin |= 1u << k;
+        } else if (v[k] < piv) {            // stable compaction of the "<" side
+            q[k] = lo + rank++;
+            fin |= (uint32_t)(c == 1) << k;
+        } else if (i - lo < c) {            // the >= side inside the "<" zone: follow the swaps
+            walk |= 1u << k;
+        }
+    }
+    for (int steps = 0; walk; steps++) {
+        if (!USE_F && steps >= cap) break;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (walk >> k & 1) q[k] = J[q[k]];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if ((walk >> k & 1) && q[k] - lo >= c) walk &= ~(1u << k);
+    }
+    if (!USE_F && walk) {                   // long chains: placed after the doubling
+        live &= ~walk;
+        if (atomicExch(&segflag[a.r], 1u) == 0u) flist[atomicAdd(nflag, 1u)] = a.r;
+    }
+    const bool rfin = c != kEq && hi - lo - c == 1;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (!(live >> k & 1)) continue;
+        const uint32_t i = i0 + k;
+        if (c != kEq && i != hi && !(v[k] < piv)) {  // the >= side
+            if (q[k] == lo + c) q[k] = hi;  // the final swap with the pivot
+            if (rfin) fin |= 1u << k;
+        }
+        if (fin >> k & 1) {
+            if (vout) vout[q[k]] = v[k];
+            if (pout) pout[q[k]] = p[k];
+        } else {
+            Vd[q[k]] = v[k];
+            Pd[q[k]] = p[k];
+        }
+    }
+}
+
+// flagged range k: items of its "<" zone (zi) and of the whole range (fi); entry F is 0
+__global__ __launch_bounds__(kTPB) void k_ld_fitems(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
+                                                    const uint32_t* __restrict__ flist, uint32_t F,
+                                                    uint32_t* __restrict__ zi, uint32_t* __restrict__ fi) {
+    for (uint32_t k = blockIdx.x * kTPB + threadIdx.x; k <= F; k += gridDim.x * kTPB) {
+        if (k == F) {
+            zi[k] = fi[k] = 0;
+            continue;
+        }
+        const uint32_t r = flist[k];
+        const LSeg g = seg[r];
+        zi[k] = items_of(g.lo, g.lo + segc[r] - 1);
+        fi[k] = items_of(g.lo, g.hi);
+    }
+}
+
+// one doubling step of J over the "<" zone [lo, lo + c) of the flagged ranges: block b
+// takes chunk b - zoff[k] of range flist[k]'s zone
+__global__ __launch_bounds__(kTPB) void k_ld_jump(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
+                                                  const uint32_t* __restrict__ flist, const uint32_t* __restrict__ zoff,
+                                                  uint32_t F, uint32_t* J, unsigned int* __restrict__ changed) {
+    const uint32_t k = upper_index(zoff, F, blockIdx.x);
+    const uint32_t r = flist[k];
+    const uint32_t lo = seg[r].lo, c = segc[r];
+    const uint32_t base = (lo / kItem + (blockIdx.x - zoff[k])) * kItem;
+    const uint32_t b = max(base, lo), e = min(base + kItem, lo + c);
+    unsigned int any = 0;
+    for (uint32_t i = b + threadIdx.x; i < e; i += kTPB) {
+        const uint32_t f = J[i];
+        if (f != i && f - lo < c) {
+            J[i] = J[f];
+            any = 1;
+        }
+    }
+    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(changed, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Small ranges: one wave each, values in LDS. A (l, h, buffer) record packs into
+// 32 bits as l | h << 12 | buffer << 24 (T <= 4096).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rec(int l, int h, int s) { return (uint32_t)l | (uint32_t)h << 12 | (uint32_t)s << 24; }
+
+template <int T>
+__global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0, const uint32_t* __restrict__ P0,
+                                                 const int32_t* __restrict__ V1, const uint32_t* __restrict__ P1,
+                                                 const uint2* __restrict__ list, uint32_t count,
+                                                 int32_t* __restrict__ vout, unsigned long long* __restrict__ pout) {
+    static_assert(T <= 4096 && T >= 64, "record packing");
+    __shared__ int32_t av[2][T];
+    __shared__ uint16_t ai[2][T];   // index within the range at the start (the row is read at the end)
+    __shared__ uint16_t J[T];
+    __shared__ uint8_t where[T];    // the buffer holding position k's final value
+    __shared__ uint32_t tiny[T / 2];
+    __shared__ uint32_t stk[T / kTiny + 8];
+    __shared__ uint16_t lstk[64][kTiny];
+    const int lane = threadIdx.x;
+    for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
+        const uint2 e = list[r];
+        const uint32_t lo = e.x, hi = e.y & 0x7FFFFFFFu;
+        const bool b1 = (e.y >> 31) != 0;
+        const int32_t* Vs = b1 ? V1 : V0;
+        const uint32_t* Ps = b1 ? P1 : P0;
+        const int m = (int)(hi - lo) + 1;
+        for (int k = lane; k < m; k += 64) {
+            av[0][k] = Vs[lo + k];
+            ai[0][k] = (uint16_t)k;
+            where[k] = 0;
+        }
+        int sp = 0, nt = 0;
+        if (m > kTiny) {
+            if (lane == 0) stk[0] = rec(0, m - 1, 0);
+            sp = 1;
+        } else if (m >= 2) {
+            if (lane == 0) tiny[0] = rec(0, m - 1, 0);
+            nt = 1;
+        }
+        __syncthreads();
+        while (sp > 0) {
+            const uint32_t t = stk[--sp];
+            const int l = t & 0xFFF, h = (t >> 12) & 0xFFF, s = t >> 24, d = s ^ 1;
+            const int32_t piv = av[s][h];
+            uint32_t carry = 0;
+            bool anygt = false;
+            for (int base = l; base < h; base += 64) {
+                const int i = base + lane;
+                const bool ok = i < h;
+                const int32_t v = ok ? av[s][i] : 0;
+                const bool lt = ok && v < piv;
+                anygt |= ok && v > piv;
+                const uint64_t mk = __ballot(lt);
+                if (lt) J[l + carry + lane_rank(mk)] = (uint16_t)i;
+                carry += (uint32_t)__popcll(mk);
+            }
+            const int c = (int)carry;
+            const bool eq = c == 0 && __ballot(anygt) == 0;
+            const int rsz = h - l - c;  // the right child's size
+            __syncthreads();
+            carry = 0;
+            for (int base = l; base <= h; base += 64) {
+                const int i = base + lane;
+                const bool ok = i <= h;
+                int32_t v = 0;
+                uint16_t x = 0;
+                if (ok) {
+                    v = av[s][i];
+                    x = ai[s][i];
+                }
+                const bool lt = !eq && ok && i != h && v < piv;
+                const uint64_t mk = __ballot(lt);
+                if (ok) {
+                    int q;
+                    bool fin;
+                    if (eq) {
+                        q = i == h ? l : i + 1;
+                        fin = true;
+                    } else if (i == h) {
+                        q = l + c;
+                        fin = true;
+                    } else if (lt) {
+                        q = l + (int)(carry + lane_rank(mk));
+                        fin = c == 1;
+                    } else {
+                        q = i;
+                        while (q - l < c) q = J[q];
+                        if (q == l + c) q = h;
+                        fin = rsz == 1;
+                    }
+                    av[d][q] = v;
+                    ai[d][q] = x;
+                    if (fin) where[q] = (uint8_t)d;
+                }
+                carry += (uint32_t)__popcll(mk);
+            }
+            if (!eq) {
+                // children in buffer d: the larger pushed first, so the stack stays shallow
+                int cl[2] = {l, l + c + 1}, ch[2] = {l + c - 1, h}, cs[2] = {c, rsz};
+                const int big = cs[0] >= cs[1] ? 0 : 1;
+                for (int k = 0; k < 2; k++) {
+                    const int j = k == 0 ? big : big ^ 1;
+                    if (cs[j] > kTiny) {
+                        if (lane == 0) stk[sp] = rec(cl[j], ch[j], d);
+                        sp++;
+                    } else if (cs[j] >= 2) {
+                        if (lane == 0) tiny[nt] = rec(cl[j], ch[j], d);
+                        nt++;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // sub-ranges of 2..kTiny indexes: the reference's partition, one lane each, in place
+        for (int tt = lane; tt < nt; tt += 64) {
+            const uint32_t t = tiny[tt];
+            const int l0 = t & 0xFFF, h0 = (t >> 12) & 0xFFF, s = t >> 24;
+            int32_t* A = av[s];
+            uint16_t* X = ai[s];
+            uint16_t* st = lstk[lane];
+            int top = 0;
+            st[top++] = (uint16_t)(0 | (h0 - l0) << 8);
+            while (top) {
+                const uint16_t w = st[--top];
+                const int lo2 = l0 + (w & 0xFF), hi2 = l0 + (w >> 8);
+                const int32_t piv = A[hi2];
+                int i = lo2 - 1;
+                for (int j = lo2; j < hi2; j++) {
+                    if (A[j] < piv) {
+                        i++;
+                        const int32_t tv = A[i];
+                        A[i] = A[j];
+                        A[j] = tv;
+                        const uint16_t tx = X[i];
+                        X[i] = X[j];
+                        X[j] = tx;
+                    }
+                }
+                {
+                    const int32_t tv = A[i + 1];
+                    A[i + 1] = A[hi2];
+                    A[hi2] = tv;
+                    const uint16_t tx = X[i + 1];
+                    X[i + 1] = X[hi2];
+                    X[hi2] = tx;
+                }
+                const int pv = i + 1;
+                if (pv - 1 > lo2) st[top++] = (uint16_t)((lo2 - l0) | (pv - 1 - l0) << 8);
+                if (hi2 > pv + 1) st[top++] = (uint16_t)((pv + 1 - l0) | (hi2 - l0) << 8);
+            }
+            for (int k = l0; k <= h0; k++) where[k] = (uint8_t)s;
+        }
+        __syncthreads();
+        for (int k = lane; k < m; k += 64) {
+            const int w = where[k];
+            if (vout) vout[lo + k] = av[w][k];
+            if (pout) pout[lo + k] = Ps[lo + ai[w][k]];
+        }
+        __syncthreads();
+    }
+}
+
+struct LdBufs {
+    void* blk[24];
+    int nb = 0, want = 0;
+    ~LdBufs() {
+        for (int i = 0; i < nb; i++) pool_free(blk[i]);
+    }
+    template <typename T>
+    T* get(size_t count) {
+        want++;
+        void* p = pool_alloc((count ? count : 1) * sizeof(T));
+        if (p) blk[nb++] = p;
+        return static_cast<T*>(p);
+    }
+};
+
+int small_threshold() {
+    static const int t = [] {
+        const char* e = getenv("MQ_LQ_SMALL");
+        const int v = e ? atoi(e) : 1024;
+        return v == 512 || v == 2048 ? v : 1024;
+    }();
+    return t;
+}
+
+int launch_small(int T, uint32_t grid, hipStream_t st, const int32_t* V0, const uint32_t* P0, const int32_t* V1,
+                 const uint32_t* P1, const uint2* list, uint32_t count, int32_t* vout, unsigned long long* pout) {
+    if (T == 512)
+        hipLaunchKernelGGL(k_ld_small<512>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+    else if (T == 2048)
+        hipLaunchKernelGGL(k_ld_small<2048>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+    else
+        hipLaunchKernelGGL(k_ld_small<1024>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+    LAUNCHCHK("k_ld_small");
+    return MQ_OK;
+}
+
+}  // namespace
+
+namespace mqi {
+
+int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64, hipStream_t st, const DevState* s) {
+    const uint32_t T = (uint32_t)small_threshold();
+    const uint64_t smax = n / (T + 1) + 2;            // large ranges are disjoint, > T indexes each
+    const uint64_t nimax = n / kItem + 2 * smax + 2;  // items of one level
+    unsigned long long* pout = reinterpret_cast<unsigned long long*>(pout64);
+    LdBufs b;
+    int32_t* V[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
+    uint32_t* P[2] = {b.get<uint32_t>(n), b.get<uint32_t>(n)};
+    uint32_t* J = b.get<uint32_t>(n);
+    LSeg* seg[2] = {b.get<LSeg>(smax), b.get<LSeg>(smax)};
+    uint32_t* ioff[2] = {b.get<uint32_t>(smax), b.get<uint32_t>(smax)};
+    uint32_t* segc = b.get<uint32_t>(smax);
+    uint32_t* segflag = b.get<uint32_t>(smax);  // ranges with a long chain, listed once in flist
+    uint32_t* flist = b.get<uint32_t>(smax);
+    uint32_t* zi = b.get<uint32_t>(smax + 1);    // per flagged range: items of its zone, of the range
+    uint32_t* fi = b.get<uint32_t>(smax + 1);
+    uint32_t* imap = b.get<uint32_t>(nimax);
+    unsigned long long* cnt = b.get<unsigned long long>(nimax + 1);
+    unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(nimax + 1));
+    uint2* slist = b.get<uint2>(n / 2 + 2);
+    unsigned long long* ctl = b.get<unsigned long long>(4);  // [next ranges << 40 | items, small | flagged, changed]
+    if (b.nb != b.want) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
+    unsigned int* ctl32 = reinterpret_cast<unsigned int*>(ctl + 1);  // [0] small count, [1] flagged, [2] changed
+    static const bool stats = getenv("MQ_LQ_STATS") != nullptr;     // per-level diagnostics (stderr)
+    static const int cap = getenv("MQ_LQ_CAP") ? atoi(getenv("MQ_LQ_CAP")) : kChainCap;
+    HIPCHK(hipMemsetAsync(ctl, 0, 32, st));
+    hipLaunchKernelGGL(k_ld_init, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, col, n, V[0], P[0]);
+    LAUNCHCHK("k_ld_init");
+    uint64_t S = 0, NI = 0;
+    uint32_t nsmall = 0;
+    if (n > T) {
+        const LSeg root{0u, (uint32_t)(n - 1)};
+        const uint32_t z = 0;
+        HIPCHK(hipMemcpyAsync(seg[0], &root, sizeof root, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ioff[0], &z, 4, hipMemcpyHostToDevice, st));
+        S = 1;
+        NI = (n - 1) / kItem + 1;
+    } else {
+        const uint2 one = make_uint2(0u, (uint32_t)(n - 1));
+        HIPCHK(hipMemcpyAsync(slist, &one, sizeof one, hipMemcpyHostToDevice, st));
+        nsmall = 1;
+    }
+    int cur = 0, level = 0;
+    while (S) {
+        const int d = cur ^ 1;
+        hipLaunchKernelGGL(k_ld_imap, dim3(stream_grid(s, NI)), dim3(kTPB), 0, st, ioff[cur], (uint32_t)S,
+                           (uint32_t)NI, imap);
+        LAUNCHCHK("k_ld_imap");
+        hipLaunchKernelGGL(k_ld_count, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap,
+                           (uint32_t)NI, cnt);
+        LAUNCHCHK("k_ld_count");
+        int rc = scan_u64_exclusive(cnt, cnt, NI + 1, scratch, st);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(ctl, 0, 8, st));
+        HIPCHK(hipMemsetAsync(ctl32 + 1, 0, 8, st));
+        hipLaunchKernelGGL(k_ld_children, dim3(stream_grid(s, S)), dim3(kTPB), 0, st, seg[cur], ioff[cur],
+                           (uint32_t)S, cnt, T, (uint32_t)d, segc, seg[d], ioff[d], ctl, slist, ctl32);
+        LAUNCHCHK("k_ld_children");
+        hipLaunchKernelGGL(k_ld_less, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap, segc,
+                           cnt, J);
+        LAUNCHCHK("k_ld_less");
+        HIPCHK(hipMemsetAsync(segflag, 0, S * 4, st));
+        hipLaunchKernelGGL(k_ld_final<false>, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur],
+                           ioff[cur], imap, segc, cnt, J, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
+                           (const uint32_t*)nullptr, 0u, cap);
+        LAUNCHCHK("k_ld_final");
+        unsigned long long h[2];
+        HIPCHK(hipMemcpyAsync(h, ctl, 16, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        int jumps = 0;
+        const uint32_t F = (uint32_t)(h[1] >> 32);
+        if (F) {  // chains longer than cap: double J over the flagged ranges' zones, then place them again
+            hipLaunchKernelGGL(k_ld_fitems, dim3(stream_grid(s, F + 1)), dim3(kTPB), 0, st, seg[cur], segc, flist, F,
+                               zi, fi);
+            LAUNCHCHK("k_ld_fitems");
+            if ((rc = scan_u32_exclusive_u32(zi, zi, F + 1, scratch, st))) return rc;
+            if ((rc = scan_u32_exclusive_u32(fi, fi, F + 1, scratch, st))) return rc;
+            uint32_t nz = 0, nf = 0;
+            HIPCHK(hipMemcpyAsync(&nz, zi + F, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&nf, fi + F, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (;; jumps++) {
+                if (jumps > 40) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
+                HIPCHK(hipMemsetAsync(ctl32 + 2, 0, 4, st));
+                hipLaunchKernelGGL(k_ld_jump, dim3(nz), dim3(kTPB), 0, st, seg[cur], segc, flist, zi, F, J, ctl32 + 2);
+                LAUNCHCHK("k_ld_jump");
+                unsigned int ch = 0;
+                HIPCHK(hipMemcpyAsync(&ch, ctl32 + 2, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                if (!ch) break;
+            }
+            hipLaunchKernelGGL(k_ld_final<true>, dim3(nf), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur], ioff[cur], imap,
+                               segc, cnt, J, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1, (const uint32_t*)fi, F,
+                               0);
+            LAUNCHCHK("k_ld_final");
+        }
+        nsmall = (uint32_t)h[1];
+        if (stats) {
+            std::vector<LSeg> hs(S);
+            HIPCHK(hipMemcpy(hs.data(), seg[cur], S * sizeof(LSeg), hipMemcpyDeviceToHost));
+            uint64_t rows = 0;
+            for (const LSeg& g : hs) rows += (uint64_t)g.hi - g.lo + 1;
+            fprintf(stderr, "lq level %d: large ranges %llu rows %llu items %llu | small so far %u | flagged %u jumps %d\n",
+                    level, (unsigned long long)S, (unsigned long long)rows, (unsigned long long)NI, nsmall,
+                    F, jumps);
+        }
+        S = h[0] >> 40;
+        NI = h[0] & ((1ull << 40) - 1);
+        cur = d;
+        level++;
+    }
+    if (nsmall) {
+        const uint32_t grid = nsmall < 16384u ? nsmall : 16384u;
+        int rc = launch_small((int)T, grid, st, V[0], P[0], V[1], P[1], slist, nsmall, vout, pout);
+        if (rc) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(st));  // the buffers go back to the pool
+    return MQ_OK;
+}
+
+}  // namespace mqi

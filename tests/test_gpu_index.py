@@ -247,3 +247,48 @@ def test_index_build_lomuto_full_size(lib, refcpu, case):
     assert ex.value == 1
     assert f"{refcpu.fnv1a64(v.get(np.int32, n)):016x}" == case["values_fnv"]
     assert f"{refcpu.fnv1a64(p.get(np.uint64, n)):016x}" == case["positions_fnv"]
+
+
+_VARIANT_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1]]
+from devbuf import Dev
+from refapi import mq
+L = mq.load()
+mq.check(L.mq_init(0))
+d = np.load(sys.argv[2])
+out = {}
+for name in d.files:
+    col = d[name]
+    n = len(col)
+    c, v, p = Dev.of(col), Dev(n * 4), Dev(n * 8)
+    mq.check(L.mq_index_build_lomuto(c.ptr, n, v.ptr, p.ptr, None))
+    out[name + "_v"], out[name + "_p"] = v.get(np.int32, n), p.get(np.uint64, n)
+np.savez(sys.argv[3], **out)
+"""
+
+
+@pytest.mark.parametrize("small,cap", [("512", "1"), ("2048", "3"), ("1024", "100000")])
+def test_index_build_lomuto_variants(refcpu, tmp_path, small, cap):
+    """The same order with the other small-range finishers (MQ_LQ_SMALL) and chain
+    caps (MQ_LQ_CAP=1: pointer doubling in every range of every level; 100000: none),
+    in a child process (both are read once per process)."""
+    import os
+    import subprocess
+    import sys
+    rng = np.random.default_rng(11)
+    cols = {"long_chain": np.concatenate([[10**6], np.arange(1, 20000), [10**6 - 1]]).astype(np.int32),
+            "dups": rng.integers(0, 500, 150_000).astype(np.int32),
+            "distinct": rng.integers(-2**31, 2**31 - 1, 250_000, dtype=np.int64).astype(np.int32),
+            "sorted_desc": np.arange(5000, 0, -1).astype(np.int32),
+            "two_values": rng.integers(0, 2, 70_000).astype(np.int32)}
+    np.savez(tmp_path / "in.npz", **cols)
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MQ_LQ_SMALL=small, MQ_LQ_CAP=cap)
+    subprocess.run([sys.executable, "-c", _VARIANT_CHILD, here, str(tmp_path / "in.npz"), str(tmp_path / "out.npz")],
+                   env=env, check=True, timeout=240)
+    got = np.load(tmp_path / "out.npz")
+    for name, col in cols.items():
+        wv, wp = refcpu.index_build_lomuto(col)
+        assert np.array_equal(got[name + "_v"], wv), name
+        assert np.array_equal(got[name + "_p"], wp), name
