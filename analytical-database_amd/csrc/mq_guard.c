@@ -63,6 +63,7 @@ typedef struct {
     size_t bytes;
     unsigned char* edge;    /* [p, lo) then [hi, p + bytes); the whole range if lo == hi */
     size_t head, tail;
+    _Atomic int refs;       /* owners of one handle: a range armed again while armed */
 } Guard;
 
 static Guard g_guard[NGUARD];
@@ -263,6 +264,19 @@ uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {
     const uintptr_t pg = page();
     uintptr_t lo = (a + pg - 1) & ~(pg - 1), hi = b & ~(pg - 1);
     if (hi <= lo) lo = hi = 0;
+    /* the same range already armed (a column resident both whole on one device and
+     * split over the row shards): one more owner of that guard, since a second
+     * mprotect-based guard cannot arm over read-only pages */
+    const int hw0 = atomic_load(&g_hw);
+    for (int i = 0; i < hw0; i++) {
+        Guard* g = &g_guard[i];
+        if (atomic_load(&g->state) == G_ARMED && g->p == (const unsigned char*)p && g->bytes == bytes &&
+            (g->hi == g->lo || still_armed(g->lo))) {
+            atomic_fetch_add(&g->refs, 1);
+            g_stats.armed++;
+            return ((uint64_t)g->gen << 32) | (uint32_t)i;
+        }
+    }
     int prot = PROT_READ | PROT_WRITE;
     if (kind == MQ_GUARD_CHUNK) {
         if (!mq_guard_chunk_ok(p)) return 0;
@@ -296,6 +310,7 @@ uint64_t mq_guard_arm(const void* p, size_t bytes, int kind) {
     g->edge = edge;
     g->head = head;
     g->tail = tail;
+    atomic_store(&g->refs, 1);
     if (!g->gen) g->gen = 1;
     install();
     atomic_store_explicit(&g->state, G_ARMED, memory_order_release);
@@ -340,6 +355,7 @@ int mq_guard_clean(uint64_t h, const void* p, size_t bytes) {
 void mq_guard_release(uint64_t h) {
     Guard* g = lookup(h);
     if (!g) return;
+    if (atomic_fetch_sub(&g->refs, 1) > 1) return; /* another owner still holds it */
     restore(g);
     slot_free(g);
 }

@@ -49,10 +49,11 @@ using namespace mqi;
 constexpr int kTPB = 256;
 constexpr uint32_t kItem = 2048;   // indexes per item: 256 lanes x 8
 constexpr uint32_t kEq = 0xFFFFFFFFu;
-constexpr int kTiny = 16;          // sub-ranges up to this size: one lane, sequential
 
 // chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
 constexpr int kChainCap = 256;
+constexpr int kMaxJumps = 64;      // doubling steps per level (2^64 > any chain)
+constexpr int kJumpBatch = 4;      // doubling steps launched per host check
 
 struct LSeg {
     uint32_t lo, hi;
@@ -137,11 +138,20 @@ __global__ __launch_bounds__(kTPB) void k_ld_imap(const uint32_t* __restrict__ i
 // per item: ("<" pivot) | (">" pivot) << 32 over its indexes, the pivot excluded; cnt[NI] = 0
 __global__ __launch_bounds__(kTPB) void k_ld_count(const int32_t* __restrict__ V, const LSeg* __restrict__ seg,
                                                    const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
-                                                   uint32_t NI, unsigned long long* __restrict__ cnt) {
+                                                   uint32_t NI, unsigned long long* __restrict__ cnt,
+                                                   unsigned long long* __restrict__ ctl,
+                                                   unsigned int* __restrict__ chg) {
     __shared__ unsigned long long s_acc;
     const uint32_t item = blockIdx.x;
     if (threadIdx.x == 0) s_acc = 0;
-    if (item == 0 && threadIdx.x == 0) cnt[NI] = 0;
+    if (item == 0) {  // this level's control words: next-level counter, flagged count, doubling flags
+        if (threadIdx.x == 0) {
+            cnt[NI] = 0;
+            ctl[0] = 0;
+            reinterpret_cast<unsigned int*>(ctl + 1)[1] = 0;
+        }
+        if (threadIdx.x < kMaxJumps) chg[threadIdx.x] = 0;
+    }
     const ItemAt a = item_at(item, imap, seg, ioff);
     const int32_t piv = V[a.g.hi];
     const uint32_t i0 = a.base + threadIdx.x * 8;
@@ -170,6 +180,7 @@ __global__ __launch_bounds__(kTPB) void k_ld_count(const int32_t* __restrict__ V
 __global__ __launch_bounds__(kTPB) void k_ld_children(const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff,
                                                       uint32_t S, const unsigned long long* __restrict__ ex,
                                                       uint32_t small, uint32_t dbuf, uint32_t* __restrict__ segc,
+                                                      uint32_t* __restrict__ segflag,
                                                       LSeg* __restrict__ seg_next, uint32_t* __restrict__ ioff_next,
                                                       unsigned long long* __restrict__ ctr, uint2* __restrict__ slist,
                                                       unsigned int* __restrict__ nsmall) {
@@ -180,6 +191,7 @@ __global__ __launch_bounds__(kTPB) void k_ld_children(const LSeg* __restrict__ s
         const uint32_t c = (uint32_t)tot, gt = (uint32_t)(tot >> 32);
         const bool eq = c == 0 && gt == 0;
         segc[r] = eq ? kEq : c;
+        segflag[r] = 0;
         if (eq) continue;
         const LSeg ch[2] = {{g.lo, g.lo + c - 1}, {g.lo + c + 1, g.hi}};
         const uint32_t sz[2] = {c, g.hi - g.lo - c};
@@ -332,11 +344,15 @@ __global__ __launch_bounds__(kTPB) void k_ld_fitems(const LSeg* __restrict__ seg
     }
 }
 
-// one doubling step of J over the "<" zone [lo, lo + c) of the flagged ranges: block b
-// takes chunk b - zoff[k] of range flist[k]'s zone
+// Doubling step `it` of J over the "<" zone [lo, lo + c) of the flagged ranges: block b
+// takes chunk b - zoff[k] of range flist[k]'s zone. chg[it] records a change; a step
+// whose predecessor changed nothing returns at once, so the host launches steps in
+// batches and reads one flag per batch.
 __global__ __launch_bounds__(kTPB) void k_ld_jump(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
                                                   const uint32_t* __restrict__ flist, const uint32_t* __restrict__ zoff,
-                                                  uint32_t F, uint32_t* J, unsigned int* __restrict__ changed) {
+                                                  uint32_t F, uint32_t* J, unsigned int* __restrict__ chg, int it) {
+    if (it > 0 && chg[it - 1] == 0u) return;
+    unsigned int* changed = chg + it;
     const uint32_t k = upper_index(zoff, F, blockIdx.x);
     const uint32_t r = flist[k];
     const uint32_t lo = seg[r].lo, c = segc[r];
@@ -359,7 +375,7 @@ __global__ __launch_bounds__(kTPB) void k_ld_jump(const LSeg* __restrict__ seg, 
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rec(int l, int h, int s) { return (uint32_t)l | (uint32_t)h << 12 | (uint32_t)s << 24; }
 
-template <int T>
+template <int T, int kTiny>
 __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0, const uint32_t* __restrict__ P0,
                                                  const int32_t* __restrict__ V1, const uint32_t* __restrict__ P1,
                                                  const uint2* __restrict__ list, uint32_t count,
@@ -540,14 +556,35 @@ int small_threshold() {
     return t;
 }
 
+int tiny_threshold() {
+    static const int t = [] {
+        const char* e = getenv("MQ_LQ_TINY");
+        const int v = e ? atoi(e) : 16;
+        return v == 8 || v == 32 ? v : 16;
+    }();
+    return t;
+}
+
+template <int T>
+void launch_small_t(uint32_t grid, hipStream_t st, const int32_t* V0, const uint32_t* P0, const int32_t* V1,
+                    const uint32_t* P1, const uint2* list, uint32_t count, int32_t* vout, unsigned long long* pout) {
+    const int tiny = tiny_threshold();
+    if (tiny == 8)
+        hipLaunchKernelGGL((k_ld_small<T, 8>), dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+    else if (tiny == 32)
+        hipLaunchKernelGGL((k_ld_small<T, 32>), dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+    else
+        hipLaunchKernelGGL((k_ld_small<T, 16>), dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+}
+
 int launch_small(int T, uint32_t grid, hipStream_t st, const int32_t* V0, const uint32_t* P0, const int32_t* V1,
                  const uint32_t* P1, const uint2* list, uint32_t count, int32_t* vout, unsigned long long* pout) {
     if (T == 512)
-        hipLaunchKernelGGL(k_ld_small<512>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+        launch_small_t<512>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
     else if (T == 2048)
-        hipLaunchKernelGGL(k_ld_small<2048>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+        launch_small_t<2048>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
     else
-        hipLaunchKernelGGL(k_ld_small<1024>, dim3(grid), dim3(64), 0, st, V0, P0, V1, P1, list, count, vout, pout);
+        launch_small_t<1024>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
     LAUNCHCHK("k_ld_small");
     return MQ_OK;
 }
@@ -576,12 +613,15 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     unsigned long long* cnt = b.get<unsigned long long>(nimax + 1);
     unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(nimax + 1));
     uint2* slist = b.get<uint2>(n / 2 + 2);
-    unsigned long long* ctl = b.get<unsigned long long>(4);  // [next ranges << 40 | items, small | flagged, changed]
+    unsigned long long* ctl = b.get<unsigned long long>(4 + kMaxJumps / 2);  // see ctl32, chg
     if (b.nb != b.want) return set_err(MQ_ENOMEM, "mq_index_build_lomuto: device allocation failed");
-    unsigned int* ctl32 = reinterpret_cast<unsigned int*>(ctl + 1);  // [0] small count, [1] flagged, [2] changed
+    // ctl[0]: next level's ranges << 40 | items; ctl32: [0] small ranges so far, [1] flagged
+    // ranges of this level; chg: one flag per doubling step of this level
+    unsigned int* ctl32 = reinterpret_cast<unsigned int*>(ctl + 1);
+    unsigned int* chg = reinterpret_cast<unsigned int*>(ctl + 4);
     static const bool stats = getenv("MQ_LQ_STATS") != nullptr;     // per-level diagnostics (stderr)
     static const int cap = getenv("MQ_LQ_CAP") ? atoi(getenv("MQ_LQ_CAP")) : kChainCap;
-    HIPCHK(hipMemsetAsync(ctl, 0, 32, st));
+    HIPCHK(hipMemsetAsync(ctl, 0, 32, st));  // (ctl32[0] is never reset after this)
     hipLaunchKernelGGL(k_ld_init, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, col, n, V[0], P[0]);
     LAUNCHCHK("k_ld_init");
     uint64_t S = 0, NI = 0;
@@ -605,19 +645,16 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
                            (uint32_t)NI, imap);
         LAUNCHCHK("k_ld_imap");
         hipLaunchKernelGGL(k_ld_count, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap,
-                           (uint32_t)NI, cnt);
+                           (uint32_t)NI, cnt, ctl, chg);
         LAUNCHCHK("k_ld_count");
         int rc = scan_u64_exclusive(cnt, cnt, NI + 1, scratch, st);
         if (rc) return rc;
-        HIPCHK(hipMemsetAsync(ctl, 0, 8, st));
-        HIPCHK(hipMemsetAsync(ctl32 + 1, 0, 8, st));
         hipLaunchKernelGGL(k_ld_children, dim3(stream_grid(s, S)), dim3(kTPB), 0, st, seg[cur], ioff[cur],
-                           (uint32_t)S, cnt, T, (uint32_t)d, segc, seg[d], ioff[d], ctl, slist, ctl32);
+                           (uint32_t)S, cnt, T, (uint32_t)d, segc, segflag, seg[d], ioff[d], ctl, slist, ctl32);
         LAUNCHCHK("k_ld_children");
         hipLaunchKernelGGL(k_ld_less, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap, segc,
                            cnt, J);
         LAUNCHCHK("k_ld_less");
-        HIPCHK(hipMemsetAsync(segflag, 0, S * 4, st));
         hipLaunchKernelGGL(k_ld_final<false>, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur],
                            ioff[cur], imap, segc, cnt, J, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
                            (const uint32_t*)nullptr, 0u, cap);
@@ -637,13 +674,14 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
             HIPCHK(hipMemcpyAsync(&nz, zi + F, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(&nf, fi + F, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
-            for (;; jumps++) {
-                if (jumps > 40) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
-                HIPCHK(hipMemsetAsync(ctl32 + 2, 0, 4, st));
-                hipLaunchKernelGGL(k_ld_jump, dim3(nz), dim3(kTPB), 0, st, seg[cur], segc, flist, zi, F, J, ctl32 + 2);
-                LAUNCHCHK("k_ld_jump");
+            for (;;) {
+                if (jumps >= kMaxJumps) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
+                for (int k = 0; k < kJumpBatch; k++, jumps++) {
+                    hipLaunchKernelGGL(k_ld_jump, dim3(nz), dim3(kTPB), 0, st, seg[cur], segc, flist, zi, F, J, chg, jumps);
+                    LAUNCHCHK("k_ld_jump");
+                }
                 unsigned int ch = 0;
-                HIPCHK(hipMemcpyAsync(&ch, ctl32 + 2, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(&ch, chg + jumps - 1, 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
                 if (!ch) break;
             }

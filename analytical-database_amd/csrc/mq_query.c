@@ -1461,6 +1461,7 @@ int mq_column_attach(Column* column, const int32_t* d_data) {
 int mq_column_upload(Column* column) {
     Status st = {OK, NULL};
     if (op_begin(&st)) return MQ_ENODEV;
+    if (shard_wants(column)) return shard_upload(column, &st) ? MQ_EHIP : MQ_OK;
     const int32_t* d;
     return column_device(column, &d, &st) ? MQ_EHIP : MQ_OK;
 }
@@ -1521,6 +1522,7 @@ double shim_now(void) { return now_s(); }
 int shim_trace_on(void) { return trace_on(); }
 int shim_fail(Status* st, const char* what, int rc) { return fail(st, what, rc); }
 void* shim_payload_alloc(size_t bytes) { return payload_alloc(bytes); }
+
 Result* shim_new_result(DataType t, size_t n, void* payload) { return new_result(t, n, payload); }
 unsigned long long shim_op(void) { return g_op; }
 size_t shim_shadow_budget(void) { return shadow_budget(); }

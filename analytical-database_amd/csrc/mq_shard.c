@@ -704,6 +704,8 @@ void shard_op_begin(void) {
     ssh_make_room(0);
 }
 
+int shard_upload(Column* c, Status* st) { return scol_get(c, st) ? 0 : -1; }
+
 void shard_forget_column(const Column* c) {
     for (int i = 0; i < g_nscols; i++)
         if (g_scols[i].col == c) {

@@ -46,6 +46,8 @@ int shard_reduce_result(const Result* r, mq_agg* a, Status* st);
 Result** shard_shared_select(SelectOperator* ops, int q, Column* c, Status* st);
 void shard_op_begin(void);                 /* sweep + budget at every operator start */
 void shard_forget_column(const Column* c);
+/* make c resident on the shards now (mq_column_upload of a sharded column): 0 or -1 */
+int shard_upload(Column* c, Status* st);
 void shard_release_all(void);
 void shard_stats(mq_residency* out);
 

@@ -11,6 +11,7 @@ stream, overlapped with the next step's scan (double-buffered aggregates). Data 
 (SURVEY.md §8(c) generator), generated on the device.
 
   python bench.py [--gpus N --steps K --warmup W] [--rows R] [--no-cpu] [--no-extra]
+  python bench.py --inproc [--gpus N]   libmq's own row-shard path, one process (inproc_main)
 
 Rank 0 prints ONE JSON line. Roofline: algorithmic bytes 4N per scan launch ÷ the
 scan kernel's mean duration from HIP events on the launch stream. cpu_baseline:
@@ -157,7 +158,118 @@ def launch_ranks(ngpus: int, argv: list) -> int:
     return bad[0] if bad else 0
 
 
+def inproc_main(args) -> None:
+    """--inproc: libmq's own multi-GPU path (mq_shard.c) in ONE process, as the
+    reference server would run it after linking libmq: one 1e9-row column (a memfd
+    file mapping, like the reference's column files) split into --gpus row shards,
+    shard g resident on GPU g (mq_shard_config) with a host thread and stream of its
+    own; a step is the reference's chain select_column -> fetch_column -> sum
+    (server.c:137-247), each operator running on every shard and concatenating /
+    folding in shard order. PCIe-inclusive (the API returns host payloads), total
+    work fixed ("strong"). MQ_BENCH_ONE_DEVICE=1 puts every shard on GPU 0 (a
+    rehearsal of the split on a one-GPU box). Parity: K and the sum against the
+    reference's goldens (seed 42)."""
+    import mmap
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    mq = _load("mq_binding", os.path.join(PKG, "mq.py"))
+    from refapi import make_column, _libc
+    ng = args.gpus
+    devices = [0] * ng if os.environ.get("MQ_BENCH_ONE_DEVICE") == "1" else list(range(ng))
+    lib = mq.load()
+    mq.check(lib.mq_init(0), "mq_init")
+    n = args.rows
+    lo = int(0.25 * n)
+    hi = lo + int(args.sel * n)
+    # the §8(c) column, generated on the device and copied into a file mapping
+    fd = os.memfd_create("col")
+    os.ftruncate(fd, 4 * n)
+    m = mmap.mmap(fd, 4 * n, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+    os.close(fd)
+    host = np.frombuffer(m, dtype=np.int32)
+    g = torch.empty(n, dtype=torch.int32, device="cuda")
+    mq.check(lib.mq_gen_uniform(g.data_ptr(), n, 42, n, None), "gen")
+    torch.cuda.synchronize()
+    host[:] = g.cpu().numpy()
+    del g
+    torch.cuda.empty_cache()
+    col = make_column(host, b"col")
+    arr = (C.c_int * ng)(*devices)
+    mq.check(lib.mq_shard_config(ng, arr, ng, 0), "mq_shard_config")
+    t0 = time.perf_counter()
+    mq.check(lib.mq_column_upload(C.byref(col)), "upload")
+    t_up = time.perf_counter() - t0
+    lo_c, hi_c = C.c_int(lo), C.c_int(hi)
+    step_s, k, total = [], None, None
+    for i in range(args.warmup + args.steps):
+        st = mq.Status(0, None)
+        t0 = time.perf_counter()
+        rp = lib.select_column(C.byref(col), C.byref(lo_c), C.byref(hi_c), C.byref(st))
+        rf = lib.fetch_column(C.byref(col), rp, C.byref(st)) if st.code == mq.OK else None
+        gc = mq.GeneralizedColumn()
+        gc.column_type = mq.RESULT
+        gc.column_pointer.result = rf
+        rs = lib.sum(C.byref(gc), C.byref(st)) if st.code == mq.OK else None
+        dt = time.perf_counter() - t0
+        if st.code != mq.OK:
+            print(f"bench.py --inproc: operator failed: {st.error_message}", file=sys.stderr)
+            sys.exit(1)
+        k = rp.contents.num_tuples
+        total = C.cast(rs.contents.payload, C.POINTER(C.c_longlong))[0]
+        for r in (rp, rf, rs):
+            _libc.free(r.contents.payload)
+            _libc.free(r)
+        if i >= args.warmup:
+            step_s.append(dt)
+    resid = mq.residency(lib)
+    lib.mq_release_all()
+    mq.check(lib.mq_shard_config(0, None, 0, 0), "mq_shard_config reset")
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "goldens.json")))
+    want = next((r for r in gold["config4"] if r["n"] == n and r["seed"] == 42 and r["low"] == lo and r["high"] == hi),
+                None)
+    parity = None if want is None else (k, total) == (want["k"], want["sum"])
+    elapsed = sum(step_s)
+    out = {
+        "metric": "rows/sec, 1B-row int32 select -> fetch -> sum through libmq's drop-in API "
+                  "(PCIe-inclusive), one process, row shards over N GPUs",
+        "value": n * len(step_s) / elapsed,
+        "unit": "rows/s",
+        "n_gpus": ng,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / len(step_s),
+        "ms_per_step_median": 1e3 * statistics.median(step_s),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": "select_column -> fetch_column -> sum on one 1e9-row column, row-sharded",
+                   "rows": n, "selectivity": args.sel, "low": lo, "high": hi, "shards": ng,
+                   "devices": devices, "parallelism": f"row shards x{ng} (mq_shard.c), one process"},
+        "ms_upload": 1e3 * t_up,
+        "upload_gbs": 4.0 * n / t_up / 1e9,
+        "residency": resid,
+        "parity": {"ok": parity, "count": k, "sum": total},
+    }
+    print(json.dumps(out), flush=True)
+    if parity is False:
+        print("bench.py --inproc: parity FAILED", file=sys.stderr)
+        sys.exit(1)
+
+
 def main() -> None:
+    if "--inproc" in sys.argv[1:]:
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--inproc", action="store_true")
+        ap.add_argument("--gpus", type=int, default=1)
+        ap.add_argument("--steps", type=int, default=10)
+        ap.add_argument("--warmup", type=int, default=2)
+        ap.add_argument("--rows", type=int, default=1_000_000_000)
+        ap.add_argument("--sel", type=float, default=0.01)
+        inproc_main(ap.parse_args())
+        return
     if "WORLD_SIZE" not in os.environ:
         pre = argparse.ArgumentParser(add_help=False)
         pre.add_argument("--gpus", type=int, default=1)

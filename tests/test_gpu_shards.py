@@ -144,6 +144,36 @@ def test_shard_residency_and_rewrite(lib, refcpu):
     lib.mq_release_all()
 
 
+def test_sharded_column_stays_resident_after_upload(lib, refcpu):
+    """mq_column_upload of a column the shards serve, then select -> fetch -> sum three
+    times (the chain of bench.py --inproc): one shard upload, no re-upload per operator.
+    (Found by --inproc: the one-device copy's write guard made the shard copy's guard
+    fail to arm, so every operator uploaded the shards again.)"""
+    config(lib, 2)
+    n = 2_000_000
+    a, m, col = memfd_column(refcpu.gen_uniform(n, 46))
+    lo, hi = n // 4, n // 4 + n // 50
+    up0 = mq.residency(lib)["shard_uploads"]
+    assert lib.mq_column_upload(C.byref(col)) == 0
+    assert mq.residency(lib)["shard_uploads"] == up0 + 1
+    want = refcpu.select_scan(a, lo, hi)
+    for _ in range(3):
+        rp = select(lib, col, lo, hi)
+        assert np.array_equal(take(rp, free=False), want)
+        rf = fetch(lib, col, rp)
+        assert agg(lib, rf)["sum"] == int(a[want].astype(np.int64).sum())
+        take(rp)
+        take(rf)
+    assert mq.residency(lib)["shard_uploads"] == up0 + 1, "shards uploaded again"
+    # the one-device path (a column below the shard threshold is not this one) takes the
+    # column back whole after the shards drop it
+    config(lib, 1)
+    assert np.array_equal(take(select(lib, col, lo, hi)), want)
+    col.data = None
+    del a
+    lib.mq_release_all()
+
+
 def test_fetch_with_foreign_positions(lib, refcpu):
     """Positions that did not come from the shards (value order, duplicates, the
     caller's own payload) take the one-device path."""

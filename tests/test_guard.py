@@ -61,6 +61,32 @@ def test_file_mapping_clean_until_written(lib):
     m.close()
 
 
+def test_same_range_armed_twice_shares_one_guard(lib):
+    """A column resident both whole on one device and split over row shards arms the
+    same range twice: the second arm joins the first guard (a second mprotect guard
+    could not arm over read-only pages); one release leaves it armed for the other
+    owner, a write is seen by both, the last release lifts it."""
+    a, m = memfd_array(1 << 16)
+    h1 = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    h2 = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    assert h1 and h2 == h1
+    lib.mq_guard_release(h1)
+    assert lib.mq_guard_clean(h2, a.ctypes.data, a.nbytes) == 1  # still armed for owner 2
+    h3 = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)
+    assert h3 == h2
+    a[7] = -1
+    assert lib.mq_guard_clean(h2, a.ctypes.data, a.nbytes) == 0
+    assert lib.mq_guard_clean(h3, a.ctypes.data, a.nbytes) == 0
+    lib.mq_guard_release(h2)
+    lib.mq_guard_release(h3)
+    h4 = lib.mq_guard_arm(a.ctypes.data, a.nbytes, mq.MQ_GUARD_FILE)  # a fresh guard now
+    assert h4 and lib.mq_guard_clean(h4, a.ctypes.data, a.nbytes) == 1
+    lib.mq_guard_release(h4)
+    a[8] = -2  # writable after the last release
+    del a
+    m.close()
+
+
 def test_reorder_like_writes_from_c(lib):
     """A write from C code (memset, like reorder_column's memcpy) is seen too."""
     a, m = memfd_array(1 << 15)
