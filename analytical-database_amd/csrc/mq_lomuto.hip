@@ -18,8 +18,8 @@
 //
 // Two phases:
 //   * large ranges (more than `small` indexes) are partitioned level by level over
-//     items of kItem indexes aligned to kItem (a block per item, 8 consecutive
-//     indexes per lane): count "<" / ">" per item, one scan over the items, the
+//     items of kItem indexes aligned to kItem (a block per item, 8 indexes per lane):
+//     count "<" / ">" per item, one scan over the items, the
 //     children, J, and the placement. Only the indexes of large ranges are read; a
 //     pivot, a child of one index and an all-equal range go straight to the output;
 //     a child of 2..small indexes joins the small list. A chain longer than kChainCap
@@ -63,22 +63,6 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// exclusive prefix of x over the 256 lanes of the block (sh: 4 words of LDS)
-__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t* sh) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) sh[w] = inc;
-    __syncthreads();
-    uint32_t pre = 0;
-    for (int k = 0; k < w; k++) pre += sh[k];
-    return pre + inc - x;
-}
-
 // The range of an item and the first index of the item's aligned chunk.
 struct ItemAt {
     uint32_t r, base;
@@ -117,6 +101,37 @@ __device__ __forceinline__ void load8(const T* __restrict__ a, uint32_t i0, uint
     } else {
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = (i0 + k >= lo && i0 + k <= hi) ? a[i0 + k] : (T)0;
+    }
+}
+
+// The less-map and placement take an item's indexes round-major: index base + k * 256
+// + tid in round k, so a wave's lanes hold consecutive indexes in every round and the
+// swap chains of consecutive indexes read nearby J entries at each step (J is
+// monotone): at p = 1/2 a wave's first chain step touches ≈ 8 lines instead of ≈ 32
+// with 8 consecutive indexes per lane. rank[k] = r0 + the "<" indexes of the item
+// before this lane's round-k index.
+__device__ __forceinline__ void round_ranks(const bool (&lt)[8], uint32_t r0, uint32_t (&rank)[8],
+                                            uint32_t (*s_cnt)[kTPB / 64]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t m[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        m[k] = __ballot(lt[k]);
+        if (lane == 0) s_cnt[k][w] = (uint32_t)__popcll(m[k]);
+    }
+    __syncthreads();
+    uint32_t run = r0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kTPB / 64; w2++) {
+            const uint32_t c = s_cnt[k][w2];
+            before += w2 < w ? c : 0u;
+            tot += c;
+        }
+        rank[k] = run + before + lane_rank(m[k]);
+        run += tot;
     }
 }
 
@@ -215,25 +230,23 @@ __global__ __launch_bounds__(kTPB) void k_ld_less(const int32_t* __restrict__ V,
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
                                                   const uint32_t* __restrict__ segc,
                                                   const unsigned long long* __restrict__ ex, uint32_t* __restrict__ J) {
-    __shared__ uint32_t sh[4];
+    __shared__ uint32_t s_cnt[8][kTPB / 64];
     const uint32_t item = blockIdx.x;
     const ItemAt a = item_at(item, imap, seg, ioff);
     if (segc[a.r] == kEq) return;
-    const int32_t piv = V[a.g.hi];
-    const uint32_t i0 = a.base + threadIdx.x * 8;
-    int32_t v[8];
-    load8(V, i0, a.g.lo, a.g.hi, v);
-    uint32_t m = 0, nl = 0;
+    const uint32_t lo = a.g.lo, hi = a.g.hi;
+    const int32_t piv = V[hi];
+    bool lt[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const bool lt = i0 + k >= a.g.lo && i0 + k < a.g.hi && v[k] < piv;
-        m |= (uint32_t)lt << k;
-        nl += lt;
+        const uint32_t i = a.base + k * kTPB + threadIdx.x;
+        lt[k] = i >= lo && i < hi && V[i] < piv;
     }
-    uint32_t rank = block_exscan(nl, sh) + ((uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]]);
+    uint32_t rank[8];
+    round_ranks(lt, (uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]], rank, s_cnt);
 #pragma unroll
     for (int k = 0; k < 8; k++)
-        if (m >> k & 1) J[a.g.lo + rank++] = i0 + k;
+        if (lt[k]) J[lo + rank[k]] = a.base + k * kTPB + threadIdx.x;
 }
 
 // Placement of one item's indexes. Finals (the pivot, a child of one index, an
@@ -252,7 +265,7 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
                                                    unsigned long long* __restrict__ pout, uint32_t* __restrict__ segflag,
                                                    uint32_t* __restrict__ flist, unsigned int* __restrict__ nflag,
                                                    const uint32_t* __restrict__ foff, uint32_t F, int cap) {
-    __shared__ uint32_t sh[4];
+    __shared__ uint32_t s_cnt[8][kTPB / 64];
     uint32_t item;
     ItemAt a;
     if (USE_F) {
@@ -267,19 +280,23 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
     }
     const uint32_t lo = a.g.lo, hi = a.g.hi, c = segc[a.r];
     const int32_t piv = V[hi];
-    const uint32_t i0 = a.base + threadIdx.x * 8;
     int32_t v[8];
     uint32_t p[8];
-    load8(V, i0, lo, hi, v);
-    load8(P, i0, lo, hi, p);
-    uint32_t nl = 0;
+    bool lt[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) nl += c != kEq && i0 + k >= lo && i0 + k < hi && v[k] < piv;
-    uint32_t rank = block_exscan(nl, sh) + ((uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]]);
+    for (int k = 0; k < 8; k++) {
+        const uint32_t i = a.base + k * kTPB + threadIdx.x;
+        const bool ok = i >= lo && i <= hi;
+        v[k] = ok ? V[i] : 0;
+        p[k] = ok ? P[i] : 0u;
+        lt[k] = ok && c != kEq && i < hi && v[k] < piv;
+    }
+    uint32_t rank[8];
+    round_ranks(lt, (uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]], rank, s_cnt);
     uint32_t q[8], fin = 0, walk = 0, live = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + k;
+        const uint32_t i = a.base + k * kTPB + threadIdx.x;
         q[k] = i;
         if (i < lo || i > hi) continue;
         live |= 1u << k;
@@ -289,8 +306,8 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
         } else if (i == hi) {               // the pivot
             q[k] = lo + c;
             fin |= 1u << k;
-        } else if (v[k] < piv) {            // stable compaction of the "<" side
-            q[k] = lo + rank++;
+        } else if (lt[k]) {                 // stable compaction of the "<" side
+            q[k] = lo + rank[k];
             fin |= (uint32_t)(c == 1) << k;
         } else if (i - lo < c) {            // the >= side inside the "<" zone: follow the swaps
             walk |= 1u << k;
@@ -313,8 +330,8 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         if (!(live >> k & 1)) continue;
-        const uint32_t i = i0 + k;
-        if (c != kEq && i != hi && !(v[k] < piv)) {  // the >= side
+        const uint32_t i = a.base + k * kTPB + threadIdx.x;
+        if (c != kEq && i != hi && !lt[k]) {  // the >= side
             if (q[k] == lo + c) q[k] = hi;  // the final swap with the pivot
             if (rfin) fin |= 1u << k;
         }
