@@ -25,7 +25,8 @@
 //     a child of 2..small indexes joins the small list. A chain longer than kChainCap
 //     flags its range: J is pointer-doubled over that range's "<" zone and the range
 //     placed again.
-//   * each small range is finished by one wave with its values in LDS: the same
+//   * each small range is finished by one wave with its values in LDS (one buffer,
+//     updated in place from registers): the same
 //     partition with a ballot-ranked "<" side and chains walked in LDS, a stack of the
 //     sub-ranges above kTiny, and sub-ranges of 2..kTiny indexes run through the
 //     reference's own sequential partition by one lane each.
@@ -397,11 +398,14 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
                                                  const int32_t* __restrict__ V1, const uint32_t* __restrict__ P1,
                                                  const uint2* __restrict__ list, uint32_t count,
                                                  int32_t* __restrict__ vout, unsigned long long* __restrict__ pout) {
-    static_assert(T <= 4096 && T >= 64, "record packing");
-    __shared__ int32_t av[2][T];
-    __shared__ uint16_t ai[2][T];   // index within the range at the start (the row is read at the end)
+    static_assert(T <= 4096 && T >= 64 && T % 64 == 0, "record packing");
+    constexpr int R = T / 64;       // a sub-range's indexes per lane, held in registers while it moves
+    // One buffer, updated in place: a partition first reads its whole sub-range into
+    // registers, then writes every value to its destination (12 KB of LDS a wave at
+    // T = 1024 instead of 19 KB with two buffers: 13 waves per CU instead of 8).
+    __shared__ int32_t av[T];
+    __shared__ uint16_t ai[T];      // index within the range at the start (the row is read at the end)
     __shared__ uint16_t J[T];
-    __shared__ uint8_t where[T];    // the buffer holding position k's final value
     __shared__ uint32_t tiny[T / 2];
     __shared__ uint32_t stk[T / kTiny + 8];
     __shared__ uint16_t lstk[64][kTiny];
@@ -414,9 +418,8 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
         const uint32_t* Ps = b1 ? P1 : P0;
         const int m = (int)(hi - lo) + 1;
         for (int k = lane; k < m; k += 64) {
-            av[0][k] = Vs[lo + k];
-            ai[0][k] = (uint16_t)k;
-            where[k] = 0;
+            av[k] = Vs[lo + k];
+            ai[k] = (uint16_t)k;
         }
         int sp = 0, nt = 0;
         if (m > kTiny) {
@@ -429,14 +432,14 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
         __syncthreads();
         while (sp > 0) {
             const uint32_t t = stk[--sp];
-            const int l = t & 0xFFF, h = (t >> 12) & 0xFFF, s = t >> 24, d = s ^ 1;
-            const int32_t piv = av[s][h];
+            const int l = t & 0xFFF, h = (t >> 12) & 0xFFF;
+            const int32_t piv = av[h];
             uint32_t carry = 0;
             bool anygt = false;
             for (int base = l; base < h; base += 64) {
                 const int i = base + lane;
                 const bool ok = i < h;
-                const int32_t v = ok ? av[s][i] : 0;
+                const int32_t v = ok ? av[i] : 0;
                 const bool lt = ok && v < piv;
                 anygt |= ok && v > piv;
                 const uint64_t mk = __ballot(lt);
@@ -446,54 +449,54 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
             const int c = (int)carry;
             const bool eq = c == 0 && __ballot(anygt) == 0;
             const int rsz = h - l - c;  // the right child's size
-            __syncthreads();
-            carry = 0;
-            for (int base = l; base <= h; base += 64) {
-                const int i = base + lane;
-                const bool ok = i <= h;
-                int32_t v = 0;
-                uint16_t x = 0;
-                if (ok) {
-                    v = av[s][i];
-                    x = ai[s][i];
+            int32_t rv[R];
+            uint32_t rx[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                const int i = l + k * 64 + lane;
+                if (l + k * 64 <= h) {
+                    rv[k] = i <= h ? av[i] : 0;
+                    rx[k] = i <= h ? ai[i] : 0u;
                 }
-                const bool lt = !eq && ok && i != h && v < piv;
+            }
+            __syncthreads();  // J complete; every value of the sub-range read
+            carry = 0;
+#pragma unroll
+            for (int k = 0; k < R; k++) {
+                if (l + k * 64 > h) break;
+                const int i = l + k * 64 + lane;
+                const bool ok = i <= h;
+                const bool lt = !eq && ok && i != h && rv[k] < piv;
                 const uint64_t mk = __ballot(lt);
                 if (ok) {
                     int q;
-                    bool fin;
                     if (eq) {
                         q = i == h ? l : i + 1;
-                        fin = true;
                     } else if (i == h) {
                         q = l + c;
-                        fin = true;
                     } else if (lt) {
                         q = l + (int)(carry + lane_rank(mk));
-                        fin = c == 1;
                     } else {
                         q = i;
                         while (q - l < c) q = J[q];
                         if (q == l + c) q = h;
-                        fin = rsz == 1;
                     }
-                    av[d][q] = v;
-                    ai[d][q] = x;
-                    if (fin) where[q] = (uint8_t)d;
+                    av[q] = rv[k];
+                    ai[q] = (uint16_t)rx[k];
                 }
                 carry += (uint32_t)__popcll(mk);
             }
             if (!eq) {
-                // children in buffer d: the larger pushed first, so the stack stays shallow
+                // children: the larger pushed first, so the stack stays shallow
                 int cl[2] = {l, l + c + 1}, ch[2] = {l + c - 1, h}, cs[2] = {c, rsz};
                 const int big = cs[0] >= cs[1] ? 0 : 1;
                 for (int k = 0; k < 2; k++) {
                     const int j = k == 0 ? big : big ^ 1;
                     if (cs[j] > kTiny) {
-                        if (lane == 0) stk[sp] = rec(cl[j], ch[j], d);
+                        if (lane == 0) stk[sp] = rec(cl[j], ch[j], 0);
                         sp++;
                     } else if (cs[j] >= 2) {
-                        if (lane == 0) tiny[nt] = rec(cl[j], ch[j], d);
+                        if (lane == 0) tiny[nt] = rec(cl[j], ch[j], 0);
                         nt++;
                     }
                 }
@@ -503,47 +506,43 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
         // sub-ranges of 2..kTiny indexes: the reference's partition, one lane each, in place
         for (int tt = lane; tt < nt; tt += 64) {
             const uint32_t t = tiny[tt];
-            const int l0 = t & 0xFFF, h0 = (t >> 12) & 0xFFF, s = t >> 24;
-            int32_t* A = av[s];
-            uint16_t* X = ai[s];
+            const int l0 = t & 0xFFF, h0 = (t >> 12) & 0xFFF;
             uint16_t* st = lstk[lane];
             int top = 0;
             st[top++] = (uint16_t)(0 | (h0 - l0) << 8);
             while (top) {
                 const uint16_t w = st[--top];
                 const int lo2 = l0 + (w & 0xFF), hi2 = l0 + (w >> 8);
-                const int32_t piv = A[hi2];
+                const int32_t piv = av[hi2];
                 int i = lo2 - 1;
                 for (int j = lo2; j < hi2; j++) {
-                    if (A[j] < piv) {
+                    if (av[j] < piv) {
                         i++;
-                        const int32_t tv = A[i];
-                        A[i] = A[j];
-                        A[j] = tv;
-                        const uint16_t tx = X[i];
-                        X[i] = X[j];
-                        X[j] = tx;
+                        const int32_t tv = av[i];
+                        av[i] = av[j];
+                        av[j] = tv;
+                        const uint16_t tx = ai[i];
+                        ai[i] = ai[j];
+                        ai[j] = tx;
                     }
                 }
                 {
-                    const int32_t tv = A[i + 1];
-                    A[i + 1] = A[hi2];
-                    A[hi2] = tv;
-                    const uint16_t tx = X[i + 1];
-                    X[i + 1] = X[hi2];
-                    X[hi2] = tx;
+                    const int32_t tv = av[i + 1];
+                    av[i + 1] = av[hi2];
+                    av[hi2] = tv;
+                    const uint16_t tx = ai[i + 1];
+                    ai[i + 1] = ai[hi2];
+                    ai[hi2] = tx;
                 }
                 const int pv = i + 1;
                 if (pv - 1 > lo2) st[top++] = (uint16_t)((lo2 - l0) | (pv - 1 - l0) << 8);
                 if (hi2 > pv + 1) st[top++] = (uint16_t)((pv + 1 - l0) | (hi2 - l0) << 8);
             }
-            for (int k = l0; k <= h0; k++) where[k] = (uint8_t)s;
         }
         __syncthreads();
         for (int k = lane; k < m; k += 64) {
-            const int w = where[k];
-            if (vout) vout[lo + k] = av[w][k];
-            if (pout) pout[lo + k] = Ps[lo + ai[w][k]];
+            if (vout) vout[lo + k] = av[k];
+            if (pout) pout[lo + k] = Ps[lo + ai[k]];
         }
         __syncthreads();
     }
