@@ -7,3 +7,4 @@ tools/gpu_steps.sh \
   "120|r03/ld5_cap2k|env MQ_LQ_CAP=2048 python -u tools/lomuto_prof.py 27 3" \
   "120|r03/ld5_cap8k|env MQ_LQ_CAP=8192 python -u tools/lomuto_prof.py 27 3" \
   "120|r03/ld5_capinf|env MQ_LQ_CAP=1000000 python -u tools/lomuto_prof.py 27 3"
+bash tools/pmc_kernel.sh gpurun_out/r03/pmc_small k_ld_small python3 tools/lomuto_prof.py 27 1
