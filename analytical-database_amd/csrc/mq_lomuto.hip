@@ -19,17 +19,18 @@
 // Two phases:
 //   * large ranges (more than `small` indexes) are partitioned level by level over
 //     items of kItem indexes aligned to kItem (a block per item, 8 indexes per lane):
-//     count "<" / ">" per item, one scan over the items, the
-//     children, J, and the placement. Only the indexes of large ranges are read; a
-//     pivot, a child of one index and an all-equal range go straight to the output;
-//     a child of 2..small indexes joins the small list. A chain longer than kChainCap
-//     flags its range: J is pointer-doubled over that range's "<" zone and the range
-//     placed again.
+//     count "<" / ">" per item, one scan over the items, the children, the back map R
+//     (k_ld_less), and the placement, which pushes the "<" values and the pivot and
+//     pulls every index of the ">=" side by walking the chains backwards. Only the
+//     indexes of large ranges are read; a pivot, a child of one index and an all-equal
+//     range go straight to the output; a child of 2..small indexes joins the small
+//     list. A walk longer than kChainCap flags its range: R is pointer-doubled over
+//     that range and the range placed again.
 //   * each small range is finished by one wave with its values in LDS (one buffer,
-//     updated in place from registers): the same
-//     partition with a ballot-ranked "<" side and chains walked in LDS, a stack of the
-//     sub-ranges above kTiny, and sub-ranges of 2..kTiny indexes run through the
-//     reference's own sequential partition by one lane each.
+//     updated in place from registers): the same partition with a ballot-ranked "<"
+//     side and forward chains walked in LDS, a stack of the sub-ranges above kTiny, and
+//     sub-ranges of 2..kTiny indexes run through the reference's own sequential
+//     partition by one lane each.
 // Values and row ids move as (int32, u32) pairs; the host reads one small record per
 // level. DESIGN.md §3.7 has the cost.
 
@@ -52,7 +53,7 @@ constexpr uint32_t kItem = 2048;   // indexes per item: 256 lanes x 8
 constexpr uint32_t kEq = 0xFFFFFFFFu;
 
 // chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
-constexpr int kChainCap = 256;
+constexpr int kChainCap = 512;
 constexpr int kMaxJumps = 64;      // doubling steps per level (2^64 > any chain)
 constexpr int kJumpBatch = 4;      // doubling steps launched per host check
 
@@ -226,42 +227,90 @@ __global__ __launch_bounds__(kTPB) void k_ld_children(const LSeg* __restrict__ s
     }
 }
 
-// J[lo + rank] = index of the rank-th value below the pivot
+// The back map R of one level, per index x of a large range (the pivot excluded):
+// kGe for a value >= the pivot; for a "<" value, the index it was swapped with,
+// lo + rank(x) (the front of the ">=" block when x was reached), with kDone set when
+// that index holds a value >= the pivot. The value that ends at an index y of the
+// ">=" side is found by walking back from y: y -> R[y] -> ... until an index whose own
+// value is >= the pivot (it never moved before being swapped out, and each swap moves
+// the block's front). Walking back contracts (R[x] - lo ≈ p (x - lo)), so consecutive
+// indexes read nearby entries at every step, and every store of the placement goes to
+// consecutive indexes (the forward walk, from the ">=" values to their destinations,
+// expands: its loads and stores scattered).
+constexpr uint32_t kGe = 0xFFFFFFFFu, kDone = 0x80000000u;
+
+// blocked: a lane's 8 consecutive indexes (two 16-byte loads, two 16-byte stores);
+// the map has no chains, so the placement's round-major order buys nothing here
 __global__ __launch_bounds__(kTPB) void k_ld_less(const int32_t* __restrict__ V, const LSeg* __restrict__ seg,
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
                                                   const uint32_t* __restrict__ segc,
-                                                  const unsigned long long* __restrict__ ex, uint32_t* __restrict__ J) {
-    __shared__ uint32_t s_cnt[8][kTPB / 64];
+                                                  const unsigned long long* __restrict__ ex, uint32_t* __restrict__ R) {
+    __shared__ uint32_t sh[kTPB / 64];
     const uint32_t item = blockIdx.x;
     const ItemAt a = item_at(item, imap, seg, ioff);
     if (segc[a.r] == kEq) return;
     const uint32_t lo = a.g.lo, hi = a.g.hi;
     const int32_t piv = V[hi];
-    bool lt[8];
+    const uint32_t i0 = a.base + threadIdx.x * 8;
+    int32_t v[8];
+    load8(V, i0, lo, hi, v);
+    uint32_t m = 0, nl = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const uint32_t i = a.base + k * kTPB + threadIdx.x;
-        lt[k] = i >= lo && i < hi && V[i] < piv;
+        const bool lt = i0 + k >= lo && i0 + k < hi && v[k] < piv;
+        m |= (uint32_t)lt << k;
+        nl += lt;
     }
-    uint32_t rank[8];
-    round_ranks(lt, (uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]], rank, s_cnt);
+    // exclusive prefix of nl over the block's lanes
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = nl;
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-        if (lt[k]) J[lo + rank[k]] = a.base + k * kTPB + threadIdx.x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    uint32_t rank = inc - nl + ((uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]]);
+    for (int k = 0; k < w; k++) rank += sh[k];
+    uint32_t t[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        t[k] = lo + rank;
+        rank += m >> k & 1;
+    }
+    int32_t vt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) vt[k] = (m >> k & 1) ? V[t[k]] : 0;
+    uint32_t out[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) out[k] = (m >> k & 1) ? (t[k] | (vt[k] < piv ? 0u : kDone)) : kGe;
+    if (i0 >= lo && i0 + 7 < hi) {
+        *reinterpret_cast<uint4*>(R + i0) = make_uint4(out[0], out[1], out[2], out[3]);
+        *reinterpret_cast<uint4*>(R + i0 + 4) = make_uint4(out[4], out[5], out[6], out[7]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (i0 + k >= lo && i0 + k < hi) R[i0 + k] = out[k];
+    }
 }
 
-// Placement of one item's indexes. Finals (the pivot, a child of one index, an
-// all-equal range) go to the output, the rest to the other buffer. The lane's 8
-// chains are walked together (their loads in flight at once). USE_F = false: a chain
-// longer than cap flags its range (appended once to flist) and leaves the index to
-// the second placement; USE_F = true (after the doubling): block b places item b -
-// foff[k] of flagged range flist[k].
+// Placement of one item's indexes, as sources and as destinations:
+//  * a "<" value goes to lo + rank (stable compaction); the pivot to lo + c; an
+//    all-equal range in closed form (the last value first, then the others in order);
+//  * index y of the ">=" side [lo + c + 1, hi] takes the value found by walking back
+//    from y (from lo + c for y = hi: the final swap with the pivot).
+// Finals (the pivot, a child of one index, an all-equal range) go to the output, the
+// rest to the other buffer. A lane's 8 walks go together (loads in flight at once).
+// USE_F = false: a walk longer than cap flags its range (listed once in flist) and
+// leaves the index to the second placement; USE_F = true (after the doubling): block
+// b places item b - foff[k] of flagged range flist[k].
 template <bool USE_F>
 __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V, const uint32_t* __restrict__ P,
                                                    const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff,
                                                    const uint32_t* __restrict__ imap, const uint32_t* __restrict__ segc,
                                                    const unsigned long long* __restrict__ ex,
-                                                   const uint32_t* __restrict__ J, int32_t* __restrict__ Vd,
+                                                   const uint32_t* __restrict__ R, int32_t* __restrict__ Vd,
                                                    uint32_t* __restrict__ Pd, int32_t* __restrict__ vout,
                                                    unsigned long long* __restrict__ pout, uint32_t* __restrict__ segflag,
                                                    uint32_t* __restrict__ flist, unsigned int* __restrict__ nflag,
@@ -294,93 +343,125 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
     }
     uint32_t rank[8];
     round_ranks(lt, (uint32_t)ex[item] - (uint32_t)ex[ioff[a.r]], rank, s_cnt);
-    uint32_t q[8], fin = 0, walk = 0, live = 0;
+    const bool lfin = c == 1, rfin = c != kEq && hi - lo - c == 1;
+    // sources: "<" values, the pivot, all-equal ranges
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const uint32_t i = a.base + k * kTPB + threadIdx.x;
-        q[k] = i;
         if (i < lo || i > hi) continue;
-        live |= 1u << k;
-        if (c == kEq) {                     // all equal: last first, then in order
-            q[k] = i == hi ? lo : i + 1;
-            fin |= 1u << k;
-        } else if (i == hi) {               // the pivot
-            q[k] = lo + c;
-            fin |= 1u << k;
-        } else if (lt[k]) {                 // stable compaction of the "<" side
-            q[k] = lo + rank[k];
-            fin |= (uint32_t)(c == 1) << k;
-        } else if (i - lo < c) {            // the >= side inside the "<" zone: follow the swaps
-            walk |= 1u << k;
-        }
-    }
-    for (int steps = 0; walk; steps++) {
-        if (!USE_F && steps >= cap) break;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (walk >> k & 1) q[k] = J[q[k]];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if ((walk >> k & 1) && q[k] - lo >= c) walk &= ~(1u << k);
-    }
-    if (!USE_F && walk) {                   // long chains: placed after the doubling
-        live &= ~walk;
-        if (atomicExch(&segflag[a.r], 1u) == 0u) flist[atomicAdd(nflag, 1u)] = a.r;
-    }
-    const bool rfin = c != kEq && hi - lo - c == 1;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        if (!(live >> k & 1)) continue;
-        const uint32_t i = a.base + k * kTPB + threadIdx.x;
-        if (c != kEq && i != hi && !lt[k]) {  // the >= side
-            if (q[k] == lo + c) q[k] = hi;  // the final swap with the pivot
-            if (rfin) fin |= 1u << k;
-        }
-        if (fin >> k & 1) {
-            if (vout) vout[q[k]] = v[k];
-            if (pout) pout[q[k]] = p[k];
+        uint32_t q;
+        bool fin;
+        if (c == kEq) {
+            q = i == hi ? lo : i + 1;
+            fin = true;
+        } else if (i == hi) {
+            q = lo + c;
+            fin = true;
+        } else if (lt[k]) {
+            q = lo + rank[k];
+            fin = lfin;
         } else {
-            Vd[q[k]] = v[k];
-            Pd[q[k]] = p[k];
-        }
-    }
-}
-
-// flagged range k: items of its "<" zone (zi) and of the whole range (fi); entry F is 0
-__global__ __launch_bounds__(kTPB) void k_ld_fitems(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
-                                                    const uint32_t* __restrict__ flist, uint32_t F,
-                                                    uint32_t* __restrict__ zi, uint32_t* __restrict__ fi) {
-    for (uint32_t k = blockIdx.x * kTPB + threadIdx.x; k <= F; k += gridDim.x * kTPB) {
-        if (k == F) {
-            zi[k] = fi[k] = 0;
             continue;
         }
-        const uint32_t r = flist[k];
-        const LSeg g = seg[r];
-        zi[k] = items_of(g.lo, g.lo + segc[r] - 1);
-        fi[k] = items_of(g.lo, g.hi);
+        if (fin) {
+            if (vout) vout[q] = v[k];
+            if (pout) pout[q] = p[k];
+        } else {
+            Vd[q] = v[k];
+            Pd[q] = p[k];
+        }
+    }
+    if (c == kEq) return;
+    // destinations: the ">=" side [lo + c + 1, hi], walked back
+    uint32_t x[8], r[8], walk = 0, dst = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t y = a.base + k * kTPB + threadIdx.x;
+        x[k] = y;
+        r[k] = kGe;
+        if (y < lo || y > hi || y - lo <= c) continue;
+        dst |= 1u << k;
+        if (y == hi) x[k] = lo + c;
+        if (y == hi || lt[k]) walk |= 1u << k;  // a ">=" value at y < hi stays
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (walk >> k & 1) r[k] = R[x[k]];
+    for (int steps = 0;; steps++) {
+        // r[k]: the back map at x[k]; kGe: x[k] holds its own value; kDone: the next index does
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (!(walk >> k & 1)) continue;
+            if (r[k] == kGe) {
+                walk &= ~(1u << k);
+            } else {
+                x[k] = r[k] & ~kDone;
+                if (r[k] & kDone) walk &= ~(1u << k);
+            }
+        }
+        if (!walk || (!USE_F && steps >= cap)) break;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (walk >> k & 1) r[k] = R[x[k]];
+    }
+    if (!USE_F && walk) {  // long walks: placed after the doubling
+        dst &= ~walk;
+        if (atomicExch(&segflag[a.r], 1u) == 0u) flist[atomicAdd(nflag, 1u)] = a.r;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (!(dst >> k & 1)) continue;
+        const uint32_t y = a.base + k * kTPB + threadIdx.x;
+        const bool own = x[k] == y;
+        const int32_t val = own ? v[k] : V[x[k]];
+        const uint32_t row = own ? p[k] : P[x[k]];
+        if (rfin) {
+            if (vout) vout[y] = val;
+            if (pout) pout[y] = row;
+        } else {
+            Vd[y] = val;
+            Pd[y] = row;
+        }
     }
 }
 
-// Doubling step `it` of J over the "<" zone [lo, lo + c) of the flagged ranges: block b
-// takes chunk b - zoff[k] of range flist[k]'s zone. chg[it] records a change; a step
-// whose predecessor changed nothing returns at once, so the host launches steps in
-// batches and reads one flag per batch.
-__global__ __launch_bounds__(kTPB) void k_ld_jump(const LSeg* __restrict__ seg, const uint32_t* __restrict__ segc,
-                                                  const uint32_t* __restrict__ flist, const uint32_t* __restrict__ zoff,
-                                                  uint32_t F, uint32_t* J, unsigned int* __restrict__ chg, int it) {
+// flagged range k: its items (fi); entry F is 0
+__global__ __launch_bounds__(kTPB) void k_ld_fitems(const LSeg* __restrict__ seg, const uint32_t* __restrict__ flist,
+                                                    uint32_t F, uint32_t* __restrict__ fi) {
+    for (uint32_t k = blockIdx.x * kTPB + threadIdx.x; k <= F; k += gridDim.x * kTPB)
+        fi[k] = k == F ? 0u : items_of(seg[flist[k]].lo, seg[flist[k]].hi);
+}
+
+// Doubling step `it` of the back map R over the flagged ranges: block b takes item
+// b - foff[k] of range flist[k]; an entry not yet at a ">=" index takes its target's
+// entry. chg[it] records a change; a step whose predecessor changed nothing returns
+// at once, so the host launches steps in batches and reads one flag per batch.
+__global__ __launch_bounds__(kTPB) void k_ld_jump(const LSeg* __restrict__ seg, const uint32_t* __restrict__ flist,
+                                                  const uint32_t* __restrict__ foff, uint32_t F, uint32_t* R,
+                                                  unsigned int* __restrict__ chg, int it) {
     if (it > 0 && chg[it - 1] == 0u) return;
     unsigned int* changed = chg + it;
-    const uint32_t k = upper_index(zoff, F, blockIdx.x);
-    const uint32_t r = flist[k];
-    const uint32_t lo = seg[r].lo, c = segc[r];
-    const uint32_t base = (lo / kItem + (blockIdx.x - zoff[k])) * kItem;
-    const uint32_t b = max(base, lo), e = min(base + kItem, lo + c);
+    const uint32_t k = upper_index(foff, F, blockIdx.x);
+    const LSeg g = seg[flist[k]];
+    const uint32_t base = (g.lo / kItem + (blockIdx.x - foff[k])) * kItem;
+    // a lane's 8 entries are loaded, then their 8 targets, then stored: two round
+    // trips per step, not two per entry
+    uint32_t t[8];
+    bool act[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t i = base + k * kTPB + threadIdx.x;
+        t[k] = i >= g.lo && i < g.hi ? R[i] : kGe;
+        act[k] = t[k] != kGe && !(t[k] & kDone);  // t holds a "<" value: a pointer
+    }
+    uint32_t u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = act[k] ? R[t[k]] : 0u;
     unsigned int any = 0;
-    for (uint32_t i = b + threadIdx.x; i < e; i += kTPB) {
-        const uint32_t f = J[i];
-        if (f != i && f - lo < c) {
-            J[i] = J[f];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (act[k] && u[k] != t[k]) {
+            R[base + k * kTPB + threadIdx.x] = u[k];
             any = 1;
         }
     }
@@ -617,14 +698,13 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     LdBufs b;
     int32_t* V[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
     uint32_t* P[2] = {b.get<uint32_t>(n), b.get<uint32_t>(n)};
-    uint32_t* J = b.get<uint32_t>(n);
+    uint32_t* R = b.get<uint32_t>(n);  // the back map of the current level
     LSeg* seg[2] = {b.get<LSeg>(smax), b.get<LSeg>(smax)};
     uint32_t* ioff[2] = {b.get<uint32_t>(smax), b.get<uint32_t>(smax)};
     uint32_t* segc = b.get<uint32_t>(smax);
     uint32_t* segflag = b.get<uint32_t>(smax);  // ranges with a long chain, listed once in flist
     uint32_t* flist = b.get<uint32_t>(smax);
-    uint32_t* zi = b.get<uint32_t>(smax + 1);    // per flagged range: items of its zone, of the range
-    uint32_t* fi = b.get<uint32_t>(smax + 1);
+    uint32_t* fi = b.get<uint32_t>(smax + 1);    // per flagged range: its items, then their prefix
     uint32_t* imap = b.get<uint32_t>(nimax);
     unsigned long long* cnt = b.get<unsigned long long>(nimax + 1);
     unsigned long long* scratch = b.get<unsigned long long>(scan_u32_scratch_elems(nimax + 1));
@@ -669,10 +749,10 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
                            (uint32_t)S, cnt, T, (uint32_t)d, segc, segflag, seg[d], ioff[d], ctl, slist, ctl32);
         LAUNCHCHK("k_ld_children");
         hipLaunchKernelGGL(k_ld_less, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap, segc,
-                           cnt, J);
+                           cnt, R);
         LAUNCHCHK("k_ld_less");
         hipLaunchKernelGGL(k_ld_final<false>, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur],
-                           ioff[cur], imap, segc, cnt, J, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
+                           ioff[cur], imap, segc, cnt, R, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
                            (const uint32_t*)nullptr, 0u, cap);
         LAUNCHCHK("k_ld_final");
         unsigned long long h[2];
@@ -680,20 +760,17 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
         HIPCHK(hipStreamSynchronize(st));
         int jumps = 0;
         const uint32_t F = (uint32_t)(h[1] >> 32);
-        if (F) {  // chains longer than cap: double J over the flagged ranges' zones, then place them again
-            hipLaunchKernelGGL(k_ld_fitems, dim3(stream_grid(s, F + 1)), dim3(kTPB), 0, st, seg[cur], segc, flist, F,
-                               zi, fi);
+        if (F) {  // walks longer than cap: double R over the flagged ranges, then place them again
+            hipLaunchKernelGGL(k_ld_fitems, dim3(stream_grid(s, F + 1)), dim3(kTPB), 0, st, seg[cur], flist, F, fi);
             LAUNCHCHK("k_ld_fitems");
-            if ((rc = scan_u32_exclusive_u32(zi, zi, F + 1, scratch, st))) return rc;
             if ((rc = scan_u32_exclusive_u32(fi, fi, F + 1, scratch, st))) return rc;
-            uint32_t nz = 0, nf = 0;
-            HIPCHK(hipMemcpyAsync(&nz, zi + F, 4, hipMemcpyDeviceToHost, st));
+            uint32_t nf = 0;
             HIPCHK(hipMemcpyAsync(&nf, fi + F, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             for (;;) {
                 if (jumps >= kMaxJumps) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
                 for (int k = 0; k < kJumpBatch; k++, jumps++) {
-                    hipLaunchKernelGGL(k_ld_jump, dim3(nz), dim3(kTPB), 0, st, seg[cur], segc, flist, zi, F, J, chg, jumps);
+                    hipLaunchKernelGGL(k_ld_jump, dim3(nf), dim3(kTPB), 0, st, seg[cur], flist, fi, F, R, chg, jumps);
                     LAUNCHCHK("k_ld_jump");
                 }
                 unsigned int ch = 0;
@@ -702,7 +779,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
                 if (!ch) break;
             }
             hipLaunchKernelGGL(k_ld_final<true>, dim3(nf), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur], ioff[cur], imap,
-                               segc, cnt, J, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1, (const uint32_t*)fi, F,
+                               segc, cnt, R, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1, (const uint32_t*)fi, F,
                                0);
             LAUNCHCHK("k_ld_final");
         }
