@@ -648,7 +648,7 @@ int small_threshold() {
     static const int t = [] {
         const char* e = getenv("MQ_LQ_SMALL");
         const int v = e ? atoi(e) : 1024;
-        return v == 512 || v == 2048 ? v : 1024;
+        return v == 256 || v == 512 || v == 2048 ? v : 1024;
     }();
     return t;
 }
@@ -676,7 +676,9 @@ void launch_small_t(uint32_t grid, hipStream_t st, const int32_t* V0, const uint
 
 int launch_small(int T, uint32_t grid, hipStream_t st, const int32_t* V0, const uint32_t* P0, const int32_t* V1,
                  const uint32_t* P1, const uint2* list, uint32_t count, int32_t* vout, unsigned long long* pout) {
-    if (T == 512)
+    if (T == 256)
+        launch_small_t<256>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
+    else if (T == 512)
         launch_small_t<512>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
     else if (T == 2048)
         launch_small_t<2048>(grid, st, V0, P0, V1, P1, list, count, vout, pout);
