@@ -47,8 +47,12 @@ int scan_u64_exclusive(const unsigned long long* in, unsigned long long* out, ui
 int radix_sort_pairs(const int* keys, const int* vals, uint64_t n, uint32_t** keys_out,
                      uint32_t** vals_out, hipStream_t st, const DevState* s);
 // The same sort of (col[i], i) written straight out as an index: values ascending
-// (int32, may be NULL) and positions (size_t rows, may be NULL). Synchronises.
+// (int32, may be NULL) and positions (size_t rows, may be NULL), equal values in
+// ascending row order. Synchronises. Picks the form by the key range (mq_isort.hip).
 int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* positions, hipStream_t st);
+// Its LSD form (mq_join.hip): npass 8-bit digits of (col ^ 2^31) - kmin.
+int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, int32_t* values, uint64_t* positions,
+                         hipStream_t st);
 
 // Frees the calling thread's pinned upload staging of shared_select (mq_shared.hip).
 void shared_staging_release();

@@ -175,8 +175,8 @@ __device__ __forceinline__ u64 sort_word(const int* c1, const int* p1, const u64
 
 template <bool FIRST, int TPB, int IT>
 __global__ __launch_bounds__(TPB) void k_sortw_hist(const int* __restrict__ c1, const u64* __restrict__ in,
-                                                    uint64_t n, int shift, uint32_t* __restrict__ hist,
-                                                    uint32_t ntiles) {
+                                                    uint64_t n, int shift, uint32_t kmin,
+                                                    uint32_t* __restrict__ hist, uint32_t ntiles) {
     constexpr uint32_t kTile = TPB * IT;
     __shared__ uint32_t h[kRadix];
     if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
@@ -191,8 +191,8 @@ __global__ __launch_bounds__(TPB) void k_sortw_hist(const int* __restrict__ c1, 
     for (int k = 0; k < IT; k++) {
         const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
         const uint64_t ic = i < n ? i : n - 1;
-        key[k] = FIRST ? ((uint32_t)__builtin_nontemporal_load(c1 + ic) ^ 0x80000000u)
-                       : (uint32_t)__builtin_nontemporal_load(in + ic);
+        key[k] = (FIRST ? ((uint32_t)__builtin_nontemporal_load(c1 + ic) ^ 0x80000000u)
+                        : (uint32_t)__builtin_nontemporal_load(in + ic)) - kmin;
     }
 #pragma unroll
     for (int k = 0; k < IT; k++)
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(TPB) void k_sortw_hist_bytes(const uint8_t* __restr
 template <bool FIRST, int LAST, int TPB, int IT>
 __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
                                                         const u64* __restrict__ in, uint64_t n, int shift,
-                                                        const u64* __restrict__ goff, uint32_t ntiles,
+                                                        uint32_t kmin, const u64* __restrict__ goff, uint32_t ntiles,
                                                         u64* __restrict__ out, uint32_t* __restrict__ kout,
                                                         uint32_t* __restrict__ vout, u64* __restrict__ pout,
                                                         uint8_t* __restrict__ dig) {
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
     for (int k = 0; k < IT; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool valid = i < n;
-        const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
+        const uint32_t d = (((uint32_t)el[k] - kmin) >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
         const uint32_t cur = wcnt[wave][d];
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
         const uint32_t e = (uint32_t)(k * TPB + tid);
         if (e < tn) {
             const u64 v = stage[e];
-            const uint32_t d = ((uint32_t)v >> shift) & 0xFF;
+            const uint32_t d = (((uint32_t)v - kmin) >> shift) & 0xFF;
             const u64 dst = gofs[d] + (e - loff[d]);
             if constexpr (LAST == 1) {
                 kout[dst] = (uint32_t)v;
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
                 if (pout) pout[dst] = v >> 32;
             } else {
                 out[dst] = v;
-                if (dig) dig[dst] = (uint8_t)((uint32_t)v >> (shift + 8));  // the next pass's digit
+                if (dig) dig[dst] = (uint8_t)(((uint32_t)v - kmin) >> (shift + 8));  // the next pass's digit
             }
         }
     }
@@ -1622,8 +1622,8 @@ int radix_sort_onesweep(const int* c1, const int* p1, uint64_t n, int mode, uint
 }
 
 template <int TPB, int IT>
-int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
-                     u64* pout, hipStream_t st);
+int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t kmin, int npass, uint32_t* kout,
+                     uint32_t* vout, u64* pout, hipStream_t st);
 
 int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
                    u64* pout, hipStream_t st) {
@@ -1642,12 +1642,14 @@ int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t*
     // tiles of 512 x 16 words: 18.7 ms for the 1e9-row index, against 21.6 with
     // 256 x 16 (digit runs of 16 words leave the block as 128-B pieces), 25.9 with
     // 1024 x 8 and 22.3 with 512 x 8 (tools/sorttpb_cmd.sh)
-    return radix_sort_tiles<kSortTPB, kSortItems>(c1, p1, n, mode, kout, vout, pout, st);
+    return radix_sort_tiles<kSortTPB, kSortItems>(c1, p1, n, mode, 0, 4, kout, vout, pout, st);
 }
 
+// npass 8-bit digits of (key ^ 2^31) - kmin, lowest first (1 <= npass <= 4): a key
+// range of at most 8 * npass bits sorts in npass passes.
 template <int TPB, int IT>
-int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
-                     u64* pout, hipStream_t st) {
+int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t kmin, int npass, uint32_t* kout,
+                     uint32_t* vout, u64* pout, hipStream_t st) {
     constexpr uint64_t kTile = (uint64_t)TPB * IT;
     u64 *w0 = nullptr, *w1 = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t* hist = nullptr;
@@ -1663,9 +1665,10 @@ int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_
         pool_free(dig);
         return rc;
     };
+    if (npass < 1 || npass > 4) return set_err(MQ_EINVAL, "sort: %d passes", npass);
     w0 = (u64*)pool_alloc(n * 8);
     const char* de = getenv("MQ_SORT_DIGITS");
-    const bool use_dig = !(de && de[0] == '0');
+    const bool use_dig = npass > 1 && !(de && de[0] == '0');
     if (use_dig) dig = (uint8_t*)pool_alloc(n + 16);
     w1 = (u64*)pool_alloc(n * 8);
     hist = (uint32_t*)pool_alloc(nh * 4);
@@ -1674,29 +1677,37 @@ int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_
     if (!w0 || !w1 || !hist || !hscan || !scratch || (use_dig && !dig))
         return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
     const dim3 g((uint32_t)ntiles), b(TPB);
-    for (int pass = 0; pass < 4; pass++) {
+    const uint32_t nt = (uint32_t)ntiles;
+    for (int pass = 0; pass < npass; pass++) {
         const int shift = 8 * pass;
-        if (pass == 0)
-            hipLaunchKernelGGL((k_sortw_hist<true, TPB, IT>), g, b, 0, st, c1, nullptr, n, shift, hist, (uint32_t)ntiles);
+        const bool first = pass == 0, last = pass == npass - 1;
+        uint8_t* dnext = last ? nullptr : dig;
+        if (first)
+            hipLaunchKernelGGL((k_sortw_hist<true, TPB, IT>), g, b, 0, st, c1, nullptr, n, shift, kmin, hist, nt);
         else if (use_dig)
-            hipLaunchKernelGGL((k_sortw_hist_bytes<TPB, IT>), g, b, 0, st, dig, n, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL((k_sortw_hist_bytes<TPB, IT>), g, b, 0, st, dig, n, hist, nt);
         else
-            hipLaunchKernelGGL((k_sortw_hist<false, TPB, IT>), g, b, 0, st, nullptr, w0, n, shift, hist, (uint32_t)ntiles);
+            hipLaunchKernelGGL((k_sortw_hist<false, TPB, IT>), g, b, 0, st, nullptr, w0, n, shift, kmin, hist, nt);
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return done(rc);
-        const uint32_t nt = (uint32_t)ntiles;
-        if (pass == 0)
-            hipLaunchKernelGGL((k_sortw_scatter<true, 0, TPB, IT>), g, b, 0, st, c1, p1, nullptr, n, shift, hscan, nt, w1,
-                               nullptr, nullptr, nullptr, dig);
-        else if (pass < 3)
-            hipLaunchKernelGGL((k_sortw_scatter<false, 0, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
-                               nt, w1, nullptr, nullptr, nullptr, dig);
-        else if (mode == 1)
-            hipLaunchKernelGGL((k_sortw_scatter<false, 1, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+        if (first && !last)
+            hipLaunchKernelGGL((k_sortw_scatter<true, 0, TPB, IT>), g, b, 0, st, c1, p1, nullptr, n, shift, kmin, hscan,
+                               nt, w1, nullptr, nullptr, nullptr, dnext);
+        else if (!last)
+            hipLaunchKernelGGL((k_sortw_scatter<false, 0, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, kmin,
+                               hscan, nt, w1, nullptr, nullptr, nullptr, dnext);
+        else if (mode == 1 && first)
+            hipLaunchKernelGGL((k_sortw_scatter<true, 1, TPB, IT>), g, b, 0, st, c1, p1, nullptr, n, shift, kmin, hscan,
                                nt, nullptr, kout, vout, nullptr, nullptr);
-        else
-            hipLaunchKernelGGL((k_sortw_scatter<false, 2, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, hscan,
+        else if (mode == 1)
+            hipLaunchKernelGGL((k_sortw_scatter<false, 1, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, kmin,
+                               hscan, nt, nullptr, kout, vout, nullptr, nullptr);
+        else if (first)
+            hipLaunchKernelGGL((k_sortw_scatter<true, 2, TPB, IT>), g, b, 0, st, c1, p1, nullptr, n, shift, kmin, hscan,
                                nt, nullptr, kout, nullptr, pout, nullptr);
+        else
+            hipLaunchKernelGGL((k_sortw_scatter<false, 2, TPB, IT>), g, b, 0, st, nullptr, nullptr, w0, n, shift, kmin,
+                               hscan, nt, nullptr, kout, nullptr, pout, nullptr);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "sort: launch"));
         u64* t = w0;
         w0 = w1;
@@ -1728,9 +1739,11 @@ int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_o
     return MQ_OK;
 }
 
-int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* positions, hipStream_t st) {
-    return n ? radix_sort_run(col, nullptr, n, 2, reinterpret_cast<uint32_t*>(values), nullptr,
-                              reinterpret_cast<u64*>(positions), st)
+int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, int32_t* values, uint64_t* positions,
+                         hipStream_t st) {
+    return n ? radix_sort_tiles<kSortTPB, kSortItems>(col, nullptr, n, 2, kmin, npass,
+                                                      reinterpret_cast<uint32_t*>(values), nullptr,
+                                                      reinterpret_cast<u64*>(positions), st)
              : MQ_OK;
 }
 

@@ -46,6 +46,43 @@ def test_index_build_vs_oracle(lib, refcpu, n, lo, hi):
     assert np.array_equal(v, wv) and np.array_equal(p, wp)
 
 
+def _wide_range_inputs():
+    """Columns that take radix_sort_index's MSD form (n >= 2^22 rows, key range over
+    24 bits, csrc/mq_isort.hip) or its shortened LSD form, with the shapes that steer
+    the MSD levels: ranges split twice or three times, finisher ranges of one key
+    (copied out in row order), ranges above the LDS capacity with no key bits left,
+    one or two LDS passes, a nonzero range minimum."""
+    rng = np.random.default_rng(77)
+    n = (1 << 22) + 17
+    yield "full_int32_4M", rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype(np.int32)
+    yield "b25_5M", rng.integers(0, 1 << 25, 5_000_000).astype(np.int32)
+    yield "b30_offset_6M", (rng.integers(0, 1 << 30, 6_000_000) - 123_456_789).astype(np.int32)
+    c = rng.integers(0, 1 << 30, n).astype(np.int32)
+    c[rng.random(n) < 0.5] = 7  # one key holds half the rows: a finisher range far above kCap
+    yield "half_one_value_4M", c
+    c = (rng.integers(0, 1 << 22, n) << 8).astype(np.int32)  # low 8 bits zero: ties everywhere
+    yield "low_bits_zero_4M", c
+    c = rng.integers(0, 1 << 30, n).astype(np.int32)
+    c[: n // 4] = rng.integers(0, 1 << 12, n // 4)  # a dense corner: ranges split three levels
+    yield "skewed_corner_4M", c
+    yield "b23_lsd3_4M", (rng.integers(0, 1 << 23, n) + 10**9).astype(np.int32)
+    yield "b8_lsd1_4M", (rng.integers(0, 200, n) - 100).astype(np.int32)
+    yield "sorted_desc_4M", np.arange(n, 0, -1, dtype=np.int64).astype(np.int32) * 64
+
+
+@pytest.mark.parametrize("form", ["default", "msd"])
+@pytest.mark.parametrize("name,col", list(_wide_range_inputs()), ids=lambda x: x if isinstance(x, str) else "")
+def test_index_build_wide_range_vs_oracle(lib, refcpu, name, col, form, monkeypatch):
+    """form "msd": MQ_INDEX_MSD_MIN=0 takes the MSD form at these sizes too (by default
+    it starts at 2^24 rows)."""
+    if form == "msd":
+        monkeypatch.setenv("MQ_INDEX_MSD_MIN", "0")
+    v, p = gpu_index(lib, col)
+    wv, wp = refcpu.index_build(col)
+    assert np.array_equal(v, wv), name
+    assert np.array_equal(p, wp), name
+
+
 def gpu_lomuto(L, col: np.ndarray):
     n = len(col)
     d = Dev.of(col.astype(np.int32)) if n else Dev(4)
