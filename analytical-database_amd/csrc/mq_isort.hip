@@ -273,23 +273,28 @@ __device__ __forceinline__ void emit(int32_t* vout, u64* pout, u64 i, u64 v) {
 }
 
 
+// Cell words (two u16 cells each) a range of keys below 2^s needs, rounded up so
+// that every wave of the block scans a whole number of words per lane.
+__device__ __forceinline__ uint32_t count_words(int s) {
+    const uint32_t nw = (1u << s) / 2;
+    return nw < (uint32_t)kFT ? (uint32_t)kFT : nw;
+}
+
 // The counting finisher of one range (keys x = k - kbase below 2^s, s <= kCountBits),
 // el[] in round-major order (element k * kFT + tid). c32: a u16 cell per key, two to
-// a word (counts, then, after the scan, running slots); rows / keys: the placed row
-// ids and keys by slot. A row takes its slot by one atomic on its key's cell; the
-// rows of a key are then put back in ascending order (they arrive in any order), and
-// values and positions leave slot by slot. Returns false, having written nothing
-// outside LDS, when some key holds more than kTieMax rows.
+// a word, zeroed by the caller (counts, then, after the scan, running slots relative
+// to the scanning wave's start); rows / keys: the placed row ids and keys by slot. A
+// row takes its slot by one atomic on its key's cell; the rows of a key are then put
+// back in ascending order (they arrive in any order), and values and positions leave
+// slot by slot, while the range's cell words are zeroed again for the next range.
+// Returns false, having written nothing outside LDS, when some key holds more than
+// kTieMax rows (the cells are then left for the caller to zero).
 __device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t len, uint32_t kbase, int s,
                                                 uint32_t* c32, uint32_t* rows, uint16_t* keys, uint32_t* wsum,
-                                                uint32_t* flag, int32_t* vout, u64* pout) {
+                                                int32_t* vout, u64* pout) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kFT / 64;
-    const uint32_t nk = 1u << s;
-    const uint32_t nw = nk / 2 < (uint32_t)kFT ? (uint32_t)kFT : nk / 2;  // cell words scanned: whole waves
-    for (uint32_t x = tid; x < nw; x += kFT) c32[x] = 0;
-    if (tid == 0) *flag = 0;
-    __syncthreads();
+    const uint32_t nw = count_words(s);
 #pragma unroll
     for (int k = 0; k < kFI; k++)
         if ((uint32_t)k * kFT + tid < len) {
@@ -297,63 +302,77 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t l
             atomicAdd(&c32[x >> 1], 1u << (16 * (x & 1)));
         }
     __syncthreads();
-    // each wave scans nw / 16 consecutive words, 64 at a time
-    const uint32_t per = nw / kW, it = per / 64;
-    uint32_t run = 0, mx = 0;
-    for (uint32_t j = 0; j < it; j++) {
-        const uint32_t w = wave * per + j * 64 + lane;
-        const uint32_t cell = c32[w], lo = cell & 0xFFFFu, hi = cell >> 16;
+    // each lane scans q consecutive words (wave w: words [w * nw / 16, (w + 1) * nw / 16))
+    const uint32_t per = nw / kW, q = per / 64, lgper = 31 - __builtin_clz(per);
+    uint32_t* mine = c32 + wave * per + lane * q;
+    uint32_t tot = 0, mx = 0;
+    for (uint32_t j = 0; j < q; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu, hi = cell >> 16;
         mx = lo > mx ? lo : mx;
         mx = hi > mx ? hi : mx;
-        const uint32_t c = lo + hi;
-        uint32_t incl = c;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        const uint32_t ex = run + incl - c;  // the wave's own exclusive prefix for now
-        c32[w] = ex | ((ex + lo) << 16);
-        run += __shfl(incl, 63, 64);
+        tot += lo + hi;
     }
-    if (lane == 0) wsum[wave] = run;
-    if (mx > kTieMax) *flag = 1;  // benign race: any writer stores 1
-    __syncthreads();
-    if (*flag) return false;
-    uint32_t woff = 0;
-    for (int w = 0; w < wave; w++) woff += wsum[w];
-    if (woff)
-        for (uint32_t j = 0; j < it; j++) c32[wave * per + j * 64 + lane] += woff | (woff << 16);
-    __syncthreads();
+    uint32_t incl = tot;
 #pragma unroll
-    for (int k = 0; k < kFI; k++)
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    uint32_t run = incl - tot;  // slots before this lane's words, within the wave
+    for (uint32_t j = 0; j < q; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu;
+        mine[j] = run | ((run + lo) << 16);
+        run += lo + (cell >> 16);
+    }
+    if (lane == 63) wsum[wave] = incl;
+    if (__ballot(mx > kTieMax)) wsum[kW] = 1;  // benign race: any writer stores 1
+    __syncthreads();
+    if (wsum[kW]) return false;
+    // the slots before each wave's words: lane w of every wave holds those of wave w
+    uint32_t wpre = lane < kW ? wsum[lane] : 0u;
+#pragma unroll
+    for (int off = 1; off < kW; off <<= 1) {
+        const uint32_t y = __shfl_up(wpre, off, 64);
+        if (lane >= off) wpre += y;
+    }
+    wpre = __shfl_up(wpre, 1, 64);
+    wpre = lane ? wpre : 0u;
+#pragma unroll
+    for (int k = 0; k < kFI; k++) {
+        const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
+        const uint32_t base = __shfl(wpre, (x >> 1) >> lgper, 64);
         if ((uint32_t)k * kFT + tid < len) {
-            const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
-            const uint32_t slot = (atomicAdd(&c32[x >> 1], 1u << sh) >> sh) & 0xFFFFu;
+            const uint32_t slot = ((atomicAdd(&c32[x >> 1], 1u << sh) >> sh) & 0xFFFFu) + base;
             rows[slot] = (uint32_t)(el[k] >> 32);
             keys[slot] = (uint16_t)x;
         }
-    __syncthreads();
-    // the cell of x now holds the end of its slots, the cell of x - 1 their start
-    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
-    for (uint32_t x = tid; x < nk; x += kFT) {
-        const uint32_t e1 = c16[x], e0 = x ? c16[x - 1] : 0u;
-        for (uint32_t i = e0 + 1; i < e1; i++) {
-            const uint32_t r = rows[i];
-            uint32_t j = i;
-            for (; j > e0 && rows[j - 1] > r; j--) rows[j] = rows[j - 1];
-            rows[j] = r;
-        }
     }
     __syncthreads();
+    // the cell of x now holds the end of its slots, the cell of x - 1 their start. A
+    // row whose key holds other rows (they took their slots in any order) goes to the
+    // group's start + the number of the group's rows with a smaller id.
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
 #pragma unroll
     for (int k = 0; k < kFI; k++) {
         const uint32_t e = (uint32_t)k * kFT + tid;
+        const uint32_t ec = e < len ? e : len - 1;
+        const uint32_t x = keys[ec], r = rows[ec];
+        const bool tied = (ec > 0 && keys[ec - 1] == x) || (ec + 1 < len && keys[ec + 1] == x);
+        const uint32_t xp = x ? x - 1 : 0;
+        const uint32_t b0 = __shfl(wpre, (xp >> 1) >> lgper, 64);
+        uint32_t pos = ec;
+        if (tied) {
+            pos = x ? c16[xp] + b0 : 0u;
+            for (uint32_t j = pos; j < len && keys[j] == x; j++) pos += rows[j] < r;
+        }
         if (e < len) {
-            if (vout) vout[e] = (int32_t)((kbase + keys[e]) ^ 0x80000000u);
-            if (pout) pout[e] = rows[e];
+            if (vout) vout[e] = (int32_t)((kbase + x) ^ 0x80000000u);
+            if (pout) pout[pos] = r;
         }
     }
+    __syncthreads();
+    for (uint32_t x = tid; x < nw; x += kFT) c32[x] = 0;
+    if (tid == 0) wsum[kW] = 0;
     return true;
 }
 
@@ -369,8 +388,7 @@ __global__ __launch_bounds__(kFT) void k_msd_finish_count(const u64* __restrict_
     __shared__ uint32_t c32[kCap / 2];  // u16 cells of 2^14 keys
     __shared__ uint32_t rows[kCap];
     __shared__ uint16_t keys[kCap];
-    __shared__ uint32_t wsum[kW];
-    __shared__ uint32_t flag;
+    __shared__ uint32_t wsum[kW + 1];  // wave totals, then the fallback flag
     const int tid = threadIdx.x;
     u64 nx[kFI];
     auto prefetch = [&](uint32_t fi) {  // the words of range fi, if the counting path sorts it
@@ -383,24 +401,33 @@ __global__ __launch_bounds__(kFT) void k_msd_finish_count(const u64* __restrict_
             nx[k] = src[i < f.len ? i : f.len - 1];
         }
     };
-    if (blockIdx.x < nfin) prefetch(blockIdx.x);
+    if (blockIdx.x >= nfin) return;
+    prefetch(blockIdx.x);
+    for (uint32_t x = tid; x < kCap / 2; x += kFT) c32[x] = 0;
+    if (tid == 0) wsum[kW] = 0;
+    __syncthreads();
     for (uint32_t fi = blockIdx.x; fi < nfin; fi += gridDim.x) {
         const Fin f = fins[fi];
         const int s = (int)(f.meta & 0xFF);
         const u64* src = ((f.meta >> 8) ? w1 : w0) + f.start;
         int32_t* vo = vout ? vout + f.start : nullptr;
         u64* po = pout ? pout + f.start : nullptr;
-        if (s == 0) {  // one key (or one row): already in row order
+        const uint32_t nxt = fi + gridDim.x;
+        if (s == 0) {  // one key (or one row): already in row order; the cells stay zero
             for (uint32_t e = tid; e < f.len; e += kFT) emit(vo, po, e, src[e]);
-            if (fi + gridDim.x < nfin) prefetch(fi + gridDim.x);
+            if (nxt < nfin) prefetch(nxt);
             continue;
         }
         u64 el[kFI];
 #pragma unroll
         for (int k = 0; k < kFI; k++) el[k] = nx[k];
-        if (fi + gridDim.x < nfin) prefetch(fi + gridDim.x);
-        if (!finish_counting(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, &flag, vo, po) && tid == 0)
-            fb[atomicAdd(&ctr->nfb, 1u)] = f;
+        if (nxt < nfin) prefetch(nxt);
+        if (!finish_counting(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po)) {
+            if (tid == 0) fb[atomicAdd(&ctr->nfb, 1u)] = f;
+            __syncthreads();
+            for (uint32_t x = tid; x < kCap / 2; x += kFT) c32[x] = 0;
+            if (tid == 0) wsum[kW] = 0;
+        }
         __syncthreads();  // LDS is reused by the next range
     }
 }

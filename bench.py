@@ -1060,7 +1060,8 @@ def exact_index_leg(lib, mq, torch, dev, stream, logn: int = 27) -> dict:
 
 def index_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
     """the sorted index of the 1e9-row column (mq_index_build:
-    stable radix sort of (value, row) -> values + size_t positions). Parity: gather
+    stable radix sort of (value, row) -> values + size_t positions; MSD levels and an
+    LDS finisher at this size, csrc/mq_isort.hip). Parity: gather
     through the positions reproduces the values (and they ascend). CPU: the
     reference's quicksort (index.c:25-46, libdbm.so) on 1e6 rows of the same column."""
     import numpy as np
@@ -1075,10 +1076,12 @@ def index_leg(lib, mq, torch, dev, stream, col, n, cpu: bool = True) -> dict:
         ok = bool(torch.equal(g, v)) and bool((v[1:] >= v[:-1]).all())
         del v, p, g
     res = {"rows": n, "ms": ms, "rows_per_s": n / (ms * 1e-3), "parity": ok,
-           "hbm_bytes_design": 4 * 20 * n,
-           "path": "mq_index_build: the stable radix sort alone (equal values in ascending row order)",
-           "note": "4 LSD passes of 8 bits: histogram (4N read) + scatter (8N read + 8N write) each, "
-                   "+ key flip and emit"}
+           "hbm_bytes_design": 58 * n,
+           "path": "mq_index_build: the stable radix sort alone (equal values in ascending row order); "
+                   "its MSD form (csrc/mq_isort.hip) at this size and key range",
+           "note": "min/max (4N), two MSD levels of 256 range-proportional digits (histogram 4N / 1N, "
+                   "scatter 4N+9N / 8N+8N), LDS counting finisher (8N read, 12N written) = 58 B a row; "
+                   "the 4-pass LSD form (MQ_INDEX_SORT=lsd4) moves 74"}
     res["exact_2e27"] = exact_index_leg(lib, mq, torch, dev, stream)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refload  # the reference's quicksort, baseline only
