@@ -273,36 +273,44 @@ __device__ __forceinline__ void emit(int32_t* vout, u64* pout, u64 i, u64 v) {
 }
 
 
-// Cell words (two u16 cells each) a range of keys below 2^s needs, rounded up so
-// that every wave of the block scans a whole number of words per lane.
+// The counting finisher runs as T threads x I rows (T * I = kCap). BF: guards without
+// branches (a lane past the range's end counts into a dummy cell word and places into
+// a dummy slot): per-row `if`s cost ≈ 12 scalar instructions each for the exec mask,
+// and scalar issue bound the 1024 x 16 form; at 1024 x 16 the branch-free form spills.
+template <int T>
 __device__ __forceinline__ uint32_t count_words(int s) {
-    const uint32_t nw = (1u << s) / 2;
-    return nw < (uint32_t)kFT ? (uint32_t)kFT : nw;
+    const uint32_t nw = (1u << s) / 2;  // cell words (two u16 cells each), whole waves
+    return nw < (uint32_t)T ? (uint32_t)T : nw;
 }
 
 // The counting finisher of one range (keys x = k - kbase below 2^s, s <= kCountBits),
-// el[] in round-major order (element k * kFT + tid). c32: a u16 cell per key, two to
-// a word, zeroed by the caller (counts, then, after the scan, running slots relative
-// to the scanning wave's start); rows / keys: the placed row ids and keys by slot. A
-// row takes its slot by one atomic on its key's cell; the rows of a key are then put
-// back in ascending order (they arrive in any order), and values and positions leave
-// slot by slot, while the range's cell words are zeroed again for the next range.
-// Returns false, having written nothing outside LDS, when some key holds more than
-// kTieMax rows (the cells are then left for the caller to zero).
-__device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t len, uint32_t kbase, int s,
+// el[] in round-major order (element k * T + tid). c32: a u16 cell per key, two to a
+// word, zeroed by the caller (counts, then, after the scan, running slots relative to
+// the scanning wave's start); rows / keys: the placed row ids and keys by slot. A row
+// takes its slot by one atomic on its key's cell; a row whose key holds other rows
+// (they took their slots in any order) is then written at the group's start + the
+// number of the group's rows with a smaller id, values and positions slot by slot,
+// and the range's cell words are zeroed again for the next range. Returns false,
+// having written nothing outside LDS, when some key holds more than kTieMax rows
+// (the cells are then left for the caller to zero).
+template <int T, int I, bool BF>
+__device__ __forceinline__ bool finish_counting(const u64 (&el)[I], uint32_t len, uint32_t kbase, int s,
                                                 uint32_t* c32, uint32_t* rows, uint16_t* keys, uint32_t* wsum,
                                                 int32_t* vout, u64* pout) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int kW = kFT / 64;
-    const uint32_t nw = count_words(s);
+    constexpr int kW = T / 64;
+    const uint32_t nw = count_words<T>(s);
 #pragma unroll
-    for (int k = 0; k < kFI; k++)
-        if ((uint32_t)k * kFT + tid < len) {
-            const uint32_t x = (uint32_t)el[k] - kbase;
+    for (int k = 0; k < I; k++) {
+        const uint32_t x = (uint32_t)el[k] - kbase;
+        const bool v = (uint32_t)k * T + tid < len;
+        if (BF)
+            atomicAdd(&c32[v ? x >> 1 : kCap / 2], 1u << (16 * (x & 1)));
+        else if (v)
             atomicAdd(&c32[x >> 1], 1u << (16 * (x & 1)));
-        }
+    }
     __syncthreads();
-    // each lane scans q consecutive words (wave w: words [w * nw / 16, (w + 1) * nw / 16))
+    // each lane scans q consecutive words (wave w: words [w * nw / kW, (w + 1) * nw / kW))
     const uint32_t per = nw / kW, q = per / 64, lgper = 31 - __builtin_clz(per);
     uint32_t* mine = c32 + wave * per + lane * q;
     uint32_t tot = 0, mx = 0;
@@ -338,26 +346,30 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t l
     wpre = __shfl_up(wpre, 1, 64);
     wpre = lane ? wpre : 0u;
 #pragma unroll
-    for (int k = 0; k < kFI; k++) {
+    for (int k = 0; k < I; k++) {
         const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
         const uint32_t base = __shfl(wpre, (x >> 1) >> lgper, 64);
-        if ((uint32_t)k * kFT + tid < len) {
+        const bool v = (uint32_t)k * T + tid < len;
+        if (BF) {
+            const uint32_t old = atomicAdd(&c32[v ? x >> 1 : kCap / 2], 1u << sh);
+            const uint32_t slot = v ? ((old >> sh) & 0xFFFFu) + base : kCap;
+            rows[slot] = (uint32_t)(el[k] >> 32);
+            keys[slot] = (uint16_t)x;
+        } else if (v) {
             const uint32_t slot = ((atomicAdd(&c32[x >> 1], 1u << sh) >> sh) & 0xFFFFu) + base;
             rows[slot] = (uint32_t)(el[k] >> 32);
             keys[slot] = (uint16_t)x;
         }
     }
     __syncthreads();
-    // the cell of x now holds the end of its slots, the cell of x - 1 their start. A
-    // row whose key holds other rows (they took their slots in any order) goes to the
-    // group's start + the number of the group's rows with a smaller id.
+    // the cell of x now holds the end of its slots, the cell of x - 1 their start
     const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
 #pragma unroll
-    for (int k = 0; k < kFI; k++) {
-        const uint32_t e = (uint32_t)k * kFT + tid;
+    for (int k = 0; k < I; k++) {
+        const uint32_t e = (uint32_t)k * T + tid;
         const uint32_t ec = e < len ? e : len - 1;
         const uint32_t x = keys[ec], r = rows[ec];
-        const bool tied = (ec > 0 && keys[ec - 1] == x) || (ec + 1 < len && keys[ec + 1] == x);
+        const bool tied = (ec > 0 && keys[ec - 1] == x) | (ec + 1 < len && keys[ec + 1] == x);
         const uint32_t xp = x ? x - 1 : 0;
         const uint32_t b0 = __shfl(wpre, (xp >> 1) >> lgper, 64);
         uint32_t pos = ec;
@@ -371,7 +383,7 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t l
         }
     }
     __syncthreads();
-    for (uint32_t x = tid; x < nw; x += kFT) c32[x] = 0;
+    for (uint32_t x = tid; x < nw; x += T) c32[x] = 0;
     if (tid == 0) wsum[kW] = 0;
     return true;
 }
@@ -380,30 +392,32 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[kFI], uint32_t l
 // range's words are loaded into registers while the current one is sorted (a block
 // holds 128 KB of LDS, so a CU runs one: without this its loads, LDS work and stores
 // would take turns). A range it cannot take goes to the ranked finisher's list.
-__global__ __launch_bounds__(kFT) void k_msd_finish_count(const u64* __restrict__ w0, const u64* __restrict__ w1,
-                                                          const Fin* __restrict__ fins, uint32_t nfin, uint32_t kmin,
-                                                          int32_t* __restrict__ vout, u64* __restrict__ pout,
-                                                          Fin* __restrict__ fb, Ctr* __restrict__ ctr) {
-    constexpr int kW = kFT / 64;
-    __shared__ uint32_t c32[kCap / 2];  // u16 cells of 2^14 keys
-    __shared__ uint32_t rows[kCap];
-    __shared__ uint16_t keys[kCap];
+template <int T, int I, bool BF>
+__global__ __launch_bounds__(T) void k_msd_finish_count(const u64* __restrict__ w0, const u64* __restrict__ w1,
+                                                        const Fin* __restrict__ fins, uint32_t nfin, uint32_t kmin,
+                                                        int32_t* __restrict__ vout, u64* __restrict__ pout,
+                                                        Fin* __restrict__ fb, Ctr* __restrict__ ctr) {
+    static_assert(T * I == (int)kCap, "a range of kCap rows per block");
+    constexpr int kW = T / 64;
+    __shared__ uint32_t c32[kCap / 2 + 1];  // u16 cells of 2^14 keys (+ BF's dummy word)
+    __shared__ uint32_t rows[kCap + 1];     // by slot (+ BF's dummy slot)
+    __shared__ uint16_t keys[kCap + 1];
     __shared__ uint32_t wsum[kW + 1];  // wave totals, then the fallback flag
     const int tid = threadIdx.x;
-    u64 nx[kFI];
+    u64 nx[I];
     auto prefetch = [&](uint32_t fi) {  // the words of range fi, if the counting path sorts it
         const Fin f = fins[fi];
         if ((f.meta & 0xFF) == 0) return;
         const u64* src = ((f.meta >> 8) ? w1 : w0) + f.start;
 #pragma unroll
-        for (int k = 0; k < kFI; k++) {
-            const uint32_t i = (uint32_t)k * kFT + tid;
+        for (int k = 0; k < I; k++) {
+            const uint32_t i = (uint32_t)k * T + tid;
             nx[k] = src[i < f.len ? i : f.len - 1];
         }
     };
     if (blockIdx.x >= nfin) return;
     prefetch(blockIdx.x);
-    for (uint32_t x = tid; x < kCap / 2; x += kFT) c32[x] = 0;
+    for (uint32_t x = tid; x < kCap / 2; x += T) c32[x] = 0;
     if (tid == 0) wsum[kW] = 0;
     __syncthreads();
     for (uint32_t fi = blockIdx.x; fi < nfin; fi += gridDim.x) {
@@ -414,18 +428,18 @@ __global__ __launch_bounds__(kFT) void k_msd_finish_count(const u64* __restrict_
         u64* po = pout ? pout + f.start : nullptr;
         const uint32_t nxt = fi + gridDim.x;
         if (s == 0) {  // one key (or one row): already in row order; the cells stay zero
-            for (uint32_t e = tid; e < f.len; e += kFT) emit(vo, po, e, src[e]);
+            for (uint32_t e = tid; e < f.len; e += T) emit(vo, po, e, src[e]);
             if (nxt < nfin) prefetch(nxt);
             continue;
         }
-        u64 el[kFI];
+        u64 el[I];
 #pragma unroll
-        for (int k = 0; k < kFI; k++) el[k] = nx[k];
+        for (int k = 0; k < I; k++) el[k] = nx[k];
         if (nxt < nfin) prefetch(nxt);
-        if (!finish_counting(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po)) {
+        if (!finish_counting<T, I, BF>(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po)) {
             if (tid == 0) fb[atomicAdd(&ctr->nfb, 1u)] = f;
             __syncthreads();
-            for (uint32_t x = tid; x < kCap / 2; x += kFT) c32[x] = 0;
+            for (uint32_t x = tid; x < kCap / 2; x += T) c32[x] = 0;
             if (tid == 0) wsum[kW] = 0;
         }
         __syncthreads();  // LDS is reused by the next range
@@ -517,6 +531,10 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
     u64* scratch = (u64*)pool_alloc(scan_u32_scratch_elems(tmax * 256) * 8);
     Seg* sl[2] = {(Seg*)pool_alloc(smax * sizeof(Seg)), (Seg*)pool_alloc(smax * sizeof(Seg))};
     Ctr* ctr = (Ctr*)pool_alloc(sizeof(Ctr));
+    // MQ_ISORT_FIN: the counting finisher's shape, 1 = 1024 x 16 with per-row guards,
+    // 2 = 512 x 32 with guards, 3 = 512 x 32 branch-free (A/B)
+    const char* ff = getenv("MQ_ISORT_FIN");
+    const int fin_form = ff ? atoi(ff) : 1;
     Fin* fl[kMaxLevels] = {};  // finisher lists of each level: counting
     Fin* rl[kMaxLevels] = {};  // ... ranked
     Fin* bl[kMaxLevels] = {};  // ... and the counting finisher's fallbacks
@@ -591,8 +609,16 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
             hipLaunchKernelGGL(k_msd_finish_ranked<false>, dim3(hc.nranked), dim3(kFT), 0, st, wb[0], wb[1], rl[level],
                                ctr, kmin, vout, pout);
         if (hc.nfin) {
-            hipLaunchKernelGGL(k_msd_finish_count, dim3(hc.nfin < cus ? hc.nfin : cus), dim3(kFT), 0, st, wb[0],
-                               wb[1], fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
+            const uint32_t g = hc.nfin < cus ? hc.nfin : cus;
+            if (fin_form == 1)
+                hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false>), dim3(g), dim3(1024), 0, st, wb[0], wb[1],
+                                   fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
+            else if (fin_form == 2)
+                hipLaunchKernelGGL((k_msd_finish_count<512, 32, false>), dim3(g), dim3(512), 0, st, wb[0], wb[1],
+                                   fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
+            else
+                hipLaunchKernelGGL((k_msd_finish_count<512, 32, true>), dim3(g), dim3(512), 0, st, wb[0], wb[1],
+                                   fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
             hipLaunchKernelGGL(k_msd_finish_ranked<true>, dim3(cus), dim3(kFT), 0, st, wb[0], wb[1], bl[level], ctr,
                                kmin, vout, pout);
         }
