@@ -65,6 +65,13 @@ __host__ __device__ inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b
 // monotone and below P. Digit d holds the keys x in [lo(d), lo(d + 1)), lo(d) =
 // ceil(d 2^32 / M), at most floor(2^32 / M) + 1 of them: the next level's R.
 __device__ __forceinline__ uint32_t digit_of(uint32_t x, u64 M) { return (uint32_t)(((u64)x * M) >> 32); }
+// The same for M < 2^32 (P < R, every level that splits a range into more than single
+// keys): one v_mul_hi_u32 instead of a 64-bit multiply.
+template <bool WIDE>
+__device__ __forceinline__ uint32_t digit_m(uint32_t x, u64 M) {
+    if constexpr (WIDE) return digit_of(x, M);
+    else return __umulhi(x, (uint32_t)M);
+}
 __host__ __device__ inline u64 digit_lo(uint32_t d, u64 M) { return cdiv((u64)d << 32, M); }
 
 __global__ void k_tile_seg(const Seg* __restrict__ segs, uint32_t* __restrict__ tseg) {
@@ -82,7 +89,7 @@ __device__ __forceinline__ void tile_range(const Seg* segs, const uint32_t* tseg
 }
 
 // Per tile: counts of the level's digit, into hist[t0 * P + d * nt + tin].
-template <bool FIRST>
+template <bool FIRST, bool WIDE>
 __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, const uint8_t* __restrict__ dig,
                                                   const Seg* __restrict__ segs, const uint32_t* __restrict__ tseg,
                                                   uint32_t kmin, u64 M, uint32_t P, uint32_t* __restrict__ hist) {
@@ -100,7 +107,7 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
         const uint32_t i = (uint32_t)k * kMT + tid;
         const u64 ic = e0 + (i < len ? i : len - 1);
         if constexpr (FIRST)
-            d[k] = digit_of(((uint32_t)__builtin_nontemporal_load(col + ic) ^ 0x80000000u) - kmin, M);
+            d[k] = digit_m<WIDE>(((uint32_t)__builtin_nontemporal_load(col + ic) ^ 0x80000000u) - kmin, M);
         else
             d[k] = (uint32_t)__builtin_nontemporal_load(dig + ic);
     }
@@ -115,7 +122,7 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
 // wc[d] (the wave's row of the block's counters). dr[k] = d << 16 | rank within the
 // wave's items of digit d. Digits: byte `sh` of key - kbase (DIG = false) or the
 // level digit of key - kbase (DIG = true).
-template <int IT, bool LEVEL>
+template <int IT, bool LEVEL, bool WIDE = true>
 __device__ __forceinline__ void rank_items(const u64 (&el)[IT], uint32_t (&dr)[IT], uint32_t wbase, uint32_t len,
                                            uint32_t kbase, int sh, uint32_t wm, u64 M, uint32_t* wc, int lane) {
     const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -123,7 +130,7 @@ __device__ __forceinline__ void rank_items(const u64 (&el)[IT], uint32_t (&dr)[I
     for (int k = 0; k < IT; k++) {
         const bool valid = wbase + (uint32_t)k * 64 + lane < len;
         const uint32_t x = (uint32_t)el[k] - kbase;
-        const uint32_t d = LEVEL ? digit_of(x, M) : (x >> sh) & wm;
+        const uint32_t d = LEVEL ? digit_m<WIDE>(x, M) : (x >> sh) & wm;
         const u64 peers = match_any8(d, __ballot(valid));
         const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
         const uint32_t cur = wc[d];
@@ -167,7 +174,7 @@ __device__ __forceinline__ void digit_offsets(uint32_t (*wcnt)[256], uint32_t* l
 // Stable scatter of a level: each tile's words ranked by digit in LDS, then written
 // as contiguous digit runs at the range's start + the scanned offsets. Mn != 0: also
 // the next level's digit of every word (of its key relative to its child range).
-template <bool FIRST>
+template <bool FIRST, bool WIDE, bool NWIDE>
 __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col, const u64* __restrict__ in,
                                                      const Seg* __restrict__ segs, const uint32_t* __restrict__ tseg,
                                                      const uint32_t* __restrict__ hscan, uint32_t kmin, u64 M,
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
         else
             el[k] = in[ic];
     }
-    rank_items<kMI, true>(el, dr, wbase, len, kbase, 0, 0, M, wcnt[wave], lane);
+    rank_items<kMI, true, WIDE>(el, dr, wbase, len, kbase, 0, 0, M, wcnt[wave], lane);
     __syncthreads();
     digit_offsets<kW>(wcnt, loff, wsum, tid);
 #pragma unroll
@@ -222,10 +229,10 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
         if (e < len) {
             const u64 v = stage[e];
             const uint32_t x = (uint32_t)v - kbase;
-            const uint32_t d = digit_of(x, M);
+            const uint32_t d = digit_m<WIDE>(x, M);
             const u64 dst = gofs[d] + (e - loff[d]);
             out[dst] = v;
-            if (Mn) dig[dst] = (uint8_t)digit_of(x - clo[d], Mn);
+            if (Mn) dig[dst] = (uint8_t)digit_m<NWIDE>(x - clo[d], Mn);
         }
     }
 }
@@ -574,12 +581,16 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
         bl[level] = (Fin*)pool_alloc((nchild < n ? nchild : n) * sizeof(Fin));
         if (!fl[level] || !rl[level] || !bl[level]) return done(set_err(MQ_ENOMEM, "index sort: range list"));
         hipLaunchKernelGGL(k_tile_seg, dim3(nseg), dim3(256), 0, st, cur, tseg);
-        if (level == 0)
-            hipLaunchKernelGGL(k_msd_hist<true>, dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg, kmin, M, P,
-                               hist);
+        const bool wide = M >> 32 != 0;
+        if (level == 0 && wide)
+            hipLaunchKernelGGL((k_msd_hist<true, true>), dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg, kmin,
+                               M, P, hist);
+        else if (level == 0)
+            hipLaunchKernelGGL((k_msd_hist<true, false>), dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg, kmin,
+                               M, P, hist);
         else
-            hipLaunchKernelGGL(k_msd_hist<false>, dim3(ntile), dim3(kMT), 0, st, nullptr, dig, cur, tseg, kmin, M, P,
-                               hist);
+            hipLaunchKernelGGL((k_msd_hist<false, true>), dim3(ntile), dim3(kMT), 0, st, nullptr, dig, cur, tseg, kmin,
+                               M, P, hist);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "index sort: histogram launch"));
         int rc = scan_u32_exclusive_u32(hist, hist, nh, scratch, st);
         if (rc) return done(rc);
@@ -599,12 +610,23 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
         Pn = Pn < 2 ? 2 : Pn > 256 ? 256 : Pn;
         if (Pn > Rn) Pn = Rn;
         const u64 Mn = hc.nnext ? (Pn << 32) / Rn : 0;
-        if (level == 0)
-            hipLaunchKernelGGL(k_msd_scatter<true>, dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg, hist, kmin,
-                               M, P, Mn, wb[dst], dig);
-        else
-            hipLaunchKernelGGL(k_msd_scatter<false>, dim3(ntile), dim3(kMT), 0, st, nullptr, wb[dst ^ 1], cur, tseg,
+        // digits by one v_mul_hi_u32 where the multipliers fit 32 bits (the usual case)
+        const u64* lin = level == 0 ? nullptr : wb[dst ^ 1];
+        const int* lcol = level == 0 ? col : nullptr;
+        if (!wide && !(Mn >> 32)) {
+            if (level == 0)
+                hipLaunchKernelGGL((k_msd_scatter<true, false, false>), dim3(ntile), dim3(kMT), 0, st, lcol, lin, cur,
+                                   tseg, hist, kmin, M, P, Mn, wb[dst], dig);
+            else
+                hipLaunchKernelGGL((k_msd_scatter<false, false, false>), dim3(ntile), dim3(kMT), 0, st, lcol, lin,
+                                   cur, tseg, hist, kmin, M, P, Mn, wb[dst], dig);
+        } else if (level == 0) {
+            hipLaunchKernelGGL((k_msd_scatter<true, true, true>), dim3(ntile), dim3(kMT), 0, st, lcol, lin, cur, tseg,
                                hist, kmin, M, P, Mn, wb[dst], dig);
+        } else {
+            hipLaunchKernelGGL((k_msd_scatter<false, true, true>), dim3(ntile), dim3(kMT), 0, st, lcol, lin, cur,
+                               tseg, hist, kmin, M, P, Mn, wb[dst], dig);
+        }
         if (hc.nranked)
             hipLaunchKernelGGL(k_msd_finish_ranked<false>, dim3(hc.nranked), dim3(kFT), 0, st, wb[0], wb[1], rl[level],
                                ctr, kmin, vout, pout);

@@ -68,6 +68,12 @@ def _wide_range_inputs():
     yield "b23_lsd3_4M", (rng.integers(0, 1 << 23, n) + 10**9).astype(np.int32)
     yield "b8_lsd1_4M", (rng.integers(0, 200, n) - 100).astype(np.int32)
     yield "sorted_desc_4M", np.arange(n, 0, -1, dtype=np.int64).astype(np.int32) * 64
+    c = rng.integers(0, 1 << 30, n).astype(np.int32)
+    hot = rng.choice(n, 3000, replace=False)
+    c[hot[:1000]] = 123_456_789  # keys on more than kTieMax rows inside ranges of many
+    c[hot[1000:2000]] = 987_654_321  # keys: the counting finisher hands them to the ranked one
+    c[hot[2000:]] = c[hot[2000:]] | 1
+    yield "hot_keys_4M", c
 
 
 @pytest.mark.parametrize("form", ["default", "msd"])
