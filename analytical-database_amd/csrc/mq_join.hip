@@ -1222,6 +1222,66 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __rest
     }
 }
 
+// The same write with more reads in flight: a wave takes kWriteWords words at a time (8:
+// 1 word 4.30, 4 words 4.00 ms at 2^28 many-to-many, same box), and every row's first
+// two run positions (all of config 5's runs) are requested for
+// all of them before any pair is stored; longer runs finish in a loop. The run reads
+// are random (one line of the key-sorted positions per hit row), so the kernel is
+// bound by how many of them are outstanding.
+template <int kWriteWords>
+__global__ __launch_bounds__(kTPB) void k_join_write_runs_mlp(const uint32_t* __restrict__ pk, uint64_t n2,
+                                                              const uint32_t* __restrict__ rs,
+                                                              const u64* __restrict__ woffs,
+                                                              const int* __restrict__ p2,
+                                                              const int* __restrict__ bpos, int* __restrict__ out1,
+                                                              int* __restrict__ out2) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (n2 + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64) * kWriteWords;
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6)) * kWriteWords; w0 < nw;
+         w0 += wstride) {
+        uint32_t pv[kWriteWords], a[kWriteWords], L[kWriteWords];
+        u64 o[kWriteWords];
+        int pp[kWriteWords], b0[kWriteWords], b1[kWriteWords];
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            const uint64_t j = (w0 + u) * 64 + (uint64_t)lane;
+            pv[u] = j < n2 ? pk[j] : 0u;
+            pp[u] = j < n2 ? p2[j] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            run_decode(pv[u], rs, &a[u], &L[u]);
+            uint32_t incl = L[u];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            o[u] = (w0 + u < nw ? woffs[w0 + u] : 0ull) + (u64)(incl - L[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            b0[u] = L[u] ? bpos[a[u]] : 0;
+            b1[u] = L[u] > 1u ? bpos[a[u] + 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            if (!L[u]) continue;
+            out1[o[u]] = b0[u];
+            out2[o[u]] = pp[u];
+            if (L[u] > 1u) {
+                out1[o[u] + 1] = b1[u];
+                out2[o[u] + 1] = pp[u];
+            }
+            for (uint32_t t = 2; t < L[u]; t++) {
+                out1[o[u] + t] = bpos[a[u] + t];
+                out2[o[u] + t] = pp[u];
+            }
+        }
+    }
+}
+
 // ---- duplicate keys as runs (the build sorted by key, stable: a key's rows are one
 // run in insertion order); the distinct keys go into the windowed unique table with
 // their run index as payload ----
@@ -1920,8 +1980,19 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         return MQ_OK;
     }
     if (j->unique == 2 && j->packed) {
-        hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
-                           (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
+        // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, default eight
+        const char* wf = getenv("MQ_JOIN_WRITE");
+        if (wf && wf[0] == '1')
+            hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
+                               (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
+        else if (wf && wf[0] == '4')
+            hipLaunchKernelGGL(k_join_write_runs_mlp<4>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 4)),
+                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
+                               d_out1, d_out2);
+        else
+            hipLaunchKernelGGL(k_join_write_runs_mlp<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)),
+                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
+                               d_out1, d_out2);
         LAUNCHCHK("k_join_write_runs");
         return MQ_OK;
     }
