@@ -1222,8 +1222,9 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __rest
     }
 }
 
-// The same write with more reads in flight: a wave takes kWriteWords words at a time (8:
-// 1 word 4.30, 4 words 4.00 ms at 2^28 many-to-many, same box), and every row's first
+// The same write with more reads in flight: a wave takes kWriteWords words at a time
+// (2^28 many-to-many, alternating on one box: 1 word 4.30, 4 words 4.00 ms; on another
+// 1 / 4 / 8 words 3.63-4.24 / 3.65-4.03 / 3.58-3.94 ms), and every row's first
 // two run positions (all of config 5's runs) are requested for
 // all of them before any pair is stored; longer runs finish in a loop. The run reads
 // are random (one line of the key-sorted positions per hit row), so the kernel is
