@@ -89,6 +89,36 @@ def test_index_build_wide_range_vs_oracle(lib, refcpu, name, col, form, monkeypa
     assert np.array_equal(p, wp), name
 
 
+@pytest.mark.parametrize("which", ["values_only", "positions_only"])
+def test_index_build_msd_one_output(lib, refcpu, which, monkeypatch):
+    """mq_index_build takes NULL for either output (mq_device.h); the MSD form's
+    finishers and the copied one-key ranges honour it too."""
+    monkeypatch.setenv("MQ_INDEX_MSD_MIN", "0")
+    rng = np.random.default_rng(91)
+    n = (1 << 22) + 3
+    col = rng.integers(0, 1 << 30, n).astype(np.int32)
+    col[rng.random(n) < 0.2] = 5  # a one-key range far above the LDS capacity
+    d = Dev.of(col)
+    v, p = Dev(n * 4), Dev(n * 8)
+    wv, wp = refcpu.index_build(col)
+    if which == "values_only":
+        mq.check(lib.mq_index_build(d.ptr, n, v.ptr, None, None))
+        assert np.array_equal(v.get(np.int32, n), wv)
+    else:
+        mq.check(lib.mq_index_build(d.ptr, n, None, p.ptr, None))
+        assert np.array_equal(p.get(np.uint64, n), wp)
+
+
+@pytest.mark.parametrize("n", [(1 << 24) - 1, 1 << 24])
+def test_index_build_form_boundary(lib, refcpu, n):
+    """Either side of the default MSD threshold (2^24 rows), a 31-bit key range."""
+    rng = np.random.default_rng(n)
+    col = rng.integers(-2**30, 2**30, n).astype(np.int32)
+    v, p = gpu_index(lib, col)
+    wv, wp = refcpu.index_build(col)
+    assert np.array_equal(v, wv) and np.array_equal(p, wp)
+
+
 def gpu_lomuto(L, col: np.ndarray):
     n = len(col)
     d = Dev.of(col.astype(np.int32)) if n else Dev(4)
