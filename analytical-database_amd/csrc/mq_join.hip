@@ -885,6 +885,14 @@ __device__ __forceinline__ void probe_emit(uint64_t j, bool hit, uint32_t payloa
     }
 }
 
+// A packed run payload's length (a hit's payload is never 0; 15 = look the run up).
+__device__ __forceinline__ uint32_t run_len(uint32_t payload, const uint32_t* __restrict__ rs) {
+    const uint32_t L = payload & 15u;
+    if (L != 15u) return L;
+    const uint32_t r = payload >> 4;
+    return rs[r + 1] - rs[r];
+}
+
 // kProbeILP probes per thread per step: the keys are loaded coalesced, then all
 // their home buckets (4 slots, 32 B, two 16-byte loads) are requested before any
 // is examined. Random reads cost per 32-B sector (tools/random_read: a 64-B bucket
@@ -906,7 +914,8 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
                                                           u64* __restrict__ hits, const uint32_t* __restrict__ rs,
-                                                          uint32_t* __restrict__ cnt, bool packed, bool marks) {
+                                                          uint32_t* __restrict__ cnt, bool packed, bool marks,
+                                                          uint32_t* __restrict__ wcnt) {
     __shared__ uint32_t q_j[kTPB / 64][kContCap], q_h[kTPB / 64][kContCap], q_k[kTPB / 64][kContCap];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* const qj = q_j[wave];
@@ -940,6 +949,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                 const uint32_t payload = hit ? (uint32_t)(c >> 32) : 0u;
                 if (RUNS || hit) probe_emit<RUNS>(cj, hit, payload, pstart, rs, cnt, packed);
                 if (!RUNS && hit) atomicOr(&hits[cj >> 6], 1ull << (cj & 63));  // word stored in an earlier step
+                if (RUNS && wcnt && hit) atomicAdd(&wcnt[cj >> 6], run_len(payload, rs));  // likewise
             } else {
                 again = true;
             }
@@ -1012,6 +1022,14 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             }
             nq += (uint32_t)__popcll(dm);
             if (j < n2 && !defer) probe_emit<RUNS>(j, hit, payload, pstart, rs, cnt, packed);
+            if (RUNS && wcnt) {
+                // packed runs: the word's run lengths, summed over the wave (a deferred
+                // row adds its own when it resolves), so no pass re-reads the payloads
+                uint32_t L = (j < n2 && !defer && hit) ? run_len(payload, rs) : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+                if (j < n2 && lane == 0) wcnt[j >> 6] = L;
+            }
             if constexpr (!RUNS) {
                 // a wave's 64 lanes hold 64 consecutive rows: their hits are one word
                 // (a deferred row's bit is set when it resolves)
@@ -1177,21 +1195,6 @@ __device__ __forceinline__ void run_decode(uint32_t pk, const uint32_t* __restri
     }
     *a = pk ? s : 0u;
     *L = pk ? l : 0u;
-}
-
-__global__ __launch_bounds__(kTPB) void k_runs_count(const uint32_t* __restrict__ pk, uint64_t n2,
-                                                     const uint32_t* __restrict__ rs, uint32_t* __restrict__ cnt) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (n2 + 63) / 64;
-    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64);
-    for (uint64_t w = (uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6); w < nw; w += wstride) {
-        const uint64_t j = w * 64 + (uint64_t)lane;
-        uint32_t a, L;
-        run_decode(j < n2 ? pk[j] : 0u, rs, &a, &L);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
-        if (lane == 0) cnt[w] = L;
-    }
 }
 
 __global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __restrict__ pk, uint64_t n2,
@@ -1934,20 +1937,20 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks);
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks, cnt);
         LAUNCHCHK("k_ht_probe_unique");
-        hipLaunchKernelGGL(k_runs_count, dim3(stream_grid(s, nw * 64)), dim3(kTPB), 0, st, j->pstart, n2, j->rs, cnt);
-        LAUNCHCHK("k_runs_count");
     } else if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks);
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks,
+                           (uint32_t*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
         auto kern = k_ht_probe_unique<false>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false, j->marks);
+                           j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false, j->marks,
+                           (uint32_t*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
         hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
         LAUNCHCHK("k_hits_count");
