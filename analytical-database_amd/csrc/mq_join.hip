@@ -852,6 +852,163 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
     for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) dst[x] = tab[x];
 }
 
+// Duplicate keys without a sort (round 3): the build rows are partitioned by window
+// like the unique build's (stable, so a window's rows keep their input order), and
+// one block per window finds the runs itself. In LDS: its keys go into the window's
+// slots by CAS (u32 keys; the key -1, the u32 empty marker, flags), a u16 count per
+// slot, one scan over the slots in slot order gives each slot's run its place in
+// the window's stretch of the run array, and each row takes a place in its run by
+// one atomic; rows of a key arrive at their places in any order, so a row's final
+// place is its run's start + the number of the run's rows before it in input order
+// (their input indices sit in LDS by place). The row writes its payload there (the
+// key's build positions in insertion order, bpos), and the window's table words
+// carry {key, start << 4 | length} with the unique build's overflow marks. A window
+// of more than kRunRows rows or a key on 15 rows or more (not packable) flags
+// *general; the caller then takes the sorted-runs build. Replaces, at 2^28 rows with
+// every key twice, the 4-pass sort of the pairs, the run extraction and the
+// partition of the distinct keys.
+constexpr uint32_t kRunRows = 6144;  // rows a window block takes (3/4 of its slots)
+constexpr uint32_t kEmpty32 = ~0u;
+
+__global__ __launch_bounds__(kWinTPB) void k_win_build_runs(const u64* __restrict__ in,
+                                                            const uint32_t* __restrict__ wstart,
+                                                            u64* __restrict__ words, int* __restrict__ bpos, Win t,
+                                                            uint32_t* __restrict__ general) {
+    constexpr uint32_t W = 1u << kWinLog;
+    constexpr int kPer = (int)(kRunRows / kWinTPB);  // rows per thread
+    constexpr int kW = kWinTPB / 64;
+    __shared__ uint32_t tab[W];          // keys by slot
+    __shared__ uint32_t c32[W / 2];      // u16 per slot: counts, then run places
+    __shared__ uint16_t pidx[kRunRows];  // input index (within the window) by place
+    __shared__ uint8_t ovf[W / kBucket];
+    __shared__ uint32_t wsum[kW + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t w = blockIdx.x;
+    const uint32_t b = wstart[w], e = wstart[w + 1], c = e - b;
+    if (W != (uint32_t)t.wmask + 1 || c > kRunRows) {  // (a table smaller than one window: never here)
+        if (tid == 0) *general = 1;
+        return;
+    }
+    for (uint32_t x = tid; x < W; x += kWinTPB) tab[x] = kEmpty32;
+    for (uint32_t x = tid; x < W / 2; x += kWinTPB) c32[x] = 0;
+    for (uint32_t x = tid; x < W / kBucket; x += kWinTPB) ovf[x] = 0;
+    if (tid == 0) wsum[kW] = 0;
+    __syncthreads();
+    uint32_t key[kPer], pay[kPer], slot[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        const u64 v = i < c ? in[b + i] : 0ull;
+        key[k] = (uint32_t)v;
+        pay[k] = (uint32_t)(v >> 32);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        slot[k] = 0;
+        if ((uint32_t)k * kWinTPB + tid >= c) continue;
+        if (key[k] == kEmpty32) {
+            bad = true;
+            continue;
+        }
+        const uint32_t h0 = (uint32_t)ht_home(key[k], t.wmask);
+        uint32_t h = h0;
+        for (uint32_t step = 0; step < W; step++) {
+            const uint32_t old = atomicCAS(&tab[h], kEmpty32, key[k]);
+            if (old == kEmpty32 || old == key[k]) {
+                if (old == kEmpty32 && step >= kBucket) ovf[h0 / kBucket] = 1;
+                break;
+            }
+            h = (h + 1) & (W - 1);
+        }
+        slot[k] = h;
+        atomicAdd(&c32[h >> 1], 1u << (16 * (h & 1)));
+    }
+    if (bad) wsum[kW] = 1;
+    __syncthreads();
+    // exclusive scan of the counts in slot order: lane-consecutive words, 4 a thread
+    constexpr int kQ = (int)(W / 2 / kWinTPB);
+    uint32_t* mine = c32 + (uint32_t)tid * kQ;
+    uint32_t tot = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < kQ; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu, hi = cell >> 16;
+        mx = lo > mx ? lo : mx;
+        mx = hi > mx ? hi : mx;
+        tot += lo + hi;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    if (__ballot(mx >= 15u)) wsum[kW] = 1;  // a run the packed payload cannot hold
+    __syncthreads();
+    if (wsum[kW]) {
+        if (tid == 0) *general = 1;
+        return;
+    }
+    uint32_t run = incl - tot;
+    for (int v = 0; v < wave; v++) run += wsum[v];
+#pragma unroll
+    for (int j = 0; j < kQ; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu;
+        mine[j] = run | ((run + lo) << 16);
+        run += lo + (cell >> 16);
+    }
+    __syncthreads();
+    uint32_t place[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        place[k] = 0;
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        if (i >= c) continue;
+        const uint32_t h = slot[k], sh = 16 * (h & 1);
+        place[k] = (atomicAdd(&c32[h >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        pidx[place[k]] = (uint16_t)i;
+    }
+    __syncthreads();
+    // c32 now holds each slot's run end; its run starts where slot h - 1's ends
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        if (i >= c) continue;
+        const uint32_t h = slot[k];
+        const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
+        uint32_t r = 0;
+        for (uint32_t q = s0; q < s1; q++) r += pidx[q] < i;
+        bpos[b + s0 + r] = (int)pay[k];
+    }
+    // the window's table words, a bucket (4 slots) per thread, with the overflow marks
+    u64* dst = words + (uint64_t)w * W;
+    for (uint32_t bk = tid; bk < W / kBucket; bk += kWinTPB) {
+        u64 o[kBucket];
+        bool full = true;
+#pragma unroll
+        for (uint32_t q = 0; q < kBucket; q++) {
+            const uint32_t h = bk * kBucket + q;
+            const uint32_t k = tab[h];
+            if (k == kEmpty32) {
+                o[q] = kEmpty;
+                full = false;
+            } else {
+                const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
+                o[q] = (u64)k | ((u64)(((b + s0) << 4) | (s1 - s0)) << 32);
+            }
+        }
+        if (full && (((uint32_t)o[0] > (uint32_t)o[1]) != (ovf[bk] != 0))) {
+            const u64 x = o[0];
+            o[0] = o[1];
+            o[1] = x;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kBucket; q++) dst[bk * kBucket + q] = o[q];
+    }
+}
+
 // 2 probes per thread per step: with whole-bucket loads 2 beat 8 (8.25 vs 8.8 ms at
 // 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8 had beaten 1.
 constexpr int kProbeILP = 2;
@@ -1577,6 +1734,83 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     return done(MQ_OK);
 }
 
+// Duplicate keys, windowed (k_win_build_runs): the build rows partitioned by window
+// (the unique build's passes), then each window's runs found in LDS. Returns 0
+// (j->unique = 2, packed payloads, j->bpos the runs), 1 when it does not apply or a
+// window flagged (the caller takes the sorted-runs build), or an error.
+int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots, uint32_t* general,
+                      hipStream_t st, const DevState* s) {
+    (void)s;
+    const char* e = getenv("MQ_JOIN_WINRUNS");  // "0": the sorted-runs build (A/B, tests)
+    const char* r = getenv("MQ_JOIN_RUNS");     // "0": the global-CAS run table (tests)
+    if ((e && e[0] == '0') || (r && r[0] == '0') || n < kWindowBuildRows || n > (1ull << 28) || j->win.wlog != kWinLog) return 1;
+    const Win t = j->win;
+    int lg = 0;
+    while ((1ull << lg) < slots) lg++;
+    const int passes = (lg - t.wlog + 7) / 8;
+    const uint32_t nw = (uint32_t)(slots >> t.wlog);
+    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t nh = ntiles * kRadix;
+    u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
+    uint32_t *hist = nullptr, *wstart = nullptr;
+    auto done = [&](int rc) {
+        pool_free(a);
+        pool_free(b);
+        pool_free(hist);
+        pool_free(hscan);
+        pool_free(scratch);
+        pool_free(wstart);
+        return rc;
+    };
+    a = (u64*)pool_alloc(n * 8);
+    b = passes > 1 ? (u64*)pool_alloc(n * 8) : nullptr;
+    hist = (uint32_t*)pool_alloc(nh * 4);
+    hscan = (u64*)pool_alloc(nh * 8);
+    scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8);
+    wstart = (uint32_t*)pool_alloc(((uint64_t)nw + 1) * 4);
+    if (!a || (passes > 1 && !b) || !hist || !hscan || !scratch || !wstart)
+        return done(set_err(MQ_ENOMEM, "join: window runs buffers (%llu rows)", (unsigned long long)n));
+    int* bp = nullptr;
+    int rc = jalloc(j, (void**)&bp, n * 4);
+    if (rc) return done(rc);
+    u64* src = nullptr;
+    u64* dst = a;
+    for (int pass = 0; pass < passes; pass++) {
+        const int shift = 8 * pass;
+        if (pass == 0)
+            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, (const u64*)nullptr, n,
+                               t, shift, hist, (uint32_t)ntiles);
+        else
+            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr, src,
+                               n, t, shift, hist, (uint32_t)ntiles);
+        if ((rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st))) return done(rc);
+        if (pass == 0)
+            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
+                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst);
+        else
+            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr,
+                               (const int*)nullptr, src, n, t, shift, hscan, (uint32_t)ntiles, dst);
+        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window partition"));
+        src = dst;
+        dst = (dst == a) ? b : a;
+    }
+    uint32_t flag = 0;
+    if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return done(set_err(MQ_EHIP, "join: memset"));
+    hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
+    hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
+    if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window runs build"));
+    if (hipMemcpyAsync(&flag, general, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return done(set_err(MQ_EHIP, "join: window runs sync"));
+    if (flag) return done(1);
+    j->unique = 2;
+    j->packed = true;
+    j->rs = nullptr;  // packed lengths stay below 15: no run is looked up
+    j->bpos = bp;
+    j->marks = !getenv("MQ_JOIN_NOMARKS");
+    return done(0);
+}
+
 // Duplicate keys: runs of the sorted build, their distinct keys into the windowed
 // unique table (payload: run index). Returns 0 (j->unique = 2), 1 when the windowed
 // build flagged (the caller takes the global-CAS run table), or an error.
@@ -1859,6 +2093,15 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
             }
             HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
+        }
+        if (dup && (rc = build_window_runs(j, d_c1, d_p1, n1, slots, dflag, st, s)) != 1) {
+            if (rc) {  // (0: the windowed runs build took it)
+                jfree_all(j);
+                delete j;
+                return rc;
+            }
+            *out = j;
+            return MQ_OK;
         }
         if (dup) {  // general path: stable sort by key, runs in insertion order
             j->unique = 0;

@@ -576,15 +576,21 @@ def _dev_join(lib, c1, p1, c2, p2):
     return o1.get(np.int32, m), o2.get(np.int32, m)
 
 
-@pytest.mark.parametrize("runs", [True, False])
+JOIN_PATHS = {"winruns": {}, "sorted": {"MQ_JOIN_WINRUNS": "0"}, "cas": {"MQ_JOIN_RUNS": "0"}}
+
+
+@pytest.mark.parametrize("path", list(JOIN_PATHS))
 @pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
                                   "unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned",
-                                  "ragged_hits"])
-def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
-    """runs: duplicate keys as sorted runs behind the windowed table of distinct keys
-    (default); MQ_JOIN_RUNS=0: the global-CAS table of run heads (the fallback)."""
-    if not runs:
-        monkeypatch.setenv("MQ_JOIN_RUNS", "0")
+                                  "ragged_hits", "dups_short_runs", "dups_run_of_15"])
+def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
+    """Duplicate keys: winruns (default) partitions the build rows by window and finds
+    each window's runs in LDS (k_win_build_runs; a window over 6144 rows or a key on
+    15+ rows falls back to:) sorted: the sorted runs behind the windowed table of
+    distinct keys (MQ_JOIN_WINRUNS=0); cas: the global-CAS table of run heads
+    (MQ_JOIN_RUNS=0, the last fallback)."""
+    for k, v in JOIN_PATHS[path].items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(hash(case) % 1000)
     if case == "unique":
         c1 = rng.permutation(200_000).astype(np.int32)
@@ -608,6 +614,18 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, runs):
     elif case == "ragged_hits":  # unique keys, probe rows 64k+1 with hits at the word edges
         c1 = rng.permutation(1000).astype(np.int32)
         c2 = np.concatenate([np.arange(129), rng.integers(500, 2000, 64 * 7 + 1), [999]]).astype(np.int32)
+    elif case == "dups_short_runs":  # > 2^16 rows, runs of 1..14 rows in input order
+        # (spread keys: the oracle's `key % size` multimap goes quadratic on dense ones)
+        keys = rng.choice(1 << 30, 90_000, replace=False).astype(np.int32)
+        c1 = np.repeat(keys[:60_000], rng.integers(1, 15, 60_000))[:300_000]
+        c1 = c1[rng.permutation(len(c1))]
+        c2 = np.concatenate([rng.choice(keys[:60_000], 100_000), keys[60_000:80_000]]).astype(np.int32)
+    elif case == "dups_run_of_15":  # one key on 15 rows: not packable, the window flags
+        keys = rng.choice(1 << 30, 250_000, replace=False).astype(np.int32)
+        c1 = keys[:200_000].copy()
+        c1[1 + rng.choice(len(c1) - 1, 14, replace=False)] = c1[0]
+        c2 = rng.choice(keys, 100_000)
+        c2[:5] = c1[0]
     elif case in ("unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned"):
         if case.endswith("nomarks"):  # the windowed table without overflow marks
             monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
@@ -733,15 +751,16 @@ def test_hash_join_goldens(lib, refcpu, goldens):
         assert (m, f"{h:016x}") == (r["m"], r["pairs_fnv1a64"]), r["n"]
 
 
-@pytest.mark.parametrize("runs", [True, False])
+@pytest.mark.parametrize("path", list(JOIN_PATHS))
 @pytest.mark.parametrize("sample", [True, False])
-def test_hash_join_dup_goldens(lib, refcpu, goldens, monkeypatch, runs, sample):
+def test_hash_join_dup_goldens(lib, refcpu, goldens, monkeypatch, path, sample):
     """Many-to-many config 5 (every build key twice, tests/golden/make_join_dup_goldens.py):
-    the duplicate-key build path against the reference's own hash_join. sample: builds
-    of 2^20 rows and up go straight to the runs build when a sample of the keys has a
-    duplicate; MQ_JOIN_SAMPLE=0: the unique attempt first, abandoned on the duplicate."""
-    if not runs:
-        monkeypatch.setenv("MQ_JOIN_RUNS", "0")
+    the duplicate-key build paths (JOIN_PATHS) against the reference's own hash_join.
+    sample: builds of 2^20 rows and up go straight to the runs build when a sample of
+    the keys has a duplicate; MQ_JOIN_SAMPLE=0: the unique attempt first, abandoned on
+    the duplicate."""
+    for k, v in JOIN_PATHS[path].items():
+        monkeypatch.setenv(k, v)
     if not sample:
         monkeypatch.setenv("MQ_JOIN_SAMPLE", "0")
     for r in goldens["join_dup"]:
