@@ -1009,6 +1009,171 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build_runs(const u64* __restric
     }
 }
 
+// The same build into 16-byte slots {key | meta << 32, p0 | p1 << 32} (meta = start << 4
+// | length, as the 8-byte table's payload): windows of 4096 slots, buckets of two
+// (32 B, one probe read), and a run of one or two rows carries its build positions
+// in the slot itself, so the probe's bucket read brings them and the write streams
+// them instead of reading the run array at random (longer runs are still looked up
+// there). As many slots as the 8-byte table (2^29 at 2^28 build rows: the 2^27
+// distinct keys of config 5 at load 1/4, 8 GB), windows of 8192 (the same partition;
+// 128 KB of LDS, one block a CU): at load 1/2 (half the slots, windows of 4096) the
+// two-slot buckets sent so many probes on along the window that the probe lost what
+// the write gained (9.9 vs 7.2 ms, write 1.4 vs 3.9). A window of more than 6144
+// distinct keys (3/4 full) flags as well.
+constexpr uint32_t kWin16Log = 13;
+constexpr uint32_t kBucket16 = 2;
+constexpr uint32_t kKeys16 = 6144;
+
+__device__ __forceinline__ uint64_t ht_home16(uint32_t key, uint64_t mask) {
+    return hash32(key) & mask & ~(uint64_t)(kBucket16 - 1);
+}
+
+__global__ __launch_bounds__(kWinTPB) void k_win_build_runs16(const u64* __restrict__ in,
+                                                              const uint32_t* __restrict__ wstart,
+                                                              ulonglong2* __restrict__ slots, int* __restrict__ bpos,
+                                                              Win t, uint32_t* __restrict__ general) {
+    constexpr uint32_t W = 1u << kWin16Log;
+    constexpr int kPer = (int)(kRunRows / kWinTPB);
+    constexpr int kW = kWinTPB / 64;
+    __shared__ uint32_t tab[W];          // keys by slot
+    __shared__ uint32_t c32[W / 2];      // u16 per slot: counts, then run places
+    __shared__ u64 pos2[W];              // a short run's build positions by slot
+    __shared__ uint16_t pidx[kRunRows];  // input index (within the window) by place
+    __shared__ uint8_t ovf[W / kBucket16];
+    __shared__ uint32_t wsum[kW + 2];    // wave totals, the flag, the distinct keys
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t w = blockIdx.x;
+    const uint32_t b = wstart[w], e = wstart[w + 1], c = e - b;
+    if (W != (uint32_t)t.wmask + 1 || c > kRunRows) {
+        if (tid == 0) *general = 1;
+        return;
+    }
+    for (uint32_t x = tid; x < W; x += kWinTPB) tab[x] = kEmpty32, pos2[x] = 0ull;
+    for (uint32_t x = tid; x < W / 2; x += kWinTPB) c32[x] = 0;
+    for (uint32_t x = tid; x < W / kBucket16; x += kWinTPB) ovf[x] = 0;
+    if (tid == 0) wsum[kW] = 0, wsum[kW + 1] = 0;
+    __syncthreads();
+    uint32_t key[kPer], pay[kPer], slot[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        const u64 v = i < c ? in[b + i] : 0ull;
+        key[k] = (uint32_t)v;
+        pay[k] = (uint32_t)(v >> 32);
+    }
+    bool bad = false;
+    uint32_t fresh = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        slot[k] = 0;
+        if ((uint32_t)k * kWinTPB + tid >= c) continue;
+        if (key[k] == kEmpty32) {
+            bad = true;
+            continue;
+        }
+        const uint32_t h0 = (uint32_t)ht_home16(key[k], t.wmask);
+        uint32_t h = h0;
+        for (uint32_t step = 0; step < W; step++) {
+            const uint32_t old = atomicCAS(&tab[h], kEmpty32, key[k]);
+            if (old == kEmpty32 || old == key[k]) {
+                if (old == kEmpty32) {
+                    fresh++;
+                    if (step >= kBucket16) ovf[h0 / kBucket16] = 1;
+                }
+                break;
+            }
+            h = (h + 1) & (W - 1);
+        }
+        slot[k] = h;
+        atomicAdd(&c32[h >> 1], 1u << (16 * (h & 1)));
+    }
+    if (bad) wsum[kW] = 1;
+    if (fresh) atomicAdd(&wsum[kW + 1], fresh);
+    __syncthreads();
+    constexpr int kQ = (int)(W / 2 / kWinTPB);
+    uint32_t* mine = c32 + (uint32_t)tid * kQ;
+    uint32_t tot = 0, mx = 0;
+#pragma unroll
+    for (int j = 0; j < kQ; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu, hi = cell >> 16;
+        mx = lo > mx ? lo : mx;
+        mx = hi > mx ? hi : mx;
+        tot += lo + hi;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    if (__ballot(mx >= 15u)) wsum[kW] = 1;
+    __syncthreads();
+    if (wsum[kW] || wsum[kW + 1] > kKeys16) {
+        if (tid == 0) *general = 1;
+        return;
+    }
+    uint32_t run = incl - tot;
+    for (int v = 0; v < wave; v++) run += wsum[v];
+#pragma unroll
+    for (int j = 0; j < kQ; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu;
+        mine[j] = run | ((run + lo) << 16);
+        run += lo + (cell >> 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        if (i >= c) continue;
+        const uint32_t h = slot[k], sh = 16 * (h & 1);
+        pidx[(atomicAdd(&c32[h >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)i;
+    }
+    __syncthreads();
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
+    uint32_t* p32 = reinterpret_cast<uint32_t*>(pos2);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        if (i >= c) continue;
+        const uint32_t h = slot[k];
+        const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
+        uint32_t r = 0;
+        for (uint32_t q = s0; q < s1; q++) r += pidx[q] < i;
+        if (s1 - s0 <= 2u)
+            p32[2 * h + r] = pay[k];
+        else
+            bpos[b + s0 + r] = (int)pay[k];
+    }
+    __syncthreads();
+    ulonglong2* dst = slots + (uint64_t)w * W;
+    for (uint32_t bk = tid; bk < W / kBucket16; bk += kWinTPB) {
+        ulonglong2 o[kBucket16];
+        bool full = true;
+#pragma unroll
+        for (uint32_t q = 0; q < kBucket16; q++) {
+            const uint32_t h = bk * kBucket16 + q;
+            const uint32_t k = tab[h];
+            if (k == kEmpty32) {
+                o[q].x = kEmpty;
+                o[q].y = 0ull;
+                full = false;
+            } else {
+                const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
+                o[q].x = (u64)k | ((u64)(((b + s0) << 4) | (s1 - s0)) << 32);
+                o[q].y = pos2[h];
+            }
+        }
+        if (full && (((uint32_t)o[0].x > (uint32_t)o[1].x) != (ovf[bk] != 0))) {
+            const ulonglong2 x = o[0];
+            o[0] = o[1];
+            o[1] = x;
+        }
+        dst[bk * kBucket16] = o[0];
+        dst[bk * kBucket16 + 1] = o[1];
+    }
+}
+
 // 2 probes per thread per step: with whole-bucket loads 2 beat 8 (8.25 vs 8.8 ms at
 // 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8 had beaten 1.
 constexpr int kProbeILP = 2;
@@ -1066,13 +1231,18 @@ __device__ __forceinline__ uint32_t run_len(uint32_t payload, const uint32_t* __
 // RUNS (duplicate keys as runs, the payload a packed run, see run_payload): per row
 // the run's start in pstart and its length in cnt (0 = no match) instead of hit
 // words. Row indices and steps are kept as u32 (n2 <= 2^31 rows).
-template <bool RUNS>
+template <bool RUNS, bool S16 = false>
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
                                                           u64* __restrict__ hits, const uint32_t* __restrict__ rs,
                                                           uint32_t* __restrict__ cnt, bool packed, bool marks,
-                                                          uint32_t* __restrict__ wcnt) {
+                                                          uint32_t* __restrict__ wcnt, u64* __restrict__ p01) {
+    // S16: the 16-byte-slot runs table (k_win_build_runs16): buckets of two slots, and a
+    // hit's slot also brings the short run's build positions (p01 per row)
+    constexpr uint32_t kB = S16 ? kBucket16 : kBucket;
+    auto home = [&](uint32_t key) { return S16 ? ht_home16(key, t.mask) : ht_home(key, t.mask); };
+    const ulonglong2* __restrict__ words16 = reinterpret_cast<const ulonglong2*>(words);
     __shared__ uint32_t q_j[kTPB / 64][kContCap], q_h[kTPB / 64][kContCap], q_k[kTPB / 64][kContCap];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* const qj = q_j[wave];
@@ -1093,11 +1263,11 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
     // a queued row: cj, its key ck and ch, the slot it is at as steps from its home
     // slot (kBucket.. W-1); the slot itself is recomputed from the key
     auto cont_slot = [&](uint32_t ck, uint32_t ch) {
-        const uint64_t hh = ht_home(ck, t.mask);
+        const uint64_t hh = home(ck);
         return (hh & ~t.wmask) | ((hh + ch) & t.wmask);
     };
     // a continuation: row cj at step ch with key ck (lanes < ntake hold one)
-    auto cont_resolve = [&](bool has, uint32_t cj, uint32_t ch, uint32_t ck, u64 c) {
+    auto cont_resolve = [&](bool has, uint32_t cj, uint32_t ch, uint32_t ck, u64 c, u64 cy) {
         // c: the slot's word. Resolved on the key or an empty slot; otherwise requeued.
         bool again = false;
         if (has) {
@@ -1107,6 +1277,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                 if (RUNS || hit) probe_emit<RUNS>(cj, hit, payload, pstart, rs, cnt, packed);
                 if (!RUNS && hit) atomicOr(&hits[cj >> 6], 1ull << (cj & 63));  // word stored in an earlier step
                 if (RUNS && wcnt && hit) atomicAdd(&wcnt[cj >> 6], run_len(payload, rs));  // likewise
+                if (S16) p01[cj] = hit ? cy : 0ull;
             } else {
                 again = true;
             }
@@ -1138,13 +1309,20 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             ck = qk[e];
         }
         nq -= ntake;
-        u64 c = 0;
-        if (has) c = words[cont_slot(ck, ch)];
+        u64 c = 0, cy = 0;
+        if (has) {
+            if constexpr (S16) {
+                const ulonglong2 v = words16[cont_slot(ck, ch)];
+                c = v.x, cy = v.y;
+            } else {
+                c = words[cont_slot(ck, ch)];
+            }
+        }
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             key[u] = knext[u];
-            h[u] = ht_home(key[u], t.mask);
-            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(words + h[u]);
+            h[u] = home(key[u]);
+            const ulonglong2* q = S16 ? words16 + h[u] : reinterpret_cast<const ulonglong2*>(words + h[u]);
             b0[u] = q[0];
             b1[u] = q[1];
         }
@@ -1153,19 +1331,24 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             const uint64_t j = j0 + stride + (uint64_t)u * kTPB;
             knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
         }
-        cont_resolve(has, cj, ch, ck, c);
+        cont_resolve(has, cj, ch, ck, c, cy);
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
-            const u64 sl[kBucket] = {b0[u].x, b0[u].y, b1[u].x, b1[u].y};
+            // the bucket's slot words (S16: the key words of its two 16-byte slots)
+            const u64 sl[4] = {b0[u].x, S16 ? b1[u].x : b0[u].y, b1[u].x, b1[u].y};
             bool hit = false, done = j >= n2;
             uint32_t payload = 0;
+            u64 py = 0;
 #pragma unroll
-            for (uint32_t i = 0; i < kBucket; i++) {
+            for (uint32_t i = 0; i < kB; i++) {
                 if (done) break;
                 const u64 w = sl[i];
                 if (w == kEmpty) done = true;
-                else if ((uint32_t)w == key[u]) hit = done = true, payload = (uint32_t)(w >> 32);
+                else if ((uint32_t)w == key[u]) {
+                    hit = done = true, payload = (uint32_t)(w >> 32);
+                    if (S16) py = i ? b1[u].y : b0[u].y;
+                }
             }
             // a full bucket without the key: on along the window, unless its mark
             // says no key homed here went on (j < n2 here)
@@ -1174,11 +1357,12 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             if (defer) {
                 const uint32_t at = nq + (uint32_t)__popcll(dm & lt);
                 qj[at] = (uint32_t)j;
-                qh[at] = kBucket;
+                qh[at] = kB;
                 qk[at] = key[u];
             }
             nq += (uint32_t)__popcll(dm);
             if (j < n2 && !defer) probe_emit<RUNS>(j, hit, payload, pstart, rs, cnt, packed);
+            if (S16 && j < n2 && !defer) p01[j] = py;
             if (RUNS && wcnt) {
                 // packed runs: the word's run lengths, summed over the wave (a deferred
                 // row adds its own when it resolves), so no pass re-reads the payloads
@@ -1200,14 +1384,19 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             const uint32_t nt = nq < 64 ? nq : 64;
             const bool hs = (uint32_t)lane < nt;
             uint32_t dj = 0, dh = 0, dk = 0;
-            u64 dc = 0;
+            u64 dc = 0, dy = 0;
             if (hs) {
                 const uint32_t e = nq - nt + (uint32_t)lane;
                 dj = qj[e], dh = qh[e], dk = qk[e];
-                dc = words[cont_slot(dk, dh)];
+                if constexpr (S16) {
+                    const ulonglong2 v = words16[cont_slot(dk, dh)];
+                    dc = v.x, dy = v.y;
+                } else {
+                    dc = words[cont_slot(dk, dh)];
+                }
             }
             nq -= nt;
-            cont_resolve(hs, dj, dh, dk, dc);
+            cont_resolve(hs, dj, dh, dk, dc, dy);
         }
     }
     // the queue's rest
@@ -1215,14 +1404,19 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
         const uint32_t nt = nq < 64 ? nq : 64;
         const bool hs = (uint32_t)lane < nt;
         uint32_t dj = 0, dh = 0, dk = 0;
-        u64 dc = 0;
+        u64 dc = 0, dy = 0;
         if (hs) {
             const uint32_t e = nq - nt + (uint32_t)lane;
             dj = qj[e], dh = qh[e], dk = qk[e];
-            dc = words[cont_slot(dk, dh)];
+            if constexpr (S16) {
+                const ulonglong2 v = words16[cont_slot(dk, dh)];
+                dc = v.x, dy = v.y;
+            } else {
+                dc = words[cont_slot(dk, dh)];
+            }
         }
         nq -= nt;
-        cont_resolve(hs, dj, dh, dk, dc);
+        cont_resolve(hs, dj, dh, dk, dc, dy);
     }
 }
 
@@ -1443,6 +1637,61 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs_mlp(const uint32_t* __
     }
 }
 
+// The write after a 16-byte-slot probe: a run of one or two rows comes from the
+// probe's per-row positions (p01, a stream), a longer one (3..14 rows) from the run
+// array as before.
+template <int kWriteWords>
+__global__ __launch_bounds__(kTPB) void k_join_write_runs16(const uint32_t* __restrict__ pk, uint64_t n2,
+                                                            const u64* __restrict__ woffs, const int* __restrict__ p2,
+                                                            const u64* __restrict__ p01, const int* __restrict__ bpos,
+                                                            int* __restrict__ out1, int* __restrict__ out2) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (n2 + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64) * kWriteWords;
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6)) * kWriteWords; w0 < nw;
+         w0 += wstride) {
+        uint32_t L[kWriteWords], a[kWriteWords];
+        u64 o[kWriteWords], pq[kWriteWords];
+        int pp[kWriteWords];
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            const uint64_t j = (w0 + u) * 64 + (uint64_t)lane;
+            const uint32_t m = j < n2 ? pk[j] : 0u;
+            pq[u] = j < n2 ? p01[j] : 0ull;
+            pp[u] = j < n2 ? p2[j] : 0;
+            L[u] = m & 15u;
+            a[u] = m >> 4;
+        }
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            uint32_t incl = L[u];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            o[u] = (w0 + u < nw ? woffs[w0 + u] : 0ull) + (u64)(incl - L[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kWriteWords; u++) {
+            if (!L[u]) continue;
+            if (L[u] <= 2u) {
+                out1[o[u]] = (int)(uint32_t)pq[u];
+                out2[o[u]] = pp[u];
+                if (L[u] == 2u) {
+                    out1[o[u] + 1] = (int)(uint32_t)(pq[u] >> 32);
+                    out2[o[u] + 1] = pp[u];
+                }
+            } else {
+                for (uint32_t t = 0; t < L[u]; t++) {
+                    out1[o[u] + t] = bpos[a[u] + t];
+                    out2[o[u] + t] = pp[u];
+                }
+            }
+        }
+    }
+}
+
 // ---- duplicate keys as runs (the build sorted by key, stable: a key's rows are one
 // run in insertion order); the distinct keys go into the windowed unique table with
 // their run index as payload ----
@@ -1586,8 +1835,12 @@ struct mq_join {
     const int* bpos;       // build positions in run order (p1 itself, or sorted copy)
     void* owned[8];        // device allocations owned by the handle
     int nowned;
+    bool slot16;           // unique == 2: the 16-byte-slot table words16 (k_win_build_runs16), geometry win16
+    Win win16;
+    ulonglong2* words16;
     // probe state
     uint64_t n2, m;
+    u64* p01;              // slot16: per probe row, a short run's build positions
     uint32_t* pstart;
     uint32_t* plen;
     u64* offs;
@@ -1744,11 +1997,19 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     const char* e = getenv("MQ_JOIN_WINRUNS");  // "0": the sorted-runs build (A/B, tests)
     const char* r = getenv("MQ_JOIN_RUNS");     // "0": the global-CAS run table (tests)
     if ((e && e[0] == '0') || (r && r[0] == '0') || n < kWindowBuildRows || n > (1ull << 28) || j->win.wlog != kWinLog) return 1;
+    // MQ_JOIN_SLOT16=1: the 16-byte-slot table (k_win_build_runs16: as many slots, in a
+    // table of their own, same windows and partition). Measured and kept off: at 2^28
+    // many-to-many the write falls 3.93 -> 1.38 ms but the build rises 5.5 -> 7.2 (8 GB
+    // of table, one block a CU) and the probe 7.2 -> 8.4 ms (two-slot buckets): 16.9
+    // against 16.7 ms in total.
+    const char* e16 = getenv("MQ_JOIN_SLOT16");
+    const bool s16 = e16 && e16[0] == '1';
     const Win t = j->win;
+    const uint64_t nslot = slots;
     int lg = 0;
-    while ((1ull << lg) < slots) lg++;
+    while ((1ull << lg) < nslot) lg++;
     const int passes = (lg - t.wlog + 7) / 8;
-    const uint32_t nw = (uint32_t)(slots >> t.wlog);
+    const uint32_t nw = (uint32_t)(nslot >> t.wlog);
     const uint64_t ntiles = ceil_div(n, kSortTile);
     const uint64_t nh = ntiles * kRadix;
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
@@ -1772,6 +2033,7 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
         return done(set_err(MQ_ENOMEM, "join: window runs buffers (%llu rows)", (unsigned long long)n));
     int* bp = nullptr;
     int rc = jalloc(j, (void**)&bp, n * 4);
+    if (!rc && s16) rc = jalloc(j, (void**)&j->words16, slots * 16);
     if (rc) return done(rc);
     u64* src = nullptr;
     u64* dst = a;
@@ -1797,7 +2059,11 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     uint32_t flag = 0;
     if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return done(set_err(MQ_EHIP, "join: memset"));
     hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
-    hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
+    if (s16)
+        hipLaunchKernelGGL(k_win_build_runs16, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words16, bp, t,
+                           general);
+    else
+        hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
     if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window runs build"));
     if (hipMemcpyAsync(&flag, general, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -1805,6 +2071,8 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     if (flag) return done(1);
     j->unique = 2;
     j->packed = true;
+    j->slot16 = s16;
+    j->win16 = t;
     j->rs = nullptr;  // packed lengths stay below 15: no run is looked up
     j->bpos = bp;
     j->marks = !getenv("MQ_JOIN_NOMARKS");
@@ -2153,6 +2421,8 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (n2 > (1ull << 31)) return set_err(MQ_EINVAL, "mq_join_probe: %llu rows (int32 positions)", (unsigned long long)n2);
     hipStream_t st = (hipStream_t)stream;
     if (j->pstart) HIPCHK(hipDeviceSynchronize());  // a queued write may still read them
+    pool_free(j->p01);
+    j->p01 = nullptr;
     pool_free(j->pstart);
     pool_free(j->plen);
     pool_free(j->offs);
@@ -2177,23 +2447,32 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     const uint64_t nw = (n2 + 63) / 64;
     const uint64_t nscan = words_scan ? nw : n2;
     uint32_t* const cnt = j->unique == 1 ? j->plen + 2 * nw : j->plen;
-    if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
+    if (pruns && j->slot16) {  // 16-byte slots: payloads, short runs' positions, word run lengths
+        if (!(j->p01 = (u64*)pool_alloc(n2 * 8))) return set_err(MQ_ENOMEM, "mq_join_probe: positions");
+        auto kern = k_ht_probe_unique<true, true>;
+        hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB),
+                           0, st, d_c2, n2, reinterpret_cast<const u64*>(j->words16), j->win16, j->pstart,
+                           (u64*)nullptr, j->rs, (uint32_t*)nullptr,
+                           true, j->marks, cnt, j->p01);
+        LAUNCHCHK("k_ht_probe_unique");
+    } else if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks, cnt);
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks, cnt,
+                           (u64*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks,
-                           (uint32_t*)nullptr);
+                           (uint32_t*)nullptr, (u64*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
         auto kern = k_ht_probe_unique<false>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false, j->marks,
-                           (uint32_t*)nullptr);
+                           (uint32_t*)nullptr, (u64*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
         hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
         LAUNCHCHK("k_hits_count");
@@ -2224,6 +2503,12 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                            reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
         LAUNCHCHK("k_join_write_hits");
+        return MQ_OK;
+    }
+    if (j->unique == 2 && j->packed && j->slot16) {
+        hipLaunchKernelGGL(k_join_write_runs16<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)), dim3(kTPB), 0,
+                           (hipStream_t)stream, j->pstart, j->n2, j->offs, d_p2, j->p01, j->bpos, d_out1, d_out2);
+        LAUNCHCHK("k_join_write_runs16");
         return MQ_OK;
     }
     if (j->unique == 2 && j->packed) {
@@ -2267,6 +2552,7 @@ int mq_random_read(const uint64_t* d_table, int slots_log2, uint64_t n_reads, vo
 int mq_join_free(mq_join* j) {
     if (!j) return MQ_OK;
     (void)hipDeviceSynchronize();  // queued probe/write kernels may still use the buffers
+    pool_free(j->p01);
     pool_free(j->pstart);
     pool_free(j->plen);
     pool_free(j->offs);
