@@ -928,8 +928,8 @@ def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = 
     m, t = run(n, False)
     res = {"n_build": n, "n_probe": n, "m": m, "ms": 1e3 * t, "rows_per_s": 2 * n / t,
            "algorithmic_bytes": 16 * n + 8 * m, "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9,
-           "parity_2e22": ok, "note": "wall time incl. the unique-key attempt, its restart on the "
-                                      "duplicate flag, and 2 host syncs"}
+           "parity_2e22": ok, "note": "wall time incl. the duplicate-key sample, the per-window runs "
+                                      "build (k_win_build_runs) and 2 host syncs"}
     if cpu and refcpu.have_reference():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from refapi import Api
