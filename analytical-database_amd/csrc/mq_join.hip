@@ -970,19 +970,11 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build_runs(const u64* __restric
         pidx[place[k]] = (uint16_t)i;
     }
     __syncthreads();
-    // c32 now holds each slot's run end; its run starts where slot h - 1's ends
+    // c32 now holds each slot's run end; its run starts where slot h - 1's ends.
+    // The window's table words first, a bucket (4 slots) per thread, with the overflow
+    // marks; then tab's space stages the payloads by final place, so the run array
+    // leaves in one coalesced copy (the rows' own stores were scattered 4-byte writes)
     const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        const uint32_t i = (uint32_t)k * kWinTPB + tid;
-        if (i >= c) continue;
-        const uint32_t h = slot[k];
-        const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
-        uint32_t r = 0;
-        for (uint32_t q = s0; q < s1; q++) r += pidx[q] < i;
-        bpos[b + s0 + r] = (int)pay[k];
-    }
-    // the window's table words, a bucket (4 slots) per thread, with the overflow marks
     u64* dst = words + (uint64_t)w * W;
     for (uint32_t bk = tid; bk < W / kBucket; bk += kWinTPB) {
         u64 o[kBucket];
@@ -1007,6 +999,20 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build_runs(const u64* __restric
 #pragma unroll
         for (uint32_t q = 0; q < kBucket; q++) dst[bk * kBucket + q] = o[q];
     }
+    __syncthreads();
+    uint32_t* stage = tab;  // (W >= kRunRows)
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t i = (uint32_t)k * kWinTPB + tid;
+        if (i >= c) continue;
+        const uint32_t h = slot[k];
+        const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
+        uint32_t r = 0;
+        for (uint32_t q = s0; q < s1; q++) r += pidx[q] < i;
+        stage[s0 + r] = pay[k];
+    }
+    __syncthreads();
+    for (uint32_t x = tid; x < c; x += kWinTPB) bpos[b + x] = (int)stage[x];
 }
 
 // The same build into 16-byte slots {key | meta << 32, p0 | p1 << 32} (meta = start << 4
