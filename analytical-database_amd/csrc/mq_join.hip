@@ -2520,9 +2520,13 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (j->unique == 2 && j->packed) {
         // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, default eight
         const char* wf = getenv("MQ_JOIN_WRITE");
-        if (wf && wf[0] == '1')
+        if (wf && wf[0] == '1' && wf[1] == 0)
             hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
                                (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
+        else if (wf && wf[0] == '1' && wf[1] == '6')
+            hipLaunchKernelGGL(k_join_write_runs_mlp<16>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 16)),
+                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
+                               d_out1, d_out2);
         else if (wf && wf[0] == '4')
             hipLaunchKernelGGL(k_join_write_runs_mlp<4>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 4)),
                                dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
