@@ -2518,7 +2518,8 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         return MQ_OK;
     }
     if (j->unique == 2 && j->packed) {
-        // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, default eight
+        // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, "16" sixteen
+        // (176 VGPRs, two waves a SIMD; not measured yet), default eight
         const char* wf = getenv("MQ_JOIN_WRITE");
         if (wf && wf[0] == '1' && wf[1] == 0)
             hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
