@@ -43,6 +43,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -105,10 +106,52 @@ static void install(void) {
     if (sigaction(SIGSEGV, &sa, &g_prev) == 0) g_installed = 1;
 }
 
+/* Per thread, the address it last returned for without an armed guard (a second
+ * fault there in a row is not a race with another handler, so it is handed on).
+ * Kept in a lock-free table keyed by thread id rather than in TLS: libmq is
+ * dlopen'd, so its TLS is dynamic, and a thread's first __tls_get_addr may allocate,
+ * which a signal handler must not do (initial-exec TLS would move the library's
+ * whole TLS block into the static surplus, which dlopen refuses). A slot is one
+ * word, tid << 32 | h(address), h != 0; a slot whose h is 0 is idle and may be taken
+ * by any thread. Every update is a CAS. */
+#define NRETRY 1024
+static _Atomic uint64_t g_retry[NRETRY];
+
+static uint32_t addr_tag(uintptr_t a) { return ((uint32_t)a ^ (uint32_t)((uint64_t)a >> 32)) | 1u; }
+
+static uint32_t retry_get(uint32_t tid) {
+    for (int i = 0; i < NRETRY; i++) {
+        const uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
+        if ((uint32_t)(v >> 32) == tid) return (uint32_t)v;
+    }
+    return 0;
+}
+
+/* Record h (0 = clear) for tid; 0 when there was no room (the caller must not count
+ * on a retry being remembered then). */
+static int retry_set(uint32_t tid, uint32_t h) {
+    const uint64_t want = ((uint64_t)tid << 32) | h;
+    for (int pass = 0; pass < 4; pass++) {
+        for (int i = 0; i < NRETRY; i++) {
+            uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
+            if ((uint32_t)(v >> 32) != tid) continue;
+            if (atomic_compare_exchange_strong(&g_retry[i], &v, want)) return 1;
+            goto again; /* taken from under us (it was idle): look again */
+        }
+        if (h == 0) return 1; /* nothing recorded for this thread: already clear */
+        for (int i = 0; i < NRETRY; i++) {
+            uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
+            if ((uint32_t)v != 0) continue;
+            if (atomic_compare_exchange_strong(&g_retry[i], &v, want)) return 1;
+        }
+        return 0;
+    again:;
+    }
+    return 0;
+}
+
 static void on_segv(int sig, siginfo_t* si, void* uc) {
-    /* the address this thread last returned for without an armed guard: a second
-     * fault there in a row is not a race with another handler, so it is handed on */
-    static __thread uintptr_t t_retry;
+    const uint32_t tid = (uint32_t)syscall(SYS_gettid);
     const uintptr_t a = (uintptr_t)si->si_addr;
     int hit = 0, covered = 0;
     if (si->si_code == SEGV_ACCERR) {
@@ -127,17 +170,14 @@ static void on_segv(int sig, siginfo_t* si, void* uc) {
         }
     }
     if (hit) {
-        t_retry = 0;
+        (void)retry_set(tid, 0);
         return;
     }
     /* Another thread's fault on the same guard (or a release) already gave the pages
      * their protection back between this fault and the scan: re-execute the store
      * once. A slot of any live state covering the address says so. */
-    if (covered && t_retry != a) {
-        t_retry = a;
-        return;
-    }
-    t_retry = 0;
+    if (covered && retry_get(tid) != addr_tag(a) && retry_set(tid, addr_tag(a))) return;
+    (void)retry_set(tid, 0);
     /* not ours: hand it on as if we were not here */
     if (g_prev.sa_flags & SA_SIGINFO) {
         if (g_prev.sa_sigaction) {

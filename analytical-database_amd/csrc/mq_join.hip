@@ -1516,20 +1516,60 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe(const int* __restrict__ pkeys
     }
 }
 
+// Per-row runs (the sorted-runs and global-CAS builds). A run longer than kLongRun
+// rows (a hot key) is not copied by its one lane: the lane lists it as chunks of
+// kLongChunk pairs (entry = row << 32 | chunk) and k_join_write_long copies each chunk
+// with a whole block, coalesced. (One lane writing a 2^26-row run alone took the wave
+// 2^26 dependent iterations.)
+constexpr uint32_t kLongRun = 4096;
+constexpr uint32_t kLongChunk = 65536;
+
 __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict__ pstart,
                                                      const uint32_t* __restrict__ plen,
                                                      const u64* __restrict__ offs,
                                                      const int* __restrict__ p2,
                                                      const int* __restrict__ bpos, uint64_t n2,
-                                                     int* __restrict__ out1, int* __restrict__ out2) {
+                                                     int* __restrict__ out1, int* __restrict__ out2,
+                                                     u64* __restrict__ longq, uint32_t* __restrict__ nlong) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
         const uint32_t L = plen[j];
         if (!L) continue;
+        if (L > kLongRun) {
+            const uint32_t nch = (L + kLongChunk - 1) / kLongChunk;
+            const uint32_t at = atomicAdd(nlong, nch);
+            for (uint32_t c = 0; c < nch; c++) longq[at + c] = (j << 32) | c;
+            continue;
+        }
         const u64 o = offs[j];
         const uint32_t s = pstart[j];
         const int pp = p2[j];
         for (uint32_t t = 0; t < L; t++) {
+            out1[o + t] = bpos[s + t];
+            out2[o + t] = pp;
+        }
+    }
+}
+
+// The listed chunks of long runs, one block per chunk (grid-stride over the list,
+// whose length k_join_write left in *nlong).
+__global__ __launch_bounds__(kTPB) void k_join_write_long(const uint32_t* __restrict__ pstart,
+                                                          const uint32_t* __restrict__ plen,
+                                                          const u64* __restrict__ offs, const int* __restrict__ p2,
+                                                          const int* __restrict__ bpos, const u64* __restrict__ longq,
+                                                          const uint32_t* __restrict__ nlong, int* __restrict__ out1,
+                                                          int* __restrict__ out2) {
+    const uint32_t n = *nlong;
+    for (uint32_t e = blockIdx.x; e < n; e += gridDim.x) {
+        const u64 q = longq[e];
+        const uint64_t j = q >> 32;
+        const uint32_t c = (uint32_t)q;
+        const uint32_t L = plen[j];
+        const uint32_t a = c * kLongChunk, b = L - a < kLongChunk ? L : a + kLongChunk;
+        const u64 o = offs[j];
+        const uint32_t s = pstart[j];
+        const int pp = p2[j];
+        for (uint32_t t = a + threadIdx.x; t < b; t += kTPB) {
             out1[o + t] = bpos[s + t];
             out2[o + t] = pp;
         }
@@ -1839,8 +1879,9 @@ struct mq_join {
     uint32_t* start;
     uint32_t* len;
     const int* bpos;       // build positions in run order (p1 itself, or sorted copy)
-    void* owned[8];        // device allocations owned by the handle
+    void* owned[12];       // device allocations owned by the handle
     int nowned;
+    bool pruns;            // the last probe took the per-64-row-word form (packed runs of < 15 rows)
     bool slot16;           // unique == 2: the 16-byte-slot table words16 (k_win_build_runs16), geometry win16
     Win win16;
     ulonglong2* words16;
@@ -1851,15 +1892,26 @@ struct mq_join {
     uint32_t* plen;
     u64* offs;
     u64* scan_scratch;
+    u64* longq;            // per-row write: chunks of the long runs (k_join_write_long)
 };
 
 namespace {
 
+int jown(mq_join* j, void* p) {
+    if (j->nowned >= (int)(sizeof(j->owned) / sizeof(j->owned[0]))) {
+        pool_free(p);
+        return set_err(MQ_EINVAL, "join: handle owns too many allocations");
+    }
+    j->owned[j->nowned++] = p;
+    return MQ_OK;
+}
+
 int jalloc(mq_join* j, void** p, size_t bytes) {
     *p = pool_alloc(bytes);
     if (!*p) return set_err(MQ_ENOMEM, "join: device allocation of %zu bytes failed", bytes);
-    j->owned[j->nowned++] = *p;
-    return MQ_OK;
+    const int rc = jown(j, *p);
+    if (rc) *p = nullptr;
+    return rc;
 }
 
 void jfree_all(mq_join* j) {
@@ -2037,10 +2089,17 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     wstart = (uint32_t*)pool_alloc(((uint64_t)nw + 1) * 4);
     if (!a || (passes > 1 && !b) || !hist || !hscan || !scratch || !wstart)
         return done(set_err(MQ_ENOMEM, "join: window runs buffers (%llu rows)", (unsigned long long)n));
-    int* bp = nullptr;
-    int rc = jalloc(j, (void**)&bp, n * 4);
-    if (!rc && s16) rc = jalloc(j, (void**)&j->words16, slots * 16);
-    if (rc) return done(rc);
+    // bp and words16 join the handle only when the build takes this path
+    int* bp = (int*)pool_alloc(n * 4);
+    ulonglong2* w16 = s16 ? (ulonglong2*)pool_alloc(slots * 16) : nullptr;
+    auto drop = [&](int rc) {
+        if (rc) (void)hipStreamSynchronize(st);  // (launched work may still use them)
+        pool_free(bp);
+        pool_free(w16);
+        return done(rc);
+    };
+    int rc = MQ_OK;
+    if (!bp || (s16 && !w16)) return drop(set_err(MQ_ENOMEM, "join: window runs outputs (%llu rows)", (unsigned long long)n));
     u64* src = nullptr;
     u64* dst = a;
     for (int pass = 0; pass < passes; pass++) {
@@ -2051,36 +2110,44 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
         else
             hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr, src,
                                n, t, shift, hist, (uint32_t)ntiles);
-        if ((rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st))) return done(rc);
+        if ((rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st))) return drop(rc);
         if (pass == 0)
             hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
                                (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst);
         else
             hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr,
                                (const int*)nullptr, src, n, t, shift, hscan, (uint32_t)ntiles, dst);
-        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window partition"));
+        if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window partition"));
         src = dst;
         dst = (dst == a) ? b : a;
     }
     uint32_t flag = 0;
-    if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return done(set_err(MQ_EHIP, "join: memset"));
+    if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return drop(set_err(MQ_EHIP, "join: memset"));
     hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
     if (s16)
-        hipLaunchKernelGGL(k_win_build_runs16, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words16, bp, t,
-                           general);
+        hipLaunchKernelGGL(k_win_build_runs16, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, w16, bp, t, general);
     else
         hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
-    if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window runs build"));
+    if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window runs build"));
     if (hipMemcpyAsync(&flag, general, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
-        return done(set_err(MQ_EHIP, "join: window runs sync"));
-    if (flag) return done(1);
+        return drop(set_err(MQ_EHIP, "join: window runs sync"));
+    if (flag) return drop(1);
+    int* const bpos = bp;
+    bp = nullptr;  // (jown frees it itself when it fails)
+    if ((rc = jown(j, bpos))) return drop(rc);
+    if (w16) {
+        ulonglong2* const w = w16;
+        w16 = nullptr;
+        if ((rc = jown(j, w))) return drop(rc);
+        j->words16 = w;
+    }
     j->unique = 2;
     j->packed = true;
     j->slot16 = s16;
     j->win16 = t;
     j->rs = nullptr;  // packed lengths stay below 15: no run is looked up
-    j->bpos = bp;
+    j->bpos = bpos;
     j->marks = !getenv("MQ_JOIN_NOMARKS");
     return done(0);
 }
@@ -2386,8 +2453,12 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
                 delete j;
                 return rc;
             }
-            j->owned[j->nowned++] = skeys;
-            j->owned[j->nowned++] = svals;
+            if ((rc = jown(j, skeys)) || (rc = jown(j, svals))) {
+                if (rc && j->owned[j->nowned - 1] != skeys) pool_free(svals);  // (skeys refused: svals still ours)
+                jfree_all(j);
+                delete j;
+                return rc;
+            }
             j->bpos = reinterpret_cast<const int*>(svals);
             if ((rc = build_runs(j, skeys, n1, slots, dflag, st, s)) != 1) {  // 0: done, else an error
                 if (rc) {
@@ -2440,7 +2511,13 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     *h_m = 0;
     if (n2 == 0 || j->n1 == 0) return MQ_OK;
     const uint64_t nwords = (n2 + 63) / 64;
-    const bool pruns = j->unique == 2 && j->packed;  // packed runs: per-word lengths
+    // packed runs: per-word lengths. Only for the windowed runs build (rs == nullptr:
+    // every run shorter than 15 rows), where a word's 64 rows sum to < 2^10; a sorted
+    // runs build may hold runs of up to n1 rows, whose sums over a word would wrap the
+    // u32 word counts and the write's u32 wave prefix, so it takes the per-row form
+    // (u32 lengths, u64 offsets).
+    const bool pruns = j->unique == 2 && j->packed && j->rs == nullptr;
+    j->pruns = pruns;
     const bool words_scan = j->unique == 1 || pruns;  // per 64-row word; else per row
     j->pstart = (uint32_t*)pool_alloc(n2 * 4);
     j->plen = (uint32_t*)pool_alloc(j->unique == 1 ? nwords * 12 : pruns ? nwords * 4 : n2 * 4);
@@ -2511,13 +2588,13 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         LAUNCHCHK("k_join_write_hits");
         return MQ_OK;
     }
-    if (j->unique == 2 && j->packed && j->slot16) {
+    if (j->pruns && j->slot16) {
         hipLaunchKernelGGL(k_join_write_runs16<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)), dim3(kTPB), 0,
                            (hipStream_t)stream, j->pstart, j->n2, j->offs, d_p2, j->p01, j->bpos, d_out1, d_out2);
         LAUNCHCHK("k_join_write_runs16");
         return MQ_OK;
     }
-    if (j->unique == 2 && j->packed) {
+    if (j->pruns) {
         // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, "16" sixteen
         // (176 VGPRs, two waves a SIMD; not measured yet), default eight
         const char* wf = getenv("MQ_JOIN_WRITE");
@@ -2539,10 +2616,21 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         LAUNCHCHK("k_join_write_runs");
         return MQ_OK;
     }
+    // the long-run list: at most m / kLongRun chunks (+ one per run for the rounding)
+    const uint64_t qcap = j->m / kLongRun + j->m / kLongChunk + 2;
+    if (qcap > 0xFFFFFFF0ull) return set_err(MQ_EINVAL, "mq_join_write: %llu pairs", (unsigned long long)j->m);
+    if (j->longq) HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    pool_free(j->longq);
+    if (!(j->longq = (u64*)pool_alloc(qcap * 8 + 16))) return set_err(MQ_ENOMEM, "mq_join_write: long-run list");
+    uint32_t* const nlong = reinterpret_cast<uint32_t*>(j->longq + qcap);
+    HIPCHK(hipMemsetAsync(nlong, 0, 4, (hipStream_t)stream));
     hipLaunchKernelGGL(k_join_write, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                        j->pstart, j->plen, j->offs, d_p2,
-                       j->bpos, j->n2, d_out1, d_out2);
+                       j->bpos, j->n2, d_out1, d_out2, j->longq, nlong);
     LAUNCHCHK("k_join_write");
+    hipLaunchKernelGGL(k_join_write_long, dim3(s->cus * 8), dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->plen,
+                       j->offs, d_p2, j->bpos, j->longq, nlong, d_out1, d_out2);
+    LAUNCHCHK("k_join_write_long");
     return MQ_OK;
 }
 
@@ -2568,6 +2656,7 @@ int mq_join_free(mq_join* j) {
     pool_free(j->plen);
     pool_free(j->offs);
     pool_free(j->scan_scratch);
+    pool_free(j->longq);
     jfree_all(j);
     delete j;
     return MQ_OK;

@@ -1615,32 +1615,61 @@ const void* scan_fn(bool vec) {
 // pool of slots handed out in rotation let >16 concurrent launches, e.g. row shards
 // on one device, share counters and fold wrong partials.) The per-thread default
 // stream is one stream per thread, so its blocks are keyed by thread as well.
+// The block lives on the stream's own device (hipStreamGetDevice; the null and
+// per-thread streams belong to the current one). Entries are dropped when libmq
+// destroys the stream (mq_stream_destroy) and, for the per-thread stream, when
+// the thread releases its resources (mq_thread_release).
+struct ArriveEntry {
+    int dev;
+    hipStream_t st;
+    std::thread::id th;
+    unsigned int* ctr;
+};
+std::mutex g_arrive_mu;
+std::vector<ArriveEntry> g_arrive;
+
+int stream_device(hipStream_t st, int* dev) {
+    if (st != nullptr && st != hipStreamPerThread && hipStreamGetDevice(st, dev) == hipSuccess) return 0;
+    return hipGetDevice(dev) == hipSuccess ? 0 : -1;
+}
+
 unsigned int* arrive_counters(hipStream_t st) {
-    struct Key {
-        int dev;
-        hipStream_t st;
-        std::thread::id th;
-    };
-    struct Entry {
-        Key k;
-        unsigned int* ctr;
-    };
-    static std::mutex mu;
-    static std::vector<Entry> tab;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (stream_device(st, &dev)) return nullptr;
     const std::thread::id th = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
-    std::lock_guard<std::mutex> lk(mu);
-    for (const Entry& e : tab)
-        if (e.k.dev == dev && e.k.st == st && e.k.th == th) return e.ctr;
+    std::lock_guard<std::mutex> lk(g_arrive_mu);
+    for (const ArriveEntry& e : g_arrive)
+        if (e.dev == dev && e.st == st && e.th == th) return e.ctr;
+    int cur = dev;
+    (void)hipGetDevice(&cur);
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     void* p = nullptr;
-    if (hipMalloc(&p, kArriveBytes) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, kArriveBytes, st) != hipSuccess) {
+    const bool ok = hipMalloc(&p, kArriveBytes) == hipSuccess;
+    if (ok && hipMemsetAsync(p, 0, kArriveBytes, st) != hipSuccess) {
         (void)hipFree(p);
-        return nullptr;
+        p = nullptr;
     }
-    tab.push_back(Entry{Key{dev, st, th}, static_cast<unsigned int*>(p)});
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!p) return nullptr;
+    g_arrive.push_back(ArriveEntry{dev, st, th, static_cast<unsigned int*>(p)});
     return static_cast<unsigned int*>(p);
+}
+
+// Free the counter blocks of stream st (every thread's, for a real stream) or, with
+// st == hipStreamPerThread, the calling thread's. The caller has synchronised the
+// work that used them.
+void arrive_forget(hipStream_t st) {
+    const std::thread::id th = st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+    std::lock_guard<std::mutex> lk(g_arrive_mu);
+    for (size_t i = 0; i < g_arrive.size();) {
+        if (g_arrive[i].st == st && g_arrive[i].th == th) {
+            (void)hipFree(g_arrive[i].ctr);
+            g_arrive[i] = g_arrive.back();
+            g_arrive.pop_back();
+        } else {
+            i++;
+        }
+    }
 }
 
 // Launch k_scan<MODE> over n rows; returns the number of blocks (partials) via *g_out.
@@ -2068,6 +2097,10 @@ void mq_host_prefault(void* p, size_t bytes) {
     if (on && p && bytes) g_fault.begin(p, bytes);
 }
 
+// mq_host_prefault_wait (mq_device.h): wait for the calling thread's population job,
+// so its range may be freed.
+void mq_host_prefault_wait(void) { g_fault.finish(); }
+
 int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream) {
     if (bytes == 0) return MQ_OK;
     int d;
@@ -2124,6 +2157,8 @@ void mq_thread_release(void) {
     }
     if (have_cur) (void)hipSetDevice(cur);
     mqi::shared_staging_release();
+    (void)hipStreamSynchronize(hipStreamPerThread);
+    arrive_forget(hipStreamPerThread);
 }
 
 // The mirror of the staged D2H: the pool copies chunk c into pinned buffer c % 4
@@ -2547,7 +2582,10 @@ int mq_stream_create(void** stream) {
 }
 
 int mq_stream_destroy(void* stream) {
-    if (stream) HIPCHK(hipStreamDestroy((hipStream_t)stream));
+    if (!stream) return MQ_OK;
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    arrive_forget((hipStream_t)stream);
+    HIPCHK(hipStreamDestroy((hipStream_t)stream));
     return MQ_OK;
 }
 

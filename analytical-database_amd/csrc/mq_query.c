@@ -734,12 +734,21 @@ Result* fetch_column(Column* column, Result* position_result, Status* ret_status
     if (column_device(column, &dcol, ret_status) || result_device(position_result, &dpos, ret_status) ||
         ensure_ws(k, ret_status))
         return NULL;
-    /* K is known before the gather runs: the payload's pages fault in while it does */
-    int32_t* host = (int32_t*)payload_alloc(k * sizeof(int32_t));
-    mq_host_prefault(host, k * sizeof(int32_t));
+    /* K is known before the gather runs: the payload's pages fault in while it does.
+     * Only a payload that takes the staged copy (which waits for the helper threads)
+     * is handed to them; the plain copy would return with them still at work. */
+    const size_t bytes = k * sizeof(int32_t);
+    int32_t* host = (int32_t*)payload_alloc(bytes);
+    if (!host) {
+        fail(ret_status, "fetch_column payload", MQ_ENOMEM);
+        return NULL;
+    }
+    const int staged = bytes >= SHADOW_MIN_BYTES && mq_guard_enabled() && mq_guard_chunk_ok(host);
+    if (staged) mq_host_prefault(host, bytes);
     int rc = mq_fetch(dcol, dpos, k, (int32_t*)g_scratch, g_stream);
     if (rc) {
         fail(ret_status, "fetch_column", rc);
+        if (staged) mq_host_prefault_wait();
         free(host);
         return NULL;
     }
@@ -1072,8 +1081,6 @@ char* print(Result** results, int result_num, Status* ret_status) {
 /* load path: db_manager.c:240-322 load_db + :164-199 insert_row      */
 /* ------------------------------------------------------------------ */
 
-/* The server's own capacity helpers (db_manager.c:430 save_data, :736 start_data),
- * resolved from the executable that links libmq; NULL when none does. */
 /* ---- J4: hashset.c (src/hashset.c:11-65) ----
  * The reference's linear-probing int32 set, kept as its own host table so that
  * code written against hashset.h behaves the same; defined behaviour where the
@@ -1158,6 +1165,8 @@ Result* get_hashset_elements(hashset* set) {
     return new_result(INT, count, elements);
 }
 
+/* The server's own capacity helpers (db_manager.c:430 save_data, :736 start_data),
+ * resolved from the executable that links libmq; NULL when none does. */
 extern void save_data(Table* table, Column* column, Status* ret_status) __attribute__((weak));
 extern void start_data(Db* db, Table* table, Column* column, Status* ret_status)
     __attribute__((weak));

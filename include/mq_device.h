@@ -62,6 +62,9 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
  * a result's size before its kernel runs start it first, so the page faults overlap
  * the kernel. MQ_PREFAULT=0 disables it, MQ_FAULT_THREADS (default 8) sizes it. */
 void mq_host_prefault(void* p, size_t bytes);
+/* Wait until the calling thread's population job (if any) has finished: call it
+ * before freeing a range handed to mq_host_prefault that no staged copy consumed. */
+void mq_host_prefault_wait(void);
 int mq_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int mq_memset(void* dptr, int value, size_t bytes, void* stream);
 int mq_stream_sync(void* stream);
