@@ -1448,7 +1448,7 @@ __global__ __launch_bounds__(kTPB) void k_join_write_hits(const u64* __restrict_
         if (!((m >> b) & 1)) continue;
         const u64 o = woffs[j >> 6] + (u64)__popcll(m & ((1ull << b) - 1));
         out1[o] = (int)pstart[j];
-        out2[o] = p2[j];
+        if (out2) out2[o] = (p2 ? p2[j] : 0);
     }
 }
 
@@ -1543,10 +1543,10 @@ __global__ __launch_bounds__(kTPB) void k_join_write(const uint32_t* __restrict_
         }
         const u64 o = offs[j];
         const uint32_t s = pstart[j];
-        const int pp = p2[j];
+        const int pp = (p2 ? p2[j] : 0);
         for (uint32_t t = 0; t < L; t++) {
             out1[o + t] = bpos[s + t];
-            out2[o + t] = pp;
+            if (out2) out2[o + t] = pp;
         }
     }
 }
@@ -1568,10 +1568,10 @@ __global__ __launch_bounds__(kTPB) void k_join_write_long(const uint32_t* __rest
         const uint32_t a = c * kLongChunk, b = L - a < kLongChunk ? L : a + kLongChunk;
         const u64 o = offs[j];
         const uint32_t s = pstart[j];
-        const int pp = p2[j];
+        const int pp = (p2 ? p2[j] : 0);
         for (uint32_t t = a + threadIdx.x; t < b; t += kTPB) {
             out1[o + t] = bpos[s + t];
-            out2[o + t] = pp;
+            if (out2) out2[o + t] = pp;
         }
     }
 }
@@ -1614,10 +1614,10 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __rest
         }
         if (!L) continue;
         const u64 o = woffs[w] + (u64)(incl - L);
-        const int pp = p2[j];
+        const int pp = (p2 ? p2[j] : 0);
         for (uint32_t t = 0; t < L; t++) {
             out1[o + t] = bpos[a + t];
-            out2[o + t] = pp;
+            if (out2) out2[o + t] = pp;
         }
     }
 }
@@ -1648,7 +1648,7 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs_mlp(const uint32_t* __
         for (int u = 0; u < kWriteWords; u++) {
             const uint64_t j = (w0 + u) * 64 + (uint64_t)lane;
             pv[u] = j < n2 ? pk[j] : 0u;
-            pp[u] = j < n2 ? p2[j] : 0;
+            pp[u] = j < n2 ? (p2 ? p2[j] : 0) : 0;
         }
 #pragma unroll
         for (int u = 0; u < kWriteWords; u++) {
@@ -1670,14 +1670,14 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs_mlp(const uint32_t* __
         for (int u = 0; u < kWriteWords; u++) {
             if (!L[u]) continue;
             out1[o[u]] = b0[u];
-            out2[o[u]] = pp[u];
+            if (out2) out2[o[u]] = pp[u];
             if (L[u] > 1u) {
                 out1[o[u] + 1] = b1[u];
-                out2[o[u] + 1] = pp[u];
+                if (out2) out2[o[u] + 1] = pp[u];
             }
             for (uint32_t t = 2; t < L[u]; t++) {
                 out1[o[u] + t] = bpos[a[u] + t];
-                out2[o[u] + t] = pp[u];
+                if (out2) out2[o[u] + t] = pp[u];
             }
         }
     }
@@ -1704,7 +1704,7 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs16(const uint32_t* __re
             const uint64_t j = (w0 + u) * 64 + (uint64_t)lane;
             const uint32_t m = j < n2 ? pk[j] : 0u;
             pq[u] = j < n2 ? p01[j] : 0ull;
-            pp[u] = j < n2 ? p2[j] : 0;
+            pp[u] = j < n2 ? (p2 ? p2[j] : 0) : 0;
             L[u] = m & 15u;
             a[u] = m >> 4;
         }
@@ -1723,15 +1723,15 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs16(const uint32_t* __re
             if (!L[u]) continue;
             if (L[u] <= 2u) {
                 out1[o[u]] = (int)(uint32_t)pq[u];
-                out2[o[u]] = pp[u];
+                if (out2) out2[o[u]] = pp[u];
                 if (L[u] == 2u) {
                     out1[o[u] + 1] = (int)(uint32_t)(pq[u] >> 32);
-                    out2[o[u] + 1] = pp[u];
+                    if (out2) out2[o[u] + 1] = pp[u];
                 }
             } else {
                 for (uint32_t t = 0; t < L[u]; t++) {
                     out1[o[u] + t] = bpos[a[u] + t];
-                    out2[o[u] + t] = pp[u];
+                    if (out2) out2[o[u] + t] = pp[u];
                 }
             }
         }
@@ -1842,6 +1842,22 @@ __global__ __launch_bounds__(kTPB) void k_run_payload(const uint32_t* __restrict
     for (uint64_t r = (uint64_t)blockIdx.x * kTPB + threadIdx.x; r < R; r += stride) {
         const uint32_t a = rs[r], L = rs[r + 1] - a;
         rid[r] = (int)(!packed ? (uint32_t)r : L < 15u ? (a << 4) | L : ((uint32_t)r << 4) | 15u);
+    }
+}
+
+// Per probe row, the number of pairs the last probe found for it (mq_join_counts),
+// from whichever per-row state the probe left: the unique table's hit words (0/1), a
+// packed payload per row (its length, < 15 on the per-word path), or a length per row.
+__global__ __launch_bounds__(kTPB) void k_join_counts(const u64* __restrict__ hits, const uint32_t* __restrict__ pk,
+                                                      const uint32_t* __restrict__ plen, uint64_t n2,
+                                                      uint32_t* __restrict__ cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB;
+    for (uint64_t j = (uint64_t)blockIdx.x * kTPB + threadIdx.x; j < n2; j += stride) {
+        uint32_t c;
+        if (hits) c = (uint32_t)(hits[j >> 6] >> (j & 63)) & 1u;
+        else if (pk) c = pk[j] & 15u;
+        else c = plen[j];
+        cnt[j] = c;
     }
 }
 
@@ -2581,7 +2597,7 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (rc) return rc;
     if (!j) return set_err(MQ_EINVAL, "mq_join_write: NULL handle");
     if (j->m == 0) return MQ_OK;
-    if (!d_p2 || !d_out1 || !d_out2) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
+    if (!d_out1 || (d_out2 && !d_p2)) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
     if (j->unique == 1) {
         hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                            reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
@@ -2631,6 +2647,25 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     hipLaunchKernelGGL(k_join_write_long, dim3(s->cus * 8), dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->plen,
                        j->offs, d_p2, j->bpos, j->longq, nlong, d_out1, d_out2);
     LAUNCHCHK("k_join_write_long");
+    return MQ_OK;
+}
+
+int mq_join_counts(mq_join* j, uint32_t* d_cnt, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (!j || (j->n2 && !d_cnt)) return set_err(MQ_EINVAL, "mq_join_counts: bad argument");
+    if (j->n2 == 0) return MQ_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (j->n1 == 0) {  // the probe ran nothing: no row matched
+        HIPCHK(hipMemsetAsync(d_cnt, 0, j->n2 * 4, st));
+        return MQ_OK;
+    }
+    const u64* hits = j->unique == 1 ? reinterpret_cast<const u64*>(j->plen) : nullptr;
+    const uint32_t* pk = (!hits && j->pruns) ? j->pstart : nullptr;
+    const uint32_t* plen = (!hits && !j->pruns) ? j->plen : nullptr;
+    hipLaunchKernelGGL(k_join_counts, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, st, hits, pk, plen, j->n2, d_cnt);
+    LAUNCHCHK("k_join_counts");
     return MQ_OK;
 }
 

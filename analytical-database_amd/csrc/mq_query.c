@@ -969,6 +969,8 @@ static Result** join_pairs(const int32_t* d1, const int32_t* dp1, size_t n1, con
 Result** hash_join(Result* column_one, Result* position_one, Result* column_two, Result* position_two,
                    Status* ret_status) {
     if (op_begin(ret_status)) return NULL;
+    if (shard_join_wants(column_one->num_tuples, column_two->num_tuples)) /* key-partitioned, DESIGN.md §6 */
+        return shard_hash_join(column_one, position_one, column_two, position_two, 0, ret_status);
     const int32_t *d1, *dp1, *d2, *dp2;
     if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
         result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))
@@ -982,6 +984,8 @@ Result** hash_join(Result* column_one, Result* position_one, Result* column_two,
 Result** nested_loop_join(Result* column_one, Result* position_one, Result* column_two,
                           Result* position_two, Status* ret_status) {
     if (op_begin(ret_status)) return NULL;
+    if (shard_join_wants(column_two->num_tuples, column_one->num_tuples))
+        return shard_hash_join(column_two, position_two, column_one, position_one, 1, ret_status);
     const int32_t *d1, *dp1, *d2, *dp2;
     if (result_device(column_one, &d1, ret_status) || result_device(position_one, &dp1, ret_status) ||
         result_device(column_two, &d2, ret_status) || result_device(position_two, &dp2, ret_status))

@@ -153,7 +153,9 @@ static void t_init(Shard* s, void* arg) {
     (void)arg;
     if ((s->rc = mq_init(s->dev))) return;
     if ((s->rc = mq_stream_create(&s->stream))) return;
-    s->rc = mq_malloc(&s->small, 4096);
+    if ((s->rc = mq_malloc(&s->small, 4096))) return;
+    /* the join's exchanges copy between shard devices (mq_memcpy_peer) */
+    for (int g = 0; g < g_G && !s->rc; g++) s->rc = mq_enable_peer(g_sh[g].dev);
 }
 
 static void t_stop(Shard* s, void* a);
@@ -687,6 +689,383 @@ Result** shard_shared_select(SelectOperator* ops, int q, Column* c, Status* st) 
         shim_fail(st, "shard shared_select", rc);
         return NULL;
     }
+    st->code = OK;
+    return out;
+}
+
+/* ---- hash_join: key-partitioned over the shards (mq_pjoin.hip's protocol) ---- */
+
+typedef struct {
+    /* inputs: shard s's rows of each side, on its device */
+    const int32_t* c1[MAXS];
+    const int32_t* p1[MAXS];
+    uint64_t n1[MAXS];
+    const int32_t* c2[MAXS];
+    const int32_t* p2[MAXS];
+    uint64_t n2[MAXS];
+    /* 1. partitioned sides on shard s, bucket sizes [s][b] */
+    int32_t *bk[MAXS], *bp[MAXS], *pk[MAXS];
+    uint32_t* inv[MAXS];
+    uint64_t cb[MAXS][MAXS], cp[MAXS][MAXS];
+    /* 2. on device g: per probe row counts, build positions of the pairs, pairs per
+     *    source shard [g][s] */
+    uint32_t* cnt[MAXS];
+    int32_t* o1[MAXS];
+    uint64_t mg[MAXS][MAXS];
+    /* 3. outputs on shard s */
+    int32_t *out1[MAXS], *out2[MAXS];
+    uint64_t m[MAXS];
+    double ms[4]; /* host wall time of the phases (partition, join, place, total) */
+} PJ;
+
+static void* pj_alloc(int* rc, size_t bytes) {
+    void* p = NULL;
+    if (!*rc) *rc = mq_pool_malloc(&p, bytes ? bytes : 4);
+    return p;
+}
+
+static void t_pj_part(Shard* s, void* a) {
+    PJ* x = (PJ*)a;
+    const int i = s->idx;
+    int rc = 0;
+    x->bk[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4);
+    x->bp[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4);
+    x->pk[i] = (int32_t*)pj_alloc(&rc, x->n2[i] * 4);
+    x->inv[i] = (uint32_t*)pj_alloc(&rc, x->n2[i] * 4);
+    if (!rc)
+        rc = mq_pjoin_partition(x->c1[i], x->p1[i], x->n1[i], g_G, x->bk[i], x->bp[i], NULL, x->cb[i], s->stream);
+    if (!rc)
+        rc = mq_pjoin_partition(x->c2[i], NULL, x->n2[i], g_G, x->pk[i], NULL, x->inv[i], x->cp[i], s->stream);
+    s->rc = rc;
+}
+
+/* first index of bucket b in shard s's partitioned side (cnt = cb or cp) */
+static uint64_t pj_seg(uint64_t (*cnt)[MAXS], int s, int b) {
+    uint64_t o = 0;
+    for (int k = 0; k < b; k++) o += cnt[s][k];
+    return o;
+}
+
+static void t_pj_join(Shard* s, void* a) {
+    PJ* x = (PJ*)a;
+    const int g = s->idx;
+    uint64_t nb = 0, np = 0;
+    for (int k = 0; k < g_G; k++) {
+        nb += x->cb[k][g];
+        np += x->cp[k][g];
+    }
+    int rc = 0;
+    int32_t* jk = (int32_t*)pj_alloc(&rc, nb * 4);
+    int32_t* jp = (int32_t*)pj_alloc(&rc, nb * 4);
+    int32_t* jq = (int32_t*)pj_alloc(&rc, np * 4);
+    x->cnt[g] = (uint32_t*)pj_alloc(&rc, np * 4);
+    /* bucket g of every shard, in shard order */
+    uint64_t ab = 0, ap = 0;
+    for (int k = 0; k < g_G && !rc; k++) {
+        const uint64_t ob = pj_seg(x->cb, k, g), op = pj_seg(x->cp, k, g);
+        const int dv = g_sh[k].dev;
+        rc = mq_memcpy_peer(jk + ab, s->dev, x->bk[k] + ob, dv, x->cb[k][g] * 4, s->stream);
+        if (!rc) rc = mq_memcpy_peer(jp + ab, s->dev, x->bp[k] + ob, dv, x->cb[k][g] * 4, s->stream);
+        if (!rc) rc = mq_memcpy_peer(jq + ap, s->dev, x->pk[k] + op, dv, x->cp[k][g] * 4, s->stream);
+        ab += x->cb[k][g];
+        ap += x->cp[k][g];
+    }
+    mq_join* j = NULL;
+    uint64_t m = 0;
+    if (!rc) rc = mq_join_build(jk, jp, nb, &j, s->stream);
+    if (!rc) rc = mq_join_probe(j, jq, np, &m, s->stream);
+    if (!rc) rc = mq_join_counts(j, x->cnt[g], s->stream);
+    /* pairs per source shard: the sum of its segment's counts */
+    if (!rc) rc = ensure(s, 0);
+    uint64_t sp = 0;
+    for (int k = 0; k < g_G && !rc; k++) {
+        x->mg[g][k] = 0;
+        if (x->cp[k][g] && m) {
+            rc = mq_reduce((const int32_t*)(x->cnt[g] + sp), x->cp[k][g], (mq_agg*)s->small, s->ws, s->ws_bytes,
+                           s->stream);
+            mq_agg ag;
+            if (!rc) rc = mq_memcpy_d2h(&ag, s->small, sizeof ag, s->stream);
+            if (!rc) x->mg[g][k] = (uint64_t)ag.sum;
+        }
+        sp += x->cp[k][g];
+    }
+    x->o1[g] = (int32_t*)pj_alloc(&rc, m * 4);
+    if (!rc && m) rc = mq_join_write(j, NULL, x->o1[g], NULL, s->stream);
+    if (!rc) rc = mq_stream_sync(s->stream);
+    if (j) mq_join_free(j);
+    mq_pool_free(jk);
+    mq_pool_free(jp);
+    mq_pool_free(jq);
+    s->rc = rc;
+}
+
+static void t_pj_place(Shard* s, void* a) {
+    PJ* x = (PJ*)a;
+    const int i = s->idx;
+    const uint64_t n = x->n2[i];
+    uint64_t M = 0;
+    for (int g = 0; g < g_G; g++) M += x->mg[g][i];
+    x->m[i] = M;
+    int rc = 0;
+    uint32_t* cntp = (uint32_t*)pj_alloc(&rc, n * 4);
+    int32_t* o1p = (int32_t*)pj_alloc(&rc, M * 4);
+    x->out1[i] = (int32_t*)pj_alloc(&rc, M * 4);
+    x->out2[i] = (int32_t*)pj_alloc(&rc, M * 4);
+    /* from every device g, in g order: this shard's bucket-g rows' counts and pairs */
+    uint64_t ac = 0, am = 0;
+    for (int g = 0; g < g_G && !rc; g++) {
+        uint64_t oc = 0, om = 0; /* the segments of shards before this one on device g */
+        for (int k = 0; k < i; k++) {
+            oc += x->cp[k][g];
+            om += x->mg[g][k];
+        }
+        const int dv = g_sh[g].dev;
+        rc = mq_memcpy_peer(cntp + ac, s->dev, x->cnt[g] + oc, dv, x->cp[i][g] * 4, s->stream);
+        if (!rc) rc = mq_memcpy_peer(o1p + am, s->dev, x->o1[g] + om, dv, x->mg[g][i] * 4, s->stream);
+        ac += x->cp[i][g];
+        am += x->mg[g][i];
+    }
+    if (!rc) rc = mq_pjoin_place(cntp, o1p, x->inv[i], x->p2[i], n, M, x->out1[i], x->out2[i], s->stream);
+    if (!rc) rc = mq_stream_sync(s->stream);
+    mq_pool_free(cntp);
+    mq_pool_free(o1p);
+    s->rc = rc;
+}
+
+static void pj_free_temps(PJ* x) {
+    for (int g = 0; g < g_G; g++) {
+        mq_pool_free(x->bk[g]);
+        mq_pool_free(x->bp[g]);
+        mq_pool_free(x->pk[g]);
+        mq_pool_free(x->inv[g]);
+        mq_pool_free(x->cnt[g]);
+        mq_pool_free(x->o1[g]);
+        x->bk[g] = x->bp[g] = x->pk[g] = x->o1[g] = NULL;
+        x->inv[g] = x->cnt[g] = NULL;
+    }
+}
+
+/* The three phases; every worker synchronises its stream before a phase ends, so the
+ * next phase's peer copies read finished data. On error nothing of x's stays allocated. */
+static int pj_run(PJ* x) {
+    double t0 = shim_now();
+    int rc = run_all(t_pj_part, x);
+    double t1 = shim_now();
+    if (!rc) rc = run_all(t_pj_join, x);
+    double t2 = shim_now();
+    if (!rc) rc = run_all(t_pj_place, x);
+    double t3 = shim_now();
+    pj_free_temps(x);
+    x->ms[0] = 1e3 * (t1 - t0);
+    x->ms[1] = 1e3 * (t2 - t1);
+    x->ms[2] = 1e3 * (t3 - t2);
+    x->ms[3] = 1e3 * (t3 - t0);
+    if (rc)
+        for (int g = 0; g < g_G; g++) {
+            mq_pool_free(x->out1[g]);
+            mq_pool_free(x->out2[g]);
+            x->out1[g] = x->out2[g] = NULL;
+        }
+    return rc;
+}
+
+static double g_pj_ms[4];
+
+void mq_shard_join_times(double* ms) {
+    for (int k = 0; k < 4; k++) ms[k] = g_pj_ms[k];
+}
+
+int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const uint64_t* n1,
+                  const int32_t* const* d_c2, const int32_t* const* d_p2, const uint64_t* n2, int32_t** d_out1,
+                  int32_t** d_out2, uint64_t* h_m) {
+    configure();
+    Status st;
+    if (g_G < 1) return MQ_EINVAL;
+    if (start(&st)) return MQ_ENODEV;
+    PJ* x = (PJ*)calloc(1, sizeof(PJ));
+    if (!x) return MQ_ENOMEM;
+    for (int g = 0; g < g_G; g++) {
+        x->c1[g] = d_c1[g];
+        x->p1[g] = d_p1[g];
+        x->n1[g] = n1[g];
+        x->c2[g] = d_c2[g];
+        x->p2[g] = d_p2[g];
+        x->n2[g] = n2[g];
+    }
+    int rc = pj_run(x);
+    for (int k = 0; k < 4; k++) g_pj_ms[k] = x->ms[k];
+    for (int g = 0; g < g_G && !rc; g++) {
+        d_out1[g] = x->out1[g];
+        d_out2[g] = x->out2[g];
+        h_m[g] = x->m[g];
+    }
+    free(x);
+    return rc;
+}
+
+int mq_shard_devices(int* devices, int max) {
+    configure();
+    for (int g = 0; g < g_G && g < max; g++) devices[g] = g_sh[g].dev;
+    return g_G;
+}
+
+/* Whether hash_join / nested_loop_join fan out: shards on, and a probe side of at
+ * least MQ_SHARD_MIN_ROWS rows (the row count columns shard at). */
+int shard_join_wants(size_t n1, size_t n2) {
+    configure();
+    if (!(g_G > 1 && n2 >= g_min_rows && n1 <= (size_t)INT32_MAX && n2 <= (size_t)INT32_MAX)) return 0;
+    if (g_started == 0) {
+        Status tmp;
+        (void)start(&tmp);
+    }
+    return g_started == 1;
+}
+
+/* one side's shard pieces (values a, positions b): the sharded shadows when both have
+ * them with one split, else uploads of the split_of(n) row ranges */
+typedef struct {
+    const Result* r[2];
+    size_t off[MAXS + 1];
+    void* dev[2][MAXS];
+    int owned;
+} PjSide;
+
+typedef struct {
+    PjSide* side;
+} PjUpArg;
+
+static void t_pj_upload(Shard* s, void* a) {
+    PjSide* x = ((PjUpArg*)a)->side;
+    const size_t b0 = x->off[s->idx], n = x->off[s->idx + 1] - b0;
+    for (int k = 0; k < 2; k++) {
+        if ((s->rc = mq_pool_malloc(&x->dev[k][s->idx], (n ? n : 1) * 4))) return;
+        double t0 = shim_now();
+        if (n) s->rc = mq_memcpy_h2d(x->dev[k][s->idx], (const int32_t*)x->r[k]->payload + b0, n * 4, s->stream);
+        s->xfer += shim_now() - t0;
+        if (s->rc) return;
+    }
+    s->rc = mq_stream_sync(s->stream);
+}
+
+static int pj_side(PjSide* x, const Result* a, const Result* b) {
+    memset(x, 0, sizeof *x);
+    x->r[0] = a;
+    x->r[1] = b;
+    const size_t n = a->num_tuples;
+    /* (a lookup may drop a stale entry and move another into its slot: look a up again) */
+    int ia = ssh_find(a->payload, n);
+    const int ib = ia >= 0 ? ssh_find(b->payload, n) : -1;
+    if (ib >= 0) ia = ssh_find(a->payload, n);
+    if (ia >= 0 && ib >= 0 && memcmp(g_ssh[ia].off, g_ssh[ib].off, sizeof(size_t) * (size_t)(g_G + 1)) == 0) {
+        memcpy(x->off, g_ssh[ia].off, sizeof(size_t) * (size_t)(g_G + 1));
+        memcpy(x->dev[0], g_ssh[ia].dev, sizeof(void*) * (size_t)g_G);
+        memcpy(x->dev[1], g_ssh[ib].dev, sizeof(void*) * (size_t)g_G);
+        return 0;
+    }
+    split_of(n, x->off);
+    x->owned = 1;
+    PjUpArg u = {x};
+    int rc = run_all(t_pj_upload, &u);
+    if (rc) {
+        free_pieces(x->dev[0]);
+        free_pieces(x->dev[1]);
+    }
+    return rc;
+}
+
+static void pj_side_free(PjSide* x) {
+    if (!x->owned) return;
+    free_pieces(x->dev[0]);
+    free_pieces(x->dev[1]);
+}
+
+typedef struct {
+    PJ* pj;
+    int32_t* payload[2];
+    size_t off[MAXS + 1];
+    int keep[2];
+} PjOutArg;
+
+static void t_pj_download(Shard* s, void* a) {
+    PjOutArg* x = (PjOutArg*)a;
+    const size_t m = x->pj->m[s->idx];
+    int32_t* dev[2] = {x->pj->out1[s->idx], x->pj->out2[s->idx]};
+    for (int k = 0; k < 2 && !s->rc; k++)
+        s->rc = download(s, x->payload[k] + x->off[s->idx], dev[k], m * 4, x->keep[k]);
+    if (!s->rc) s->rc = mq_stream_sync(s->stream);
+}
+
+/* hash_join (query.c:652-696) with the build side (c1, p1) and the probe side (c2, p2)
+ * over the shards; swap puts the probe positions first (nested_loop_join). */
+Result** shard_hash_join(Result* c1, Result* p1, Result* c2, Result* p2, int swap, Status* st) {
+    const double t0 = shim_now();
+    PjSide bs, ps;
+    int rc = pj_side(&bs, c1, p1);
+    if (rc) {
+        shim_fail(st, "shard join upload", rc);
+        return NULL;
+    }
+    if ((rc = pj_side(&ps, c2, p2))) {
+        pj_side_free(&bs);
+        shim_fail(st, "shard join upload", rc);
+        return NULL;
+    }
+    PJ* x = (PJ*)calloc(1, sizeof(PJ));
+    PjOutArg* o = (PjOutArg*)calloc(1, sizeof(PjOutArg));
+    if (!x || !o) {
+        free(x);
+        free(o);
+        pj_side_free(&bs);
+        pj_side_free(&ps);
+        shim_fail(st, "shard join", MQ_ENOMEM);
+        return NULL;
+    }
+    for (int g = 0; g < g_G; g++) {
+        x->c1[g] = (const int32_t*)bs.dev[0][g];
+        x->p1[g] = (const int32_t*)bs.dev[1][g];
+        x->n1[g] = bs.off[g + 1] - bs.off[g];
+        x->c2[g] = (const int32_t*)ps.dev[0][g];
+        x->p2[g] = (const int32_t*)ps.dev[1][g];
+        x->n2[g] = ps.off[g + 1] - ps.off[g];
+    }
+    rc = pj_run(x);
+    for (int k = 0; k < 4; k++) g_pj_ms[k] = x->ms[k];
+    pj_side_free(&bs);
+    pj_side_free(&ps);
+    Result** out = NULL;
+    if (!rc) {
+        o->pj = x;
+        o->off[0] = 0;
+        for (int g = 0; g < g_G; g++) o->off[g + 1] = o->off[g] + x->m[g];
+        const size_t M = o->off[g_G];
+        for (int k = 0; k < 2; k++) {
+            o->payload[k] = (int32_t*)shim_payload_alloc(M * 4);
+            o->keep[k] = o->payload[k] && keep_payload(o->payload[k], M * 4);
+            if (!o->payload[k]) rc = MQ_ENOMEM;
+        }
+        if (!rc) rc = run_all(t_pj_download, o);
+        if (!rc) {
+            out = (Result**)malloc(2 * sizeof(Result*));
+            /* the pieces stay as the payloads' sharded shadows (rows 0: not positions of a
+             * column split, so fetch_column does not take them) */
+            Result* r1 = finish(o->payload[0], M, 0, o->off, (void**)x->out1, o->keep[0]);
+            Result* r2 = finish(o->payload[1], M, 0, o->off, (void**)x->out2, o->keep[1]);
+            out[0] = swap ? r2 : r1;
+            out[1] = swap ? r1 : r2;
+        } else {
+            free(o->payload[0]);
+            free(o->payload[1]);
+            free_pieces((void**)x->out1);
+            free_pieces((void**)x->out2);
+        }
+    }
+    free(x);
+    free(o);
+    if (rc) {
+        shim_fail(st, "shard hash_join", rc);
+        return NULL;
+    }
+    if (shim_trace_on()) fprintf(stderr, "mq-trace shard_hash_join(G=%d)  %9.3f ms\n", g_G, 1e3 * (shim_now() - t0));
     st->code = OK;
     return out;
 }

@@ -44,6 +44,11 @@ int shard_reduce_column(Column* c, mq_agg* a, Status* st);
 int shard_reduce_result(const Result* r, mq_agg* a, Status* st);
 /* shared_select (query.c:439-583) over a sharded column */
 Result** shard_shared_select(SelectOperator* ops, int q, Column* c, Status* st);
+/* hash_join (query.c:652-696) key-partitioned over the shards: the
+ * build side (c1, p1), the probe side (c2, p2); swap = 1 returns the probe positions
+ * first (nested_loop_join). */
+int shard_join_wants(size_t n1, size_t n2);
+Result** shard_hash_join(Result* c1, Result* p1, Result* c2, Result* p2, int swap, Status* st);
 void shard_op_begin(void);                 /* sweep + budget at every operator start */
 void shard_forget_column(const Column* c);
 /* make c resident on the shards now (mq_column_upload of a sharded column): 0 or -1 */

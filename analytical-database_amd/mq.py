@@ -103,11 +103,14 @@ _SIGS = {
     "mq_version": (C.c_char_p, []),
     "mq_malloc": (_int, [C.POINTER(_vp), _sz]),
     "mq_free": (_int, [_vp]),
+    "mq_pool_malloc": (_int, [C.POINTER(_vp), _sz]),
+    "mq_pool_free": (_int, [_vp]),
     "mq_memcpy_h2d": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2h": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2d": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2h_staged": (_int, [_vp, _vp, _sz, _vp]),
     "mq_host_prefault": (None, [_vp, _sz]),
+    "mq_host_prefault_wait": (None, []),
     "mq_stream_create": (_int, [C.POINTER(_vp)]),
     "mq_stream_destroy": (_int, [_vp]),
     "mq_thread_release": (None, []),
@@ -165,6 +168,17 @@ _SIGS = {
     "mq_join_probe": (_int, [_vp, _vp, _u64, C.POINTER(_u64), _vp]),
     "mq_join_write": (_int, [_vp, _vp, _vp, _vp, _vp]),
     "mq_join_free": (_int, [_vp]),
+    "mq_join_counts": (_int, [_vp, _vp, _vp]),
+    # key-partitioned join (mq_pjoin.hip, mq_shard.c)
+    "mq_pjoin_bucket": (C.c_uint32, [_i32, _int]),
+    "mq_pjoin_partition": (_int, [_vp, _vp, _u64, _int, _vp, _vp, _vp, C.POINTER(_u64), _vp]),
+    "mq_pjoin_place": (_int, [_vp, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp]),
+    "mq_memcpy_peer": (_int, [_vp, _int, _vp, _int, _sz, _vp]),
+    "mq_enable_peer": (_int, [_int]),
+    "mq_shard_join": (_int, [C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_u64), C.POINTER(_vp), C.POINTER(_vp),
+                             C.POINTER(_u64), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_u64)]),
+    "mq_shard_devices": (_int, [C.POINTER(_int), _int]),
+    "mq_shard_join_times": (None, [C.POINTER(C.c_double)]),
     # reference API (query.h:20-50)
     "select_result": (_PR, [_PR, _PR, C.POINTER(_int), C.POINTER(_int), _PS]),
     "select_column": (_PR, [C.POINTER(Column), C.POINTER(_int), C.POINTER(_int), _PS]),

@@ -292,6 +292,31 @@ int mq_join_probe(mq_join* join, const int32_t* d_c2, uint64_t n2, uint64_t* h_m
 int mq_join_write(mq_join* join, const int32_t* d_p2, int32_t* d_out1, int32_t* d_out2,
                   void* stream);
 int mq_join_free(mq_join* join);
+/* Per probe row of the last mq_join_probe, its number of pairs (d_cnt: n2 u32).
+ * mq_join_write also accepts d_p2 = d_out2 = NULL: build positions only. */
+int mq_join_counts(mq_join* join, uint32_t* d_cnt, void* stream);
+
+/* ---- key-partitioned hash join over G devices ----
+ * The device pieces; mq_shard_join (mq_query.h) runs them over the row-shard workers,
+ * analytical-database_amd/dist.py one process per GPU.
+ * mq_pjoin_bucket: the bucket (0..G-1) of a key, as the partition kernels compute it.
+ * mq_pjoin_partition: stable split of n rows into G buckets by key: d_keys_out (and
+ *   d_pay_out with d_pay, and d_inv[r] = row r's new index, when not NULL) hold bucket
+ *   0's rows in row order, then bucket 1's, ...; h_counts[b] (host, G entries) their
+ *   numbers. Synchronous. G <= 64, n < 2^32.
+ * mq_pjoin_place: a probe shard's output from its partitioned counts d_cntp (n u32) and
+ *   pairs d_out1p (m build positions, partitioned order): row r's pairs go to the offset
+ *   of the rows before it, out2 = d_p2[r]. */
+uint32_t mq_pjoin_bucket(int32_t key, int G);
+int mq_pjoin_partition(const int32_t* d_keys, const int32_t* d_pay, uint64_t n, int G, int32_t* d_keys_out,
+                       int32_t* d_pay_out, uint32_t* d_inv, uint64_t* h_counts, void* stream);
+int mq_pjoin_place(const uint32_t* d_cntp, const int32_t* d_out1p, const uint32_t* d_inv, const int32_t* d_p2,
+                   uint64_t n, uint64_t m, int32_t* d_out1, int32_t* d_out2, void* stream);
+/* Device-to-device copy between (or within) devices on stream (the destination's). */
+int mq_memcpy_peer(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, void* stream);
+/* Let the current device read and write peer's memory directly (a no-op where the
+ * platform cannot; peer copies still work then). */
+int mq_enable_peer(int peer);
 
 /* ---- J1 hash_join in one call: build on (c1,p1) (n1 rows), probe with (c2,p2) (n2 rows) ----
  * Output pairs (out1[m], out2[m]) = (build position, probe position) in

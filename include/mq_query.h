@@ -217,6 +217,21 @@ const void* mq_result_device_ptr(const Result* result);
  * copy first. shards <= 0 returns to the environment's layout. Several shards may
  * share one device (a rehearsal of the split on a one-GPU machine). */
 int mq_shard_config(int shards, const int* devices, int ndev, uint64_t min_rows);
+/* The current layout: returns the shard count G, devices[g] (up to max) its devices. */
+int mq_shard_devices(int* devices, int max);
+/* hash_join (query.c:652-696) key-partitioned over the G shards (DESIGN.md
+ * §6; hash_join / nested_loop_join take it for probe sides of at least min_rows rows).
+ * Shard g holds build rows (d_c1[g], d_p1[g], n1[g]) and probe rows (d_c2[g], d_p2[g],
+ * n2[g]) on its device, the ranges of each side in row order (any split). On return
+ * shard g's device holds d_out1[g] / d_out2[g]: the h_m[g] pairs of probe rows of range
+ * g, in the reference's order; their concatenation over g is hash_join's output. The
+ * outputs are pool memory (mq_pool_free). Starts the shard workers if needed. */
+int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const uint64_t* n1,
+                  const int32_t* const* d_c2, const int32_t* const* d_p2, const uint64_t* n2,
+                  int32_t** d_out1, int32_t** d_out2, uint64_t* h_m);
+/* Host wall ms of the last partitioned join's phases: partition, exchange + local join,
+ * return exchange + place, total. */
+void mq_shard_join_times(double* ms);
 /* Drop every cached device copy. */
 void mq_release_all(void);
 /* Residency counters since load (tests and the bench read them). */
