@@ -395,11 +395,103 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[I], uint32_t len
     return true;
 }
 
+// The counting finisher, second form (round 4, MQ_ISORT_FIN=4): the same sort with
+// fewer scalar and LDS instructions. The first form's PMC at 1e9 rows: 2.5 G SALU
+// (exec-mask bookkeeping of per-row guards) and 0.71 G LDS instructions with 1.35 G
+// bank-conflict cycles. Here:
+//  * after the scan every cell holds an absolute slot (each wave adds the slots of the
+//    waves before it to its own words; one more barrier), so no row looks up its
+//    wave's base with a lane shuffle (ds_bpermute, an LDS instruction);
+//  * the placement has no branch: a row past the range's end takes the dummy cell word
+//    and the dummy slot kCap;
+//  * a row's tie rank is counted over its key's slot group [cell(x - 1), cell(x)), read
+//    from the cells (an untied row's group is itself), instead of testing both
+//    neighbours' keys for every row and walking the group by key.
+// Static counts (hipcc -S): 905 SALU / 201 LDS / 90 exec saves against 1265 / 252 /
+// 182, 128 VGPRs, no spills. (Branch-free counting, or per-round uniform guards, spilled
+// the prefetched next range: tools-free A/B of 36 variants by the compiler's counts.)
+template <int T, int I>
+__device__ __forceinline__ bool finish_counting2(const u64 (&el)[I], uint32_t len, uint32_t kbase, int s,
+                                                 uint32_t* c32, uint32_t* rows, uint16_t* keys, uint32_t* wsum,
+                                                 int32_t* vout, u64* pout) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = T / 64;
+    const uint32_t nw = count_words<T>(s);
+#pragma unroll
+    for (int k = 0; k < I; k++) {
+        const uint32_t x = (uint32_t)el[k] - kbase;
+        const bool v = (uint32_t)k * T + tid < len;
+        if (v) atomicAdd(&c32[x >> 1], 1u << (16 * (x & 1)));
+    }
+    __syncthreads();
+    const uint32_t per = nw / kW, q = per / 64;
+    uint32_t* mine = c32 + wave * per + lane * q;
+    uint32_t tot = 0, mx = 0;
+    for (uint32_t j = 0; j < q; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu, hi = cell >> 16;
+        mx = lo > mx ? lo : mx;
+        mx = hi > mx ? hi : mx;
+        tot += lo + hi;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    if (__ballot(mx > kTieMax)) wsum[kW] = 1;  // benign race: any writer stores 1
+    __syncthreads();
+    if (wsum[kW]) return false;
+    uint32_t base = 0;  // the slots of the waves before this one (wave-uniform)
+    for (int w = 0; w < wave; w++) base += wsum[w];
+    uint32_t run = base + incl - tot;
+    for (uint32_t j = 0; j < q; j++) {
+        const uint32_t cell = mine[j], lo = cell & 0xFFFFu;
+        mine[j] = run | ((run + lo) << 16);
+        run += lo + (cell >> 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < I; k++) {
+        const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
+        const bool v = (uint32_t)k * T + tid < len;
+        const uint32_t old = atomicAdd(&c32[v ? x >> 1 : kCap / 2], 1u << sh);
+        const uint32_t slot = v ? ((old >> sh) & 0xFFFFu) : kCap;
+        rows[slot] = (uint32_t)(el[k] >> 32);
+        keys[slot] = (uint16_t)x;
+    }
+    __syncthreads();
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
+#pragma unroll
+    for (int k = 0; k < I; k++) {
+        const uint32_t e = (uint32_t)k * T + tid;
+        const uint32_t ec = e < len ? e : len - 1;
+        const uint32_t x = keys[ec], r = rows[ec];
+        const uint32_t xp = x ? x - 1 : 0;
+        const uint32_t ge = c16[x], gs = c16[xp];
+        uint32_t pos = x ? gs : 0u;
+#pragma unroll 1
+        for (uint32_t j = pos; j < ge; j++) pos += rows[j] < r;
+        if (e < len) {
+            vout[e] = (int32_t)((kbase + x) ^ 0x80000000u);
+            pout[pos] = r;
+        }
+    }
+    __syncthreads();
+    for (uint32_t x = tid; x < nw; x += T) c32[x] = 0;
+    if (tid == 0) {
+        wsum[kW] = 0;
+        c32[kCap / 2] = 0;
+    }
+    return true;
+}
+
 // The counting finisher, persistent: a block per CU walks the list, and the next
 // range's words are loaded into registers while the current one is sorted (a block
 // holds 128 KB of LDS, so a CU runs one: without this its loads, LDS work and stores
 // would take turns). A range it cannot take goes to the ranked finisher's list.
-template <int T, int I, bool BF>
+template <int T, int I, bool BF, bool V2 = false>
 __global__ __launch_bounds__(T) void k_msd_finish_count(const u64* __restrict__ w0, const u64* __restrict__ w1,
                                                         const Fin* __restrict__ fins, uint32_t nfin, uint32_t kmin,
                                                         int32_t* __restrict__ vout, u64* __restrict__ pout,
@@ -443,7 +535,9 @@ __global__ __launch_bounds__(T) void k_msd_finish_count(const u64* __restrict__ 
 #pragma unroll
         for (int k = 0; k < I; k++) el[k] = nx[k];
         if (nxt < nfin) prefetch(nxt);
-        if (!finish_counting<T, I, BF>(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po)) {
+        const bool ok = V2 ? finish_counting2<T, I>(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po)
+                           : finish_counting<T, I, BF>(el, f.len, kmin + f.klo, s, c32, rows, keys, wsum, vo, po);
+        if (!ok) {
             if (tid == 0) fb[atomicAdd(&ctr->nfb, 1u)] = f;
             __syncthreads();
             for (uint32_t x = tid; x < kCap / 2; x += T) c32[x] = 0;
@@ -539,9 +633,9 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
     Seg* sl[2] = {(Seg*)pool_alloc(smax * sizeof(Seg)), (Seg*)pool_alloc(smax * sizeof(Seg))};
     Ctr* ctr = (Ctr*)pool_alloc(sizeof(Ctr));
     // MQ_ISORT_FIN: the counting finisher's shape, 1 = 1024 x 16 with per-row guards,
-    // 2 = 512 x 32 with guards, 3 = 512 x 32 branch-free (A/B)
+    // 2 = 512 x 32 with guards, 3 = 512 x 32 branch-free, 4 = 1024 x 16 second form (A/B)
     const char* ff = getenv("MQ_ISORT_FIN");
-    const int fin_form = ff ? atoi(ff) : 1;
+    const int fin_form = ff ? atoi(ff) : 4;
     Fin* fl[kMaxLevels] = {};  // finisher lists of each level: counting
     Fin* rl[kMaxLevels] = {};  // ... ranked
     Fin* bl[kMaxLevels] = {};  // ... and the counting finisher's fallbacks
@@ -632,7 +726,10 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
                                ctr, kmin, vout, pout);
         if (hc.nfin) {
             const uint32_t g = hc.nfin < cus ? hc.nfin : cus;
-            if (fin_form == 1)
+            if (fin_form == 4 && vout && pout)  // (the second form writes both outputs)
+                hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false, true>), dim3(g), dim3(1024), 0, st, wb[0],
+                                   wb[1], fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
+            else if (fin_form == 1 || fin_form == 4)
                 hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false>), dim3(g), dim3(1024), 0, st, wb[0], wb[1],
                                    fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
             else if (fin_form == 2)

@@ -224,8 +224,9 @@ def inproc_main(args) -> None:
             step_s.append(dt)
     resid = mq.residency(lib)
     lib.mq_release_all()
-    mq.check(lib.mq_shard_config(0, None, 0, 0), "mq_shard_config reset")
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "goldens.json")))
+    join = None if args.no_join else inproc_join_leg(lib, mq, torch, devices, gold)
+    mq.check(lib.mq_shard_config(0, None, 0, 0), "mq_shard_config reset")
     want = next((r for r in gold["config4"] if r["n"] == n and r["seed"] == 42 and r["low"] == lo and r["high"] == hi),
                 None)
     parity = None if want is None else (k, total) == (want["k"], want["sum"])
@@ -252,11 +253,80 @@ def inproc_main(args) -> None:
         "upload_gbs": 4.0 * n / t_up / 1e9,
         "residency": resid,
         "parity": {"ok": parity, "count": k, "sum": total},
+        "extra": {"config5_partitioned_join": join},
     }
+    bad = parity_failures(out)
+    out["parity_failures"] = bad
     print(json.dumps(out), flush=True)
-    if parity is False:
+    if parity is False or bad:
         print("bench.py --inproc: parity FAILED", file=sys.stderr)
         sys.exit(1)
+
+
+def inproc_join_leg(lib, mq, torch, devices, gold, logn: int = 28, reps: int = 3) -> dict:
+    """Config 5 (2^28 x 2^28 hash join, SURVEY §8(c) keys) key-partitioned over the row
+    shards (mq_shard_join): each side split into len(devices) contiguous
+    row ranges, range g resident on devices[g]; partition, exchange (peer copies), local
+    joins, return exchange, place. Device-resident inputs and outputs (no PCIe). Parity:
+    M and the FNV-1a of the concatenated pairs against the reference's goldens."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu  # checker only (pair hash)
+    G = len(devices)
+    n = 1 << logn
+    full = [torch.empty(n, dtype=torch.int32, device="cuda:0") for _ in range(3)]
+    mq.check(lib.mq_gen_join_keys(full[0].data_ptr(), n, 0, None))
+    mq.check(lib.mq_gen_join_keys(full[1].data_ptr(), n, 1, None))
+    mq.check(lib.mq_gen_iota(full[2].data_ptr(), n, None))
+    torch.cuda.synchronize()
+    b = [n * g // G for g in range(G + 1)]
+    pieces = [[x[b[g]:b[g + 1]].to(f"cuda:{devices[g]}") for x in full] for g in range(G)]
+    del full
+    torch.cuda.synchronize()
+    V, U = C.c_void_p * G, C.c_uint64 * G
+    c1 = V(*[pieces[g][0].data_ptr() for g in range(G)])
+    c2 = V(*[pieces[g][1].data_ptr() for g in range(G)])
+    pp = V(*[pieces[g][2].data_ptr() for g in range(G)])
+    ns = U(*[b[g + 1] - b[g] for g in range(G)])
+    times, phases = [], []
+    o1 = o2 = m = None
+    for rep in range(reps + 1):
+        if o1 is not None:
+            for g in range(G):
+                lib.mq_pool_free(o1[g])
+                lib.mq_pool_free(o2[g])
+        o1, o2, m = V(), V(), U()
+        t0 = time.perf_counter()
+        mq.check(lib.mq_shard_join(c1, pp, ns, c2, pp, ns, o1, o2, m), "mq_shard_join")
+        dt = time.perf_counter() - t0
+        ph = (C.c_double * 4)()
+        lib.mq_shard_join_times(ph)
+        if rep:
+            times.append(dt)
+            phases.append(list(ph))
+    import numpy as np
+    parts = []
+    for g in range(G):
+        a1, a2 = np.empty(m[g], np.int32), np.empty(m[g], np.int32)
+        for a, o in ((a1, o1), (a2, o2)):
+            if m[g]:
+                mq.check(lib.mq_memcpy_d2h(a.ctypes.data, o[g], a.nbytes, None))
+        parts.append((a1, a2))
+        lib.mq_pool_free(o1[g])
+        lib.mq_pool_free(o2[g])
+    M = int(sum(m))
+    fnv = refcpu.fnv1a64_pairs(np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    want = [r for r in gold["join_survey"] if r["n"] == n]
+    ok = bool(want) and (M, f"{fnv:016x}") == (want[0]["m"], want[0]["pairs_fnv1a64"])
+    del pieces
+    t = statistics.median(times)
+    k = len(times) // 2
+    return {"n_build": n, "n_probe": n, "m": M, "shards": G, "devices": devices, "ms": 1e3 * t,
+            "rows_per_s": 2 * n / t, "algorithmic_bytes": 16 * n + 8 * M,
+            "ms_phases": dict(zip(("partition", "exchange_join", "return_place", "total"),
+                                  sorted(phases, key=lambda x: x[3])[k])),
+            "pairs_per_shard": list(m), "parity": ok,
+            "note": "mq_shard_join wall time (host), device-resident inputs and outputs; on one GPU "
+                    "(MQ_BENCH_ONE_DEVICE=1) every shard and exchange shares device 0"}
 
 
 def main() -> None:
@@ -268,6 +338,7 @@ def main() -> None:
         ap.add_argument("--warmup", type=int, default=2)
         ap.add_argument("--rows", type=int, default=1_000_000_000)
         ap.add_argument("--sel", type=float, default=0.01)
+        ap.add_argument("--no-join", action="store_true", help="skip the partitioned-join leg")
         inproc_main(ap.parse_args())
         return
     if "WORLD_SIZE" not in os.environ:
@@ -641,11 +712,23 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
             "ms": t_chain, "rows_per_s": n / (t_chain * 1e-3), "parity": chain_ok,
             "avg": (int(a[1]) / int(a[0])) if int(a[0]) else None,
             "algorithmic_bytes": 4 * n + 12 * k}
+        # the gather's line over-fetch: every match reads its
+        # col1 row through a whole 64-byte line; distinct lines touched = the lines that
+        # hold at least one matching row (counted from the positions, on the device)
+        lines = torch.unique_consecutive(pos[:k].to(torch.int64) // 16).numel()
         out["config3_fused"] = {
             "ms": t_fused, "rows_per_s": n / (t_fused * 1e-3), "parity": fused_ok,
             "algorithmic_bytes": 4 * n + 8 * k,
+            "gather_lines": lines, "gather_lines_bytes": 64 * lines,
+            "gather_overfetch": (64 * lines) / (4 * k) if k else None,
+            "hbm_bytes_design": 4 * n + 64 * lines,
+            "gbs_design": (4 * n + 64 * lines) / (t_fused * 1e-3) / 1e9,
+            "frac_design": (4 * n + 64 * lines) / (t_fused * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "note": "select col0 + gather col1 at matches, one kernel (k_scan_gather: matches "
-                    "staged per wave in LDS, gathered 8 loads in flight per lane)"}
+                    "staged per wave in LDS, gathered 8 loads in flight per lane); the gather reads "
+                    "gather_lines 64-B lines of col1 for its 4K useful bytes"}
+        out["positions_sweep"] = positions_sweep(lib, mq, torch, dev, stream, col, col1, ws, ws_bytes, n, pos, cnt,
+                                                 gold)
         del pos, col1, vals
     out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
@@ -655,6 +738,41 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
     out["pcie_probe"] = pcie_probe(torch, dev, stream)
     out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
     return out
+
+
+def positions_sweep(lib, mq, torch, dev, stream, col, col1, ws, ws_bytes, n, pos, cnt, gold) -> dict:
+    """SURVEY §8(d) config 2's selectivity sweep through the ordered compaction
+    (k_select_stage): select_column_scan's positions (query.c:92-137) and the
+    select_result payload form (query.c:38-86: a match emits payload[row], here col1),
+    at 0.1 / 1 / 10 / 50 / 100 % of the 1e9-row column, [N/4, N/4 + sel N). HIP events,
+    median of 5. Algorithmic bytes: positions 4N + 4K; payload 4N + 4K (payload rows
+    read at matches) + 4K. Parity: K and the FNV of the positions against the
+    reference's goldens at 1 % and 50 % (tests/golden/goldens.json)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import refcpu  # checker only (FNV of the positions)
+    sp = mq.stream_of(stream)
+    res = {}
+    for sel in (0.001, 0.01, 0.1, 0.5, 1.0):
+        lo = int(0.25 * n)
+        hi = lo + int(sel * n)
+        row = {}
+        for form, payload in (("positions", None), ("select_result", col1)):
+            fn = lambda: mq.check(lib.mq_select_positions(  # noqa: E731
+                col.data_ptr(), None if payload is None else payload.data_ptr(), n, 1, lo, 1, hi, pos.data_ptr(),
+                cnt.data_ptr(), ws.data_ptr(), ws_bytes, sp), "select_positions")
+            with torch.cuda.stream(stream):
+                ms = _events_ms(torch, stream, fn, 5)
+            k = int(cnt.item())
+            ab = 4 * n + 4 * k + (4 * k if payload is not None else 0)
+            row[form] = {"ms": ms, "k": k, "algorithmic_bytes": ab, "gbs": ab / (ms * 1e-3) / 1e9,
+                         "frac": ab / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            if payload is None:
+                want = [r for r in gold["select"] if r["n"] == n and abs(r["sel"] - sel) < 1e-12]
+                if want:
+                    fnv = refcpu.fnv1a64(pos[:k].cpu().numpy())
+                    row[form]["parity"] = (k, f"{fnv:016x}") == (want[0]["k"], want[0]["pos_fnv1a64"])
+        res[f"sel_{sel:g}"] = row
+    return res
 
 
 def api_leg(lib, mq, n, lo, hi, gold) -> dict:

@@ -25,7 +25,7 @@ case "$what" in
       "200|$tag/bench_n2|MQ_BENCH_BACKEND=gloo MQ_BENCH_ONE_DEVICE=1 python3 bench.py --gpus 2 --no-extra --no-cpu"
     ;;
   tests)
-    exec tools/gpu_steps.sh "900|$tag/pytest|python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -s $*"
+    exec tools/gpu_steps.sh "900|$tag/pytest|python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -s ${*:-tests}"
     ;;
   bench)
     exec tools/gpu_steps.sh \
