@@ -901,7 +901,7 @@ template <bool PAYLOAD, bool VEC, int BUF = kStBuf>
 __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, uint64_t rw, Pred pred,
     unsigned long long* status, unsigned long long* __restrict__ bm, int* __restrict__ out,
-    unsigned long long* __restrict__ d_count, unsigned int* err) {
+    unsigned long long* __restrict__ d_count, unsigned int* err, int xmode) {
     __shared__ int s_buf[kWaves][BUF > 0 ? BUF : 1];
     __shared__ unsigned int s_cnt[kWaves];
     __shared__ unsigned long long s_red[kWaves];
@@ -1036,6 +1036,42 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         const unsigned int tot = __shfl(incl, 63, 64);
         const unsigned long long ol = o + (incl - c);
         const uint64_t row0 = T * 256;
+        if (xmode == 1 && tot > 256) {
+            // staged (round 4): tile by tile, the wave puts the tile's outputs in row
+            // order into its LDS ring (free now: its entries went out above), then
+            // stores them as consecutive dwords, 64 lanes per instruction. Stores
+            // straight from the lanes' rows (below) leave every instruction's
+            // addresses with gaps wherever a row does not match, so the memory
+            // pipeline splits them.
+            const uint64_t tend = tb + 64 < T1 ? tb + 64 : T1;
+            for (uint64_t Tj = tb; Tj < tend; Tj++) {
+                const unsigned long long* wp = bm + Tj * 4;  // wave-uniform
+                const unsigned long long x0 = wp[0], x1 = wp[1], x2 = wp[2], x3 = wp[3];
+                const uint32_t cj = (uint32_t)(__popcll(x0) + __popcll(x1) + __popcll(x2) + __popcll(x3));
+                if (cj == 0) continue;
+                const uint64_t rj = Tj * 256 + 4 * (uint64_t)lane;
+                int pv[4] = {0, 0, 0, 0};
+                if constexpr (PAYLOAD) {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) pv[e] = payload[rj + e < n ? rj + e : n - 1];
+                }
+                uint32_t k = (uint32_t)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) + __popcll(x2 & ltmask) +
+                                        __popcll(x3 & ltmask));
+                if ((x0 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[0] : (int)(rj + 0) + rbase;
+                if ((x1 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[1] : (int)(rj + 1) + rbase;
+                if ((x2 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[2] : (int)(rj + 2) + rbase;
+                if ((x3 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[3] : (int)(rj + 3) + rbase;
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t e = (uint32_t)i * 64u + (uint32_t)lane;
+                    if (e < cj) out[o + e] = buf[e];
+                }
+                __builtin_amdgcn_wave_barrier();
+                o += cj;
+            }
+            continue;
+        }
         if (tot > 1024) {
             // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e).
             // select_result: the payload rows of 4 tiles are loaded (indices clamped)
@@ -1783,12 +1819,15 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     unsigned long long* bm = reinterpret_cast<unsigned long long*>(w + partial_bytes());
     HIPCHK(hipMemsetAsync(w, 0, stage_state_bytes(g), st));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
+    // MQ_STAGE_EXPAND=0: the bitmap tiles expanded by lane-scattered stores (A/B)
+    const char* xe = getenv("MQ_STAGE_EXPAND");
+    const int xmode = xe && xe[0] == '0' ? 0 : 1;
     if (payload) {
-        if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
-        else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
+        else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
     } else {
-        if (vec) hipLaunchKernelGGL((k_select_stage<false, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
-        else hipLaunchKernelGGL((k_select_stage<false, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        if (vec) hipLaunchKernelGGL((k_select_stage<false, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
+        else hipLaunchKernelGGL((k_select_stage<false, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
     }
     LAUNCHCHK("k_select_stage");
     return MQ_OK;

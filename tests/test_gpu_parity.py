@@ -71,12 +71,16 @@ def _data(n, seed):
     return d
 
 
-POS_IMPLS = ["stage", "mask", "lookback"]  # MQ_POSITIONS_IMPL (read by libmq per call)
+# MQ_POSITIONS_IMPL (read by libmq per call); "stage_lanes": k_select_stage with its
+# bitmap tiles expanded by lane-scattered stores (MQ_STAGE_EXPAND=0) instead of staged
+POS_IMPLS = ["stage", "stage_lanes", "mask", "lookback"]
 
 
 @pytest.fixture(params=POS_IMPLS)
 def pos_impl(request, monkeypatch):
-    monkeypatch.setenv("MQ_POSITIONS_IMPL", request.param)
+    monkeypatch.setenv("MQ_POSITIONS_IMPL", "stage" if request.param.startswith("stage") else request.param)
+    if request.param == "stage_lanes":
+        monkeypatch.setenv("MQ_STAGE_EXPAND", "0")
     return request.param
 
 
