@@ -487,100 +487,8 @@ static int result_device(const Result* r, const int32_t** d, Status* st) {
  * Large ones are advised onto transparent huge pages first: the D2H that fills a
  * fresh buffer otherwise takes one page fault per 4 KB (tools/d2h_paths: 40 MB in
  * 2.0 ms plain, 1.7 ms advised). */
-/* Warm payloads (round 4). A fresh payload's pages fault in on first touch, and for a
- * select the touch can only start once K is known (§1 of DESIGN.md: ≥ 0.9 ms for
- * 40 MB, more than the DMA). A large payload request therefore leaves behind a warm
- * chunk for the next one: a helper thread mallocs a chunk of 5/4 of its size (an
- * mmapped chunk: the threshold is 1 MB), advises it onto huge pages and populates it
- * (MADV_POPULATE_WRITE, else one write per page) while the caller goes on. The next
- * payload of at most that size, and at least a quarter of it, takes the warm chunk:
- * it is plain malloc'd memory that the caller free()s as usual, only already in
- * memory. One chunk is kept (MQ_WARM_PAYLOAD=0 turns this off). */
-#define WARM_MIN ((size_t)8 << 20)
-#define WARM_MAX ((size_t)1 << 30)
-static pthread_mutex_t g_warm_mu = PTHREAD_MUTEX_INITIALIZER;
-static pthread_cond_t g_warm_cv = PTHREAD_COND_INITIALIZER;
-static void* g_warm;          /* a populated chunk ready to hand out, or NULL */
-static size_t g_warm_bytes;   /* its usable request size */
-static size_t g_warm_want;    /* the chunk the helper is asked to make (0 = none) */
-static int g_warm_busy;       /* the helper is making one */
-static int g_warm_state;      /* 0 = not started, 1 = running, -1 = off */
-
-static void* warm_main(void* arg) {
-    (void)arg;
-    pthread_mutex_lock(&g_warm_mu);
-    for (;;) {
-        while (!g_warm_want) pthread_cond_wait(&g_warm_cv, &g_warm_mu);
-        const size_t want = g_warm_want;
-        g_warm_want = 0;
-        g_warm_busy = 1;
-        pthread_mutex_unlock(&g_warm_mu);
-        void* p = malloc(want);
-        if (p) {
-            const uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095;
-            const uintptr_t e = ((uintptr_t)p + want) & ~(uintptr_t)4095;
-            if (e > a) {
-                (void)madvise((void*)a, e - a, MADV_HUGEPAGE);
-                if (madvise((void*)a, e - a, 23 /* MADV_POPULATE_WRITE */) != 0)
-                    for (uintptr_t q = a; q < e; q += 4096) *(volatile char*)q = 0;
-            }
-        }
-        pthread_mutex_lock(&g_warm_mu);
-        g_warm_busy = 0;
-        if (p && !g_warm) {
-            g_warm = p;
-            g_warm_bytes = want;
-        } else {
-            free(p);
-        }
-    }
-    return NULL;
-}
-
-static pthread_once_t g_warm_once = PTHREAD_ONCE_INIT;
-static void warm_start(void) {
-    const char* e = getenv("MQ_WARM_PAYLOAD");
-    pthread_t th;
-    g_warm_state = (e && e[0] == '0') ? -1 : pthread_create(&th, NULL, warm_main, NULL) == 0 ? 1 : -1;
-    if (g_warm_state == 1) pthread_detach(th);
-}
-
-/* Give the warm chunk back (mq_release_all). */
-static void warm_release(void) {
-    pthread_mutex_lock(&g_warm_mu);
-    free(g_warm);
-    g_warm = NULL;
-    pthread_mutex_unlock(&g_warm_mu);
-}
-
-/* A warm chunk for a request of `bytes`, or NULL; asks for the next one either way. */
-static void* warm_take(size_t bytes) {
-    if (bytes < WARM_MIN || bytes > WARM_MAX) return NULL;
-    pthread_once(&g_warm_once, warm_start);
-    if (g_warm_state != 1) return NULL;
-    void* p = NULL;
-    pthread_mutex_lock(&g_warm_mu);
-    if (g_warm && g_warm_bytes >= bytes && g_warm_bytes / 4 <= bytes) {
-        p = g_warm;
-        g_warm = NULL;
-    }
-    if (!g_warm && !g_warm_busy) { /* the next one: 5/4 of this request, 2 MB-rounded */
-        size_t want = bytes + bytes / 4;
-        want = (want + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-        g_warm_want = want > WARM_MAX ? WARM_MAX : want;
-        pthread_cond_signal(&g_warm_cv);
-    }
-    pthread_mutex_unlock(&g_warm_mu);
-    return p;
-}
-
 static void* payload_alloc(size_t bytes) {
-    void* p = warm_take(bytes);
-    if (p) {
-        mq_guard_forget_range((uintptr_t)p, bytes);
-        return p;
-    }
-    p = malloc(bytes ? bytes : 1);
+    void* p = malloc(bytes ? bytes : 1);
     if (!p) return NULL;
     mq_guard_forget_range((uintptr_t)p, bytes ? bytes : 1); /* a guard left on recycled memory */
     if (bytes >= ((size_t)8 << 20)) {
@@ -1596,7 +1504,6 @@ void mq_release_all(void) {
     while (g_nshadows) shadow_drop(g_nshadows - 1);
     while (g_nidx) idx_drop(&g_idx[g_nidx - 1]);
     shard_release_all();
-    warm_release();
     mq_trim();
 }
 
