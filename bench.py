@@ -355,6 +355,8 @@ def main() -> None:
     ap.add_argument("--sel", type=float, default=0.01)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the positions/config-3 legs")
+    ap.add_argument("--join", action="store_true",
+                    help="N > 1: also time config 5 key-partitioned over the ranks (dist.partitioned_join)")
     args = ap.parse_args()
 
     import torch
@@ -468,6 +470,8 @@ def main() -> None:
     achievable = achievable_read_peak(lib, mq, torch, stream, col, ws) if world == 1 else None
 
     extra = {}
+    if world > 1 and args.join:  # every rank takes part (all_to_all exchanges)
+        extra["config5_partitioned_join"] = dist_join_leg(lib, mq, mqd, torch, dist, dev, rank, world, gold)
     if rank == 0 and world == 1 and not args.no_extra:
         extra = extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold,
                            cpu=not args.no_cpu)
@@ -519,6 +523,53 @@ def main() -> None:
     if parity is False or (rank == 0 and bad):
         print(f"bench.py: parity FAILED: {'headline' if parity is False else ''} {bad}", file=sys.stderr)
         sys.exit(1)
+
+
+def dist_join_leg(lib, mq, mqd, torch, dist, dev, rank, world, gold, logn: int = 28, reps: int = 3) -> dict:
+    """Config 5 (2^28 x 2^28, SURVEY §8(c) keys) key-partitioned over the ranks, one per
+    GPU (dist.partitioned_join: libmq's partition / local join / place kernels, RCCL
+    all_to_all exchanges): rank r holds rows [r n / N, (r + 1) n / N) of both sides. Time =
+    max over ranks, between barriers. Parity: the total M equals the reference's golden,
+    and every rank's pairs join equal keys in probe-major, build-ascending order (with
+    the identity positions and unique build keys this fixes the output)."""
+    n = 1 << logn
+    a, b = n * rank // world, n * (rank + 1) // world
+    c1 = torch.empty(b - a, dtype=torch.int32, device=dev)
+    c2 = torch.empty(b - a, dtype=torch.int32, device=dev)
+    full = torch.empty(n, dtype=torch.int32, device=dev)
+    mq.check(lib.mq_gen_join_keys(full.data_ptr(), n, 0, None))
+    c1.copy_(full[a:b])
+    mq.check(lib.mq_gen_join_keys(full.data_ptr(), n, 1, None))
+    c2.copy_(full[a:b])
+    p = torch.arange(a, b, dtype=torch.int32, device=dev)
+    ph = mqd.LibmqPhases(lib, mq)
+    ts = []
+    for rep in range(reps + 1):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        o1, o2 = mqd.partitioned_join(ph, c1, p, c2, p)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rep:
+            ts.append(float(t.item()))
+    mq.check(lib.mq_gen_join_keys(full.data_ptr(), n, 0, None))
+    bk = full[o1.long()] if o1.numel() else o1
+    mq.check(lib.mq_gen_join_keys(full.data_ptr(), n, 1, None))
+    pk = full[o2.long()] if o2.numel() else o2
+    ok = bool(torch.equal(bk, pk))
+    if o2.numel() > 1:
+        ok = ok and bool((o2[1:] > o2[:-1]).all()) and int(o2[0]) >= a and int(o2[-1]) < b
+    m = torch.tensor([o1.numel(), int(ok)], dtype=torch.int64, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.SUM)
+    want = [r for r in gold["join_survey"] if r["n"] == n]
+    t = statistics.median(ts)
+    return {"n_build": n, "n_probe": n, "m": int(m[0]), "ranks": world, "ms": 1e3 * t, "rows_per_s": 2 * n / t,
+            "parity": bool(want) and int(m[0]) == want[0]["m"] and int(m[1]) == world,
+            "note": "strong scaling of config 5: the 2^28 x 2^28 join split over the ranks, exchanges by RCCL "
+                    "all_to_all (DESIGN.md §6)"}
 
 
 def parity_failures(out: dict) -> list:
