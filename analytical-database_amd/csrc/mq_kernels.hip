@@ -1819,9 +1819,11 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     unsigned long long* bm = reinterpret_cast<unsigned long long*>(w + partial_bytes());
     HIPCHK(hipMemsetAsync(w, 0, stage_state_bytes(g), st));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
-    // MQ_STAGE_EXPAND=0: the bitmap tiles expanded by lane-scattered stores (A/B)
+    // MQ_STAGE_EXPAND=1: the bitmap tiles expanded through the LDS ring into coalesced
+    // stores. Measured and kept off: 1.19 / 1.55 / 1.79 ms at 10 / 50 / 100 % against
+    // 1.11 / 1.49 / 1.82 ms for the lane-scattered stores (profiles/r04_positions_ab.log)
     const char* xe = getenv("MQ_STAGE_EXPAND");
-    const int xmode = xe && xe[0] == '0' ? 0 : 1;
+    const int xmode = xe && xe[0] == '1' ? 1 : 0;
     if (payload) {
         if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
         else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);

@@ -807,12 +807,16 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             const uint32_t ent = qe[slot];
             r = qr[slot];
             uint32_t ei = ent - 1u;
-            if (ent & 0x8000u) {  // bounds inside the cell: from its first EI on
-                ei = ent & 0x7FFFu;
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (ei < m && s_b[ei] <= x) ei++;
-                if (ei < m && s_b[ei] <= x) {
+            if (ent & 0x8000u) {  // bounds inside the cell: b[e0 ..), e0 = its first EI
+                ei = ent & 0xFFFu;
+                const uint32_t nb = (ent >> 12) & 7u;  // their number when below 7, else 0
+                if (nb) {
+                    // (round 4) e(v) = e0 + the cell's bounds <= v: nb reads, no search.
+                    // PMC at Q = 150: the search made every 64-row round pay ~130 VALU
+                    // (almost every round holds a row of a flagged cell)
+                    const uint32_t e0 = ei;
+                    for (uint32_t i = 0; i < nb; i++) ei += s_b[e0 + i] <= x ? 1u : 0u;
+                } else if (ei < m && s_b[ei] <= x) {
                     uint32_t lo = ei + 1, hi = m;
                     while (lo < hi) {
                         const uint32_t mid = (lo + hi) >> 1;
@@ -1325,7 +1329,10 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
             if (ph < pl) ph = pl;
             while (ph < m && b[ph] <= ce) ph++;
             const bool any = cp[ph + 1] - cp[pl] > 0;  // a covered EI among [pl, ph]
-            hcell[c] = !any ? (uint16_t)0 : pl == ph ? (uint16_t)(pl + 1) : (uint16_t)(0x8000 | pl);
+            // bounds inside the cell: b[pl .. ph) (ph - pl of them, in the entry when fewer
+            // than 7: e(v) = pl + the ones <= v, no search)
+            const int nb = ph - pl < 7 ? ph - pl : 0;
+            hcell[c] = !any ? (uint16_t)0 : pl == ph ? (uint16_t)(pl + 1) : (uint16_t)(0x8000 | nb << 12 | pl);
         }
         // past bmax's cell every value is in EI m; below bmin (wrapped) in EI 0
         hcell[kCells - 1] = hqoff[m + 1] > hqoff[m] ? (uint16_t)0x8000 : (uint16_t)0;

@@ -71,16 +71,16 @@ def _data(n, seed):
     return d
 
 
-# MQ_POSITIONS_IMPL (read by libmq per call); "stage_lanes": k_select_stage with its
-# bitmap tiles expanded by lane-scattered stores (MQ_STAGE_EXPAND=0) instead of staged
-POS_IMPLS = ["stage", "stage_lanes", "mask", "lookback"]
+# MQ_POSITIONS_IMPL (read by libmq per call); "stage_staged": k_select_stage with its
+# bitmap tiles expanded through the LDS ring (MQ_STAGE_EXPAND=1) instead of by lanes
+POS_IMPLS = ["stage", "stage_staged", "mask", "lookback"]
 
 
 @pytest.fixture(params=POS_IMPLS)
 def pos_impl(request, monkeypatch):
     monkeypatch.setenv("MQ_POSITIONS_IMPL", "stage" if request.param.startswith("stage") else request.param)
-    if request.param == "stage_lanes":
-        monkeypatch.setenv("MQ_STAGE_EXPAND", "0")
+    if request.param == "stage_staged":
+        monkeypatch.setenv("MQ_STAGE_EXPAND", "1")
     return request.param
 
 
