@@ -57,31 +57,44 @@ int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, i
 // Frees the calling thread's pinned upload staging of shared_select (mq_shared.hip).
 void shared_staging_release();
 
+// The reference's exact quicksort order (index.c:25-46) of col[0..n), n < 2^31, into
+// vout (values) and pout (size_t positions), either may be NULL (mq_lomuto.hip).
+int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, hipStream_t st, const DevState* s);
 // Caching device allocator for per-call scratch (join tables and partitions,
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
 // idle blocks are released by mq_trim(). A freed block may be handed out again at
 // once, so callers free only what no queued kernel still uses (sync first).
-// The reference's exact quicksort order (index.c:25-46) of col[0..n), n < 2^31, into
-// vout (values) and pout (size_t positions), either may be NULL (mq_lomuto.hip).
-int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, hipStream_t st, const DevState* s);
 void* pool_alloc(size_t bytes);
 void pool_free(void* p);
 
 // Lanes of the wave (within `among`) whose 8-bit value d equals this lane's: a
-// match-any from 8 ballots. Per bit: one v_bfe_i32 (the bit as 0 / all-ones),
-// one ballot and one or-of-xor per half, accumulating the lanes that differ from
-// this lane in some bit (written as `peers &= bit ? m : ~m`, the compiler spent
-// 9 VALU per bit on it).
+// match-any from 8 ballots. Per bit: one v_bfe_i32 (the bit as 0 / all-ones), one
+// ballot, and per half one v_bitop3 accumulating acc | (bit ^ ballot), the lanes that
+// differ from this lane in some bit: 4 VALU a bit (the or-of-xor the compiler formed
+// took 5; `peers &= bit ? m : ~m` took 9). v_bitop3's table is indexed by
+// (src0, src1, src2) bits as 4 s0 + 2 s1 + s2: a | (b ^ c) = 0xF0 | (0xCC ^ 0xAA) = 0xF6.
 __device__ __forceinline__ unsigned long long match_any8(uint32_t d, unsigned long long among) {
+    uint32_t sb[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) sb[b] = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);  // bit b as 0 / ~0
+    // opaque (else each ballot is rebuilt from a second shift), all eight at once so
+    // the ballots and their uses interleave (a VALU-written SGPR needs wait states)
+    asm("" : "+v"(sb[0]), "+v"(sb[1]), "+v"(sb[2]), "+v"(sb[3]), "+v"(sb[4]), "+v"(sb[5]), "+v"(sb[6]), "+v"(sb[7]));
+    unsigned long long m[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++) m[b] = __ballot(sb[b] != 0);
     uint32_t dlo = 0, dhi = 0;
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-        const uint32_t sb = (uint32_t)(((int32_t)(d << (31 - b))) >> 31);  // bit b as 0 / ~0
-        const unsigned long long m = __ballot(sb != 0);
-        dlo |= sb ^ (uint32_t)m;
-        dhi |= sb ^ (uint32_t)(m >> 32);
+        dlo = __builtin_amdgcn_bitop3_b32(dlo, sb[b], (uint32_t)m[b], 0xF6);
+        dhi = __builtin_amdgcn_bitop3_b32(dhi, sb[b], (uint32_t)(m[b] >> 32), 0xF6);
     }
     return among & ~(((unsigned long long)dhi << 32) | dlo);
+}
+
+// Lanes below this one in mask m (v_mbcnt: 2 VALU, against and + popcount of both halves).
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // XCD-aware tile of block b in a grid of g blocks (cdna_hip_programming.md T1):

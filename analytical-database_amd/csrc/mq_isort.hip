@@ -125,14 +125,13 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
 template <int IT, bool LEVEL, bool WIDE = true>
 __device__ __forceinline__ void rank_items(const u64 (&el)[IT], uint32_t (&dr)[IT], uint32_t wbase, uint32_t len,
                                            uint32_t kbase, int sh, uint32_t wm, u64 M, uint32_t* wc, int lane) {
-    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int k = 0; k < IT; k++) {
         const bool valid = wbase + (uint32_t)k * 64 + lane < len;
         const uint32_t x = (uint32_t)el[k] - kbase;
         const uint32_t d = LEVEL ? digit_m<WIDE>(x, M) : (x >> sh) & wm;
         const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t lt = lanes_below(peers);
         const uint32_t cur = wc[d];
         __builtin_amdgcn_wave_barrier();
         if (valid && lt == 0) wc[d] = cur + (uint32_t)__popcll(peers);

@@ -254,7 +254,6 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
     __syncthreads();
     const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * IT);
-    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[IT];
     uint32_t dr[IT];
     // all items loaded first (indices clamped, no branch): one round trip, not one
@@ -270,7 +269,7 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
         const bool valid = i < n;
         const uint32_t d = (((uint32_t)el[k] - kmin) >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t lt = lanes_below(peers);
         const uint32_t cur = wcnt[wave][d];
         __builtin_amdgcn_wave_barrier();
         if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
@@ -424,7 +423,6 @@ __global__ __launch_bounds__(kTPB) void k_sort1_scatter(const int* __restrict__ 
     const uint32_t tile = s_tile;
     const uint64_t tile0 = (uint64_t)tile * kSortTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
-    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
     uint32_t dr[kSortItems];
 #pragma unroll
@@ -438,7 +436,7 @@ __global__ __launch_bounds__(kTPB) void k_sort1_scatter(const int* __restrict__ 
         const bool valid = i < n;
         const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t lt = lanes_below(peers);
         const uint32_t cur = wcnt[wave][d];
         __builtin_amdgcn_wave_barrier();
         if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
@@ -700,7 +698,6 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
     __syncthreads();
     const uint64_t tile0 = (uint64_t)tile * kSortTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
-    const u64 ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     u64 el[kSortItems];
     uint32_t dr[kSortItems];
     // all items loaded first (indices clamped, no branch): one round trip, not one
@@ -716,7 +713,7 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
         const bool valid = i < n;
         const uint32_t d = (win_id((uint32_t)el[k], t) >> shift) & 0xFF;
         const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = (uint32_t)__popcll(peers & ltmask);
+        const uint32_t lt = lanes_below(peers);
         const uint32_t cur = wcnt[wave][d];
         __builtin_amdgcn_wave_barrier();
         if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);

@@ -1074,17 +1074,22 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         }
         if (tot > 1024) {
             // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e).
+            // A tile's words, count and offset are read into scalars (v_readlane: the
+            // tile index is wave-uniform); round 4: as lane shuffles they were 12
+            // ds_bpermute round trips per tile, and 10-50 % selectivity paid ~0.5 ms
+            // for them after the scan.
             // select_result: the payload rows of 4 tiles are loaded (indices clamped)
             // before any of them is written; gathering at each write made every
             // tile wait for its own round trip (10-50 % selectivity ran at twice the
             // positions-only time)
             constexpr int kPf = 4;  // tiles per payload batch (registers: launch bounds 8 waves)
+            const uint32_t olo = (uint32_t)ol, ohi = (uint32_t)(ol >> 32);
             for (int j0 = 0; j0 < 64; j0 += kPf) {
                 int pv[kPf][4];
                 if constexpr (PAYLOAD) {
 #pragma unroll
                     for (int jj = 0; jj < kPf; jj++) {
-                        const uint64_t rj = __shfl(row0, j0 + jj, 64) + 4 * (uint64_t)lane;
+                        const uint64_t rj = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
 #pragma unroll
                         for (int e = 0; e < 4; e++) pv[jj][e] = payload[rj + e < n ? rj + e : n - 1];
                     }
@@ -1092,13 +1097,16 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
 #pragma unroll
                 for (int jj = 0; jj < kPf; jj++) {
                     const int j = j0 + jj;
-                    if (__shfl(c, j, 64) == 0) continue;
-                    const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
-                                             x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
-                    const unsigned long long oj = __shfl(ol, j, 64);
-                    const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
-                    const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
-                                                            __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
+                    if (__builtin_amdgcn_readlane((int)c, j) == 0) continue;
+                    auto rl64 = [&](unsigned long long x) {
+                        return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
+                               ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
+                    };
+                    const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
+                    const unsigned long long oj = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)olo, j) |
+                                                  ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)ohi, j) << 32);
+                    const uint64_t rj = (tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane;
+                    const unsigned int pre = rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
                     int* q = out + oj + pre;
                     unsigned int k = 0;
                     if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][0] : (int)(rj + 0) + rbase;

@@ -56,7 +56,6 @@ constexpr uint32_t kEq = 0xFFFFFFFFu;
 constexpr int kChainCap = 512;
 constexpr int kMaxJumps = 64;      // doubling steps per level (2^64 > any chain)
 constexpr int kJumpBatch = 4;      // doubling steps launched per host check
-constexpr int kPlainSteps = 32;    // walk steps before the region skips start
 
 struct LSeg {
     uint32_t lo, hi;
@@ -245,8 +244,7 @@ constexpr uint32_t kGe = 0xFFFFFFFFu, kDone = 0x80000000u;
 __global__ __launch_bounds__(kTPB) void k_ld_less(const int32_t* __restrict__ V, const LSeg* __restrict__ seg,
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ imap,
                                                   const uint32_t* __restrict__ segc,
-                                                  const unsigned long long* __restrict__ ex, uint32_t* __restrict__ R,
-                                                  uint32_t* __restrict__ Gpos) {
+                                                  const unsigned long long* __restrict__ ex, uint32_t* __restrict__ R) {
     __shared__ uint32_t sh[kTPB / 64];
     const uint32_t item = blockIdx.x;
     const ItemAt a = item_at(item, imap, seg, ioff);
@@ -287,13 +285,6 @@ __global__ __launch_bounds__(kTPB) void k_ld_less(const int32_t* __restrict__ V,
     uint32_t out[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) out[k] = (m >> k & 1) ? (t[k] | (vt[k] < piv ? 0u : kDone)) : kGe;
-    // the ">=" indexes in order: Gpos[lo + g] = the g-th one (g = its index - lo - the "<"
-    // indexes before it), for the placement's region skips
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + k;
-        if (Gpos && !(m >> k & 1) && i >= lo && i < hi) Gpos[lo + (i - t[k])] = i;
-    }
     if (i0 >= lo && i0 + 7 < hi) {
         *reinterpret_cast<uint4*>(R + i0) = make_uint4(out[0], out[1], out[2], out[3]);
         *reinterpret_cast<uint4*>(R + i0 + 4) = make_uint4(out[4], out[5], out[6], out[7]);
@@ -319,12 +310,11 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
                                                    const LSeg* __restrict__ seg, const uint32_t* __restrict__ ioff,
                                                    const uint32_t* __restrict__ imap, const uint32_t* __restrict__ segc,
                                                    const unsigned long long* __restrict__ ex,
-                                                   const uint32_t* __restrict__ R, const uint32_t* __restrict__ Gpos,
-                                                   int32_t* __restrict__ Vd,
+                                                   const uint32_t* __restrict__ R, int32_t* __restrict__ Vd,
                                                    uint32_t* __restrict__ Pd, int32_t* __restrict__ vout,
                                                    unsigned long long* __restrict__ pout, uint32_t* __restrict__ segflag,
                                                    uint32_t* __restrict__ flist, unsigned int* __restrict__ nflag,
-                                                   const uint32_t* __restrict__ foff, uint32_t F, int cap, int skip) {
+                                                   const uint32_t* __restrict__ foff, uint32_t F, int cap) {
     __shared__ uint32_t s_cnt[8][kTPB / 64];
     uint32_t item;
     ItemAt a;
@@ -397,97 +387,22 @@ __global__ __launch_bounds__(kTPB) void k_ld_final(const int32_t* __restrict__ V
 #pragma unroll
     for (int k = 0; k < 8; k++)
         if (walk >> k & 1) r[k] = R[x[k]];
-    if (!USE_F) {
-        // Plain steps first (most walks end within a few), then region skips (round 4).
-        // Between the last ">=" index g below x and x every index holds a "<" value, and
-        // there R[z] = z - G with G = the ">=" indexes below z, one constant: the walk
-        // steps down by G until it reaches g or passes it. From x (R[x] = t, G = x - t) it
-        // takes one step (to t) when t <= g, else it jumps to x - ceil((x - g) / G) G at
-        // once: g itself (the value found) or an index below g. Both reads (R[t] and
-        // g = Gpos[lo + G - 1]) are issued together; a jump of two steps or more then reads
-        // R at its landing index. A range with few ">=" values (the pivot near its
-        // maximum) has long walks of small strides through wide gaps: they take about one
-        // iteration per gap instead of one per step. (After pointer doubling R no longer
-        // has this form: USE_F walks plainly. MQ_LQ_SKIP=0: no skips, A/B.)
-        int steps = 0;
-        for (; steps < kPlainSteps; steps++) {
+    for (int steps = 0;; steps++) {
+        // r[k]: the back map at x[k]; kGe: x[k] holds its own value; kDone: the next index does
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if (!(walk >> k & 1)) continue;
-                if (r[k] == kGe) {
-                    walk &= ~(1u << k);
-                } else {
-                    x[k] = r[k] & ~kDone;
-                    if (r[k] & kDone) walk &= ~(1u << k);
-                }
-            }
-            if (!walk) break;
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (walk >> k & 1) r[k] = R[x[k]];
-        }
-        for (; walk && steps < cap; steps++) {
-            uint32_t a[8], gg[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                a[k] = 0, gg[k] = 0;
-                if (!(walk >> k & 1)) continue;
-                if (r[k] == kGe) {
-                    walk &= ~(1u << k);
-                    continue;
-                }
-                const uint32_t t = r[k] & ~kDone;
-                if (r[k] & kDone) {
-                    x[k] = t;
-                    walk &= ~(1u << k);
-                    continue;
-                }
-                const uint32_t G = x[k] - t;
-                a[k] = R[t];
-                gg[k] = (skip && G) ? Gpos[lo + G - 1] : t;
-            }
-            if (!walk) break;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if (!(walk >> k & 1)) continue;
-                const uint32_t t = r[k] & ~kDone, G = x[k] - t, g = gg[k];
-                if (G == 0 || t <= g) {  // one step (it reaches g or passes it)
-                    x[k] = t;
-                    r[k] = a[k];
-                } else {  // s >= 2 steps of G at once; s = ceil((x - g) / G) by a float
-                          // quotient, corrected (x - g < 2^31: exact to one)
-                    const uint32_t d = x[k] - g;
-                    uint32_t q = (uint32_t)((float)d * __builtin_amdgcn_rcpf((float)G));
-                    while (q * G < d) q++;
-                    while (q > 1 && (q - 1) * G >= d) q--;
-                    const uint32_t xn = x[k] - q * G;
-                    x[k] = xn;
-                    if (xn == g) {
-                        walk &= ~(1u << k);
-                    } else {
-                        r[k] = R[xn];
-                    }
-                }
+        for (int k = 0; k < 8; k++) {
+            if (!(walk >> k & 1)) continue;
+            if (r[k] == kGe) {
+                walk &= ~(1u << k);
+            } else {
+                x[k] = r[k] & ~kDone;
+                if (r[k] & kDone) walk &= ~(1u << k);
             }
         }
-    } else {
-        for (;;) {
-            // r[k]: the back map at x[k]; kGe: x[k] holds its own value; kDone: the next index does
+        if (!walk || (!USE_F && steps >= cap)) break;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if (!(walk >> k & 1)) continue;
-                if (r[k] == kGe) {
-                    walk &= ~(1u << k);
-                } else {
-                    x[k] = r[k] & ~kDone;
-                    if (r[k] & kDone) walk &= ~(1u << k);
-                }
-            }
-            if (!walk) break;
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                if (walk >> k & 1) r[k] = R[x[k]];
-        }
+        for (int k = 0; k < 8; k++)
+            if (walk >> k & 1) r[k] = R[x[k]];
     }
     if (!USE_F && walk) {  // long walks: placed after the doubling
         dst &= ~walk;
@@ -715,7 +630,7 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
 }
 
 struct LdBufs {
-    void* blk[28];
+    void* blk[24];
     int nb = 0, want = 0;
     ~LdBufs() {
         for (int i = 0; i < nb; i++) pool_free(blk[i]);
@@ -786,7 +701,6 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     int32_t* V[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
     uint32_t* P[2] = {b.get<uint32_t>(n), b.get<uint32_t>(n)};
     uint32_t* R = b.get<uint32_t>(n);  // the back map of the current level
-    uint32_t* Gpos = b.get<uint32_t>(n);  // ... and its ">=" indexes in order (region skips)
     LSeg* seg[2] = {b.get<LSeg>(smax), b.get<LSeg>(smax)};
     uint32_t* ioff[2] = {b.get<uint32_t>(smax), b.get<uint32_t>(smax)};
     uint32_t* segc = b.get<uint32_t>(smax);
@@ -805,7 +719,6 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     unsigned int* chg = reinterpret_cast<unsigned int*>(ctl + 4);
     static const bool stats = getenv("MQ_LQ_STATS") != nullptr;     // per-level diagnostics (stderr)
     static const int cap = getenv("MQ_LQ_CAP") ? atoi(getenv("MQ_LQ_CAP")) : kChainCap;
-    const int skip = !(getenv("MQ_LQ_SKIP") && getenv("MQ_LQ_SKIP")[0] == '0');
     HIPCHK(hipMemsetAsync(ctl, 0, 32, st));  // (ctl32[0] is never reset after this)
     hipLaunchKernelGGL(k_ld_init, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, col, n, V[0], P[0]);
     LAUNCHCHK("k_ld_init");
@@ -838,11 +751,11 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
                            (uint32_t)S, cnt, T, (uint32_t)d, segc, segflag, seg[d], ioff[d], ctl, slist, ctl32);
         LAUNCHCHK("k_ld_children");
         hipLaunchKernelGGL(k_ld_less, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], seg[cur], ioff[cur], imap, segc,
-                           cnt, R, skip ? Gpos : nullptr);
+                           cnt, R);
         LAUNCHCHK("k_ld_less");
         hipLaunchKernelGGL(k_ld_final<false>, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur],
-                           ioff[cur], imap, segc, cnt, R, Gpos, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
-                           (const uint32_t*)nullptr, 0u, cap, skip);
+                           ioff[cur], imap, segc, cnt, R, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
+                           (const uint32_t*)nullptr, 0u, cap);
         LAUNCHCHK("k_ld_final");
         unsigned long long h[2];
         HIPCHK(hipMemcpyAsync(h, ctl, 16, hipMemcpyDeviceToHost, st));
@@ -868,8 +781,8 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
                 if (!ch) break;
             }
             hipLaunchKernelGGL(k_ld_final<true>, dim3(nf), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur], ioff[cur], imap,
-                               segc, cnt, R, (const uint32_t*)nullptr, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
-                               (const uint32_t*)fi, F, 0, 0);
+                               segc, cnt, R, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1, (const uint32_t*)fi, F,
+                               0);
             LAUNCHCHK("k_ld_final");
         }
         nsmall = (uint32_t)h[1];

@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
                 const uint32_t me = valid ? pl[i] : 0u;
                 const uint32_t mq = me >> 16;  // < q <= kMaxQ = 256: 8 bits
                 const unsigned long long peers = match_any8(mq, __ballot(valid));
-                const uint32_t rank = (uint32_t)__popcll(peers & ltmask);
+                const uint32_t rank = lanes_below(peers);
                 const bool last = (peers & ~ltmask & ~(1ull << lane)) == 0;
                 unsigned long long at0 = 0;
                 if (valid) {
@@ -798,6 +798,7 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
     uint32_t* qr = s_qr[wave];
     uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0;
     bool direct = false;
+    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
     auto round = [&](uint32_t nr) {
         const bool has = (uint32_t)lane < nr;
         uint32_t qa = 0, qn = 0, r = 0;
@@ -832,7 +833,8 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         }
         head += nr;
         uint32_t pre = 0, tot = 0;
-        if (!__ballot(qn > 1u)) {  // the usual case: at most one query per row
+        const bool single = !__ballot(qn > 1u);
+        if (single) {  // the usual case: at most one query per row
             const unsigned long long bm = __ballot(qn != 0u);
             pre = mbcnt64(bm);
             tot = (uint32_t)__popcll(bm);
@@ -854,16 +856,24 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         if (tot == 0) return;
         if ((uint64_t)run + tot <= cap) {
             direct = direct || fill + tot > kPb;
-            if (!direct) {
-                uint32_t at = fill + pre;
-                for (uint32_t i = 0; i < qn; i++)
-                    pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
-                fill += tot;
+            // (round 4) the query list read from LDS or global memory by a wave-uniform
+            // branch, and one pair per row without a loop in the usual case: a ternary of
+            // the two pointers compiled to flat loads (both memory paths, and waits on
+            // both), in a per-lane loop
+            // (the list by buffer stores: else the compiler selects between the two
+            // pointers and stores through flat)
+            auto put = [&](uint32_t i, uint32_t y) {
+                if (!direct) pb[fill + pre + i] = y;
+                else __builtin_amdgcn_raw_buffer_store_b32(y, lrs, (int)((run + pre + i) * 4u), 0, 0);
+            };
+            if (single && ql_lds) {
+                if (qn) put(0, ((uint32_t)s_ql[qa] << 24) | r);
+            } else if (ql_lds) {
+                for (uint32_t i = 0; i < qn; i++) put(i, ((uint32_t)s_ql[qa + i] << 24) | r);
             } else {
-                uint32_t at = run + pre;
-                for (uint32_t i = 0; i < qn; i++)
-                    list[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
+                for (uint32_t i = 0; i < qn; i++) put(i, ((uint32_t)T.qlist[qa + i] << 24) | r);
             }
+            if (!direct) fill += tot;
         }
         run += tot;
     };
@@ -883,7 +893,6 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         head = 0;
         tail = rest;
     };
-    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
     constexpr int kV = kSsUnroll * 4;
     for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
         int v[kV];
@@ -1046,7 +1055,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
                 const unsigned long long peers = match_any8(qid, __ballot(valid));
                 const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
                 s_buf[li] = x[b];
-                s_loc[li] = (uint16_t)(before + (uint32_t)__popcll(peers & ltmask));
+                s_loc[li] = (uint16_t)(before + lanes_below(peers));
                 __builtin_amdgcn_wave_barrier();
                 if (valid && (peers & ~ltmask & ~(1ull << lane)) == 0)
                     s_cnt[wave][qid] = before + (uint32_t)__popcll(peers);

@@ -9,7 +9,7 @@ sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "
 import torch  # noqa: E402
 from refapi import mq  # noqa: E402
 
-L = mq.load()
+L = mq.load(os.environ["MQ_LIB"]) if os.environ.get("MQ_LIB") else mq.load()
 mq.check(L.mq_init(0))
 logn = int(sys.argv[1]) if len(sys.argv) > 1 else 27
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2

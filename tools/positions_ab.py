@@ -11,7 +11,7 @@ sys.path[:0] = ['tests', 'oracle']
 import torch
 from refapi import mq
 
-lib = mq.load()
+lib = mq.load(os.environ["MQ_LIB"]) if os.environ.get("MQ_LIB") else mq.load()
 mq.check(lib.mq_init(0))
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000_000
 impls = sys.argv[2].split(',') if len(sys.argv) > 2 else ['stage', 'mask', 'lookback']

@@ -1,11 +1,14 @@
 """select_result timing (not product code): ordered compaction with and without a
 payload (mq_select_positions payload = a second 1e9-row column) at 0.1-50 %
 selectivity, HIP events, median of 5."""
-import sys, json
+import json
+import os
+import sys
 sys.path[:0] = ['tests', 'oracle']
 import torch
 from refapi import mq
-lib = mq.load(); mq.check(lib.mq_init(0))
+lib = mq.load(os.environ["MQ_LIB"]) if os.environ.get("MQ_LIB") else mq.load()
+mq.check(lib.mq_init(0))
 n = 1_000_000_000
 col = torch.empty(n, dtype=torch.int32, device='cuda'); pay = torch.empty(n, dtype=torch.int32, device='cuda')
 mq.check(lib.mq_gen_uniform(col.data_ptr(), n, 42, n, 0)); mq.check(lib.mq_gen_uniform(pay.data_ptr(), n, 43, n, 0))

@@ -11,7 +11,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from refapi import mq  # noqa: E402
 
-L = mq.load()
+L = mq.load(os.environ["MQ_LIB"]) if os.environ.get("MQ_LIB") else mq.load()
 mq.check(L.mq_init(0))
 n = 1_000_000_000
 col = torch.empty(n, dtype=torch.int32, device="cuda")
