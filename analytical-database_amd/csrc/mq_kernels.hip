@@ -902,7 +902,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, uint64_t rw, Pred pred,
     unsigned long long* status, unsigned long long* __restrict__ bm, int* __restrict__ out,
     unsigned long long* __restrict__ d_count, unsigned int* err, int xmode) {
-    __shared__ int s_buf[kWaves][BUF > 0 ? BUF : 1];
+    __shared__ __attribute__((aligned(16))) int s_buf[kWaves][BUF > 0 ? BUF : 1];
     __shared__ unsigned int s_cnt[kWaves];
     __shared__ unsigned long long s_red[kWaves];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1012,9 +1012,30 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     for (uint32_t i = flushed + (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i % (uint32_t)BUF];
     if (sw >= E) return;
     // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     unsigned long long o = D + fill;
     const uint64_t T1 = (E + 255) >> 8;
+    // xmode 1: ring entries [bst, bst + bfill) go to out[ob ...]; bst = out + ob's
+    // dword offset within its 16 bytes
+    unsigned long long ob = o;
+    uint32_t bfill = 0, bst = (uint32_t)(((uintptr_t)(out + ob) >> 2) & 3u);
+    auto flush = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t end = bst + bfill;
+        int* base = out + ob - bst;  // base + q is 16-byte aligned for q % 4 == 0
+        for (uint32_t q = 4u * (uint32_t)lane; q < end; q += 256u) {
+            if (q >= bst && q + 4u <= end) {
+                *reinterpret_cast<int4*>(base + q) = *reinterpret_cast<const int4*>(buf + q);
+            } else {
+#pragma unroll
+                for (uint32_t e = 0; e < 4; e++)
+                    if (q + e >= bst && q + e < end) base[q + e] = buf[q + e];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        ob += bfill;
+        bfill = 0;
+        bst = (uint32_t)(((uintptr_t)(out + ob) >> 2) & 3u);
+    };
     for (uint64_t tb = sw >> 8; tb < T1; tb += 64) {
         const uint64_t T = tb + (uint64_t)lane;
         unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -1036,40 +1057,32 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         const unsigned int tot = __shfl(incl, 63, 64);
         const unsigned long long ol = o + (incl - c);
         const uint64_t row0 = T * 256;
-        if (xmode == 1 && tot > 256) {
-            // staged (round 4): tile by tile, the wave puts the tile's outputs in row
-            // order into its LDS ring (free now: its entries went out above), then
-            // stores them as consecutive dwords, 64 lanes per instruction. Stores
-            // straight from the lanes' rows (below) leave every instruction's
-            // addresses with gaps wherever a row does not match, so the memory
-            // pipeline splits them.
-            const uint64_t tend = tb + 64 < T1 ? tb + 64 : T1;
-            for (uint64_t Tj = tb; Tj < tend; Tj++) {
-                const unsigned long long* wp = bm + Tj * 4;  // wave-uniform
-                const unsigned long long x0 = wp[0], x1 = wp[1], x2 = wp[2], x3 = wp[3];
-                const uint32_t cj = (uint32_t)(__popcll(x0) + __popcll(x1) + __popcll(x2) + __popcll(x3));
+        if (!PAYLOAD && xmode == 1) {
+            // batched (round 4, the default): tiles' outputs gathered in row order in
+            // the wave's LDS ring (free now: its entries went out above), placed so that
+            // ring index and output address agree mod 16 bytes, and flushed when the next
+            // tile would not fit as 16-byte stores, 64 lanes per instruction. Straight
+            // from the lanes' rows (below), every store instruction's addresses have gaps
+            // wherever a row does not match. (A first form flushed every tile behind a
+            // wave barrier: slower at 10-50 %.)
+            for (int j = 0; j < 64; j++) {
+                const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
                 if (cj == 0) continue;
-                const uint64_t rj = Tj * 256 + 4 * (uint64_t)lane;
-                int pv[4] = {0, 0, 0, 0};
-                if constexpr (PAYLOAD) {
-#pragma unroll
-                    for (int e = 0; e < 4; e++) pv[e] = payload[rj + e < n ? rj + e : n - 1];
-                }
-                uint32_t k = (uint32_t)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) + __popcll(x2 & ltmask) +
-                                        __popcll(x3 & ltmask));
-                if ((x0 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[0] : (int)(rj + 0) + rbase;
-                if ((x1 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[1] : (int)(rj + 1) + rbase;
-                if ((x2 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[2] : (int)(rj + 2) + rbase;
-                if ((x3 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[3] : (int)(rj + 3) + rbase;
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const uint32_t e = (uint32_t)i * 64u + (uint32_t)lane;
-                    if (e < cj) out[o + e] = buf[e];
-                }
-                __builtin_amdgcn_wave_barrier();
-                o += cj;
+                if (bst + bfill + cj > (uint32_t)BUF) flush();
+                auto rl64 = [&](unsigned long long x) {
+                    return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
+                           ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
+                };
+                const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
+                const int rj = (int)((tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane) + rbase;
+                uint32_t k = bst + bfill + rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
+                if ((x0 >> lane) & 1ull) buf[k++] = rj + 0;
+                if ((x1 >> lane) & 1ull) buf[k++] = rj + 1;
+                if ((x2 >> lane) & 1ull) buf[k++] = rj + 2;
+                if ((x3 >> lane) & 1ull) buf[k++] = rj + 3;
+                bfill += cj;
             }
+            o += tot;
             continue;
         }
         if (tot > 1024) {
@@ -1131,6 +1144,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         }
         o += tot;
     }
+    if (!PAYLOAD && xmode == 1 && bfill) flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -1827,11 +1841,13 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     unsigned long long* bm = reinterpret_cast<unsigned long long*>(w + partial_bytes());
     HIPCHK(hipMemsetAsync(w, 0, stage_state_bytes(g), st));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
-    // MQ_STAGE_EXPAND=1: the bitmap tiles expanded through the LDS ring into coalesced
-    // stores. Measured and kept off: 1.19 / 1.55 / 1.79 ms at 10 / 50 / 100 % against
-    // 1.11 / 1.49 / 1.82 ms for the lane-scattered stores (profiles/r04_positions_ab.log)
+    // The bitmap tiles expanded through the LDS ring into 16-byte stores, several tiles
+    // a flush (default), or (MQ_STAGE_EXPAND=0) by lane-scattered dword stores: 1.022 /
+    // 1.355 / 1.56 ms against 1.064 / 1.475 / 1.84 ms at 10 / 50 / 100 % alternating on
+    // one box (profiles/r04_positions_batched_ab.log; a first staged form that flushed
+    // every tile lost to the lanes, profiles/r04_positions_ab.log)
     const char* xe = getenv("MQ_STAGE_EXPAND");
-    const int xmode = xe && xe[0] == '1' ? 1 : 0;
+    const int xmode = xe && xe[0] == '0' ? 0 : 1;
     if (payload) {
         if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
         else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);

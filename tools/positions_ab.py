@@ -1,5 +1,5 @@
 """A/B of the ordered-compaction paths (MQ_POSITIONS_IMPL = stage | mask | lookback, and
-stage_staged: stage with MQ_STAGE_EXPAND=1) on
+stage_lanes: stage with MQ_STAGE_EXPAND=0, the lane-scattered bitmap expansion) on
 1e9 rows at several selectivities, each output fully checked: K equals the fused
 count, positions strictly ascending, every position's value in range (together:
 exactly the reference's list)."""
@@ -29,9 +29,9 @@ for sel in (0.001, 0.01, 0.1, 0.5, 1.0):
     mq.check(lib.mq_select_agg(col.data_ptr(), n, 1, lo, 1, hi, agg.data_ptr(), ws.data_ptr(), ws_b, 0))
     want = int(agg[0].item())
     for impl in impls:
-        # stage_staged: k_select_stage with the LDS-staged bitmap expansion (MQ_STAGE_EXPAND=1)
+        # stage_lanes: k_select_stage with the lane-scattered bitmap expansion (MQ_STAGE_EXPAND=0)
         os.environ['MQ_POSITIONS_IMPL'] = 'stage' if impl.startswith('stage') else impl
-        os.environ['MQ_STAGE_EXPAND'] = '1' if impl == 'stage_staged' else '0'
+        os.environ['MQ_STAGE_EXPAND'] = '0' if impl == 'stage_lanes' else '1'
 
         def run():
             mq.check(lib.mq_select_positions(col.data_ptr(), None, n, 1, lo, 1, hi, pos.data_ptr(),
