@@ -581,8 +581,8 @@ def _dev_join(lib, c1, p1, c2, p2):
     return o1.get(np.int32, m), o2.get(np.int32, m)
 
 
-JOIN_PATHS = {"winruns": {}, "winruns_plain": {"MQ_JOIN_SEC": "0"}, "winruns16": {"MQ_JOIN_SLOT16": "1"},
-              "sorted": {"MQ_JOIN_WINRUNS": "0"}, "cas": {"MQ_JOIN_RUNS": "0"}}
+JOIN_PATHS = {"winruns": {}, "winruns16": {"MQ_JOIN_SLOT16": "1"}, "sorted": {"MQ_JOIN_WINRUNS": "0"},
+              "cas": {"MQ_JOIN_RUNS": "0"}}
 
 
 @pytest.mark.parametrize("path", list(JOIN_PATHS))
@@ -591,9 +591,7 @@ JOIN_PATHS = {"winruns": {}, "winruns_plain": {"MQ_JOIN_SEC": "0"}, "winruns16":
                                   "ragged_hits", "dups_short_runs", "dups_run_of_15"])
 def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
     """Duplicate keys: winruns (default) partitions the build rows by window and finds
-    each window's runs in LDS (k_win_build_runs), its table in the sector layout (a
-    bucket's runs of one or two rows inline in the bucket's 64-byte line); winruns_plain
-    the same in the plain 8-byte-slot layout (MQ_JOIN_SEC=0); winruns16 the same into 16-byte slots
+    each window's runs in LDS (k_win_build_runs); winruns16 the same into 16-byte slots
     that carry runs of one or two rows (k_win_build_runs16, MQ_JOIN_SLOT16=1);
     a window over 6144 rows or 3072 keys, or a key on 15+ rows, falls back to: sorted,
     the sorted runs behind the windowed table of distinct keys (MQ_JOIN_WINRUNS=0);
