@@ -79,20 +79,17 @@ __global__ void k_tile_seg(const Seg* __restrict__ segs, uint32_t* __restrict__ 
     for (uint32_t i = threadIdx.x; i < sg.nt; i += blockDim.x) tseg[sg.t0 + i] = blockIdx.x;
 }
 
-// The tile's range, its tile index within the range and its row count (tiles of
-// kMT x MI rows).
-template <int MI = kMI>
+// The tile's range, its tile index within the range and its row count.
 __device__ __forceinline__ void tile_range(const Seg* segs, const uint32_t* tseg, uint32_t t, Seg& sg, uint32_t& tin,
                                            uint32_t& len) {
-    constexpr uint32_t kT = (uint32_t)kMT * MI;
     sg = segs[tseg[t]];
     tin = t - sg.t0;
-    const uint32_t r = sg.len - tin * kT;
-    len = r < kT ? r : kT;
+    const uint32_t r = sg.len - tin * kMTile;
+    len = r < kMTile ? r : kMTile;
 }
 
 // Per tile: counts of the level's digit, into hist[t0 * P + d * nt + tin].
-template <bool FIRST, bool WIDE, int MI = kMI>
+template <bool FIRST, bool WIDE>
 __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, const uint8_t* __restrict__ dig,
                                                   const Seg* __restrict__ segs, const uint32_t* __restrict__ tseg,
                                                   uint32_t kmin, u64 M, uint32_t P, uint32_t* __restrict__ hist) {
@@ -102,11 +99,11 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
     __syncthreads();
     Seg sg;
     uint32_t tin, len;
-    tile_range<MI>(segs, tseg, xcd_tile(blockIdx.x, gridDim.x), sg, tin, len);
-    const u64 e0 = sg.start + (u64)tin * ((uint32_t)kMT * MI);
-    uint32_t d[MI];
+    tile_range(segs, tseg, xcd_tile(blockIdx.x, gridDim.x), sg, tin, len);
+    const u64 e0 = sg.start + (u64)tin * kMTile;
+    uint32_t d[kMI];
 #pragma unroll
-    for (int k = 0; k < MI; k++) {
+    for (int k = 0; k < kMI; k++) {
         const uint32_t i = (uint32_t)k * kMT + tid;
         const u64 ic = e0 + (i < len ? i : len - 1);
         if constexpr (FIRST)
@@ -115,7 +112,7 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
             d[k] = (uint32_t)__builtin_nontemporal_load(dig + ic);
     }
 #pragma unroll
-    for (int k = 0; k < MI; k++)
+    for (int k = 0; k < kMI; k++)
         if ((uint32_t)k * kMT + tid < len) atomicAdd(&h[d[k]], 1u);
     __syncthreads();
     if (tid < (int)P) hist[(u64)sg.t0 * P + (u64)tid * sg.nt + tin] = h[tid];
@@ -176,7 +173,7 @@ __device__ __forceinline__ void digit_offsets(uint32_t (*wcnt)[256], uint32_t* l
 // Stable scatter of a level: each tile's words ranked by digit in LDS, then written
 // as contiguous digit runs at the range's start + the scanned offsets. Mn != 0: also
 // the next level's digit of every word (of its key relative to its child range).
-template <bool FIRST, bool WIDE, bool NWIDE, int MI = kMI>
+template <bool FIRST, bool WIDE, bool NWIDE>
 __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col, const u64* __restrict__ in,
                                                      const Seg* __restrict__ segs, const uint32_t* __restrict__ tseg,
                                                      const uint32_t* __restrict__ hscan, uint32_t kmin, u64 M,
@@ -187,26 +184,26 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
     __shared__ uint32_t loff[256];
     __shared__ u64 gofs[256];
     __shared__ uint32_t clo[256];
-    __shared__ u64 stage[kMT * MI];
+    __shared__ u64 stage[kMTile];
     __shared__ uint32_t wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int x = tid; x < kW * 256; x += kMT) (&wcnt[0][0])[x] = 0;
     Seg sg;
     uint32_t tin, len;
-    tile_range<MI>(segs, tseg, xcd_tile(blockIdx.x, gridDim.x), sg, tin, len);
+    tile_range(segs, tseg, xcd_tile(blockIdx.x, gridDim.x), sg, tin, len);
     const u64 hb = (u64)sg.t0 * P;
     if (tid < (int)P) {
         gofs[tid] = sg.start + (u64)(hscan[hb + (u64)tid * sg.nt + tin] - hscan[hb]);
         clo[tid] = Mn ? (uint32_t)digit_lo(tid, M) : 0u;
     }
     __syncthreads();
-    const u64 e0 = sg.start + (u64)tin * ((uint32_t)kMT * MI);
-    const uint32_t wbase = (uint32_t)wave * (64 * MI);
+    const u64 e0 = sg.start + (u64)tin * kMTile;
+    const uint32_t wbase = (uint32_t)wave * (64 * kMI);
     const uint32_t kbase = kmin + sg.klo;
-    u64 el[MI];
-    uint32_t dr[MI];
+    u64 el[kMI];
+    uint32_t dr[kMI];
 #pragma unroll
-    for (int k = 0; k < MI; k++) {
+    for (int k = 0; k < kMI; k++) {
         const uint32_t i = wbase + (uint32_t)k * 64 + lane;
         const u64 ic = e0 + (i < len ? i : len - 1);
         if constexpr (FIRST)
@@ -214,11 +211,11 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
         else
             el[k] = in[ic];
     }
-    rank_items<MI, true, WIDE>(el, dr, wbase, len, kbase, 0, 0, M, wcnt[wave], lane);
+    rank_items<kMI, true, WIDE>(el, dr, wbase, len, kbase, 0, 0, M, wcnt[wave], lane);
     __syncthreads();
     digit_offsets<kW>(wcnt, loff, wsum, tid);
 #pragma unroll
-    for (int k = 0; k < MI; k++) {
+    for (int k = 0; k < kMI; k++) {
         if (dr[k] != 0xFFFFFFFFu) {
             const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
             stage[loff[d] + wcnt[wave][d] + r] = el[k];
@@ -226,7 +223,7 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < MI; k++) {
+    for (int k = 0; k < kMI; k++) {
         const uint32_t e = (uint32_t)k * kMT + tid;
         if (e < len) {
             const u64 v = stage[e];
@@ -658,11 +655,7 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
     };
     if (!wb[0] || !wb[1] || !dig || !hist || !tseg || !scratch || !sl[0] || !sl[1] || !ctr)
         return done(set_err(MQ_ENOMEM, "index sort: buffers (%llu rows)", (unsigned long long)n));
-    // MQ_ISORT_TILE0=32: the first level in tiles of 512 x 32 rows (its digit runs twice
-    // as long in the 8 GB output; 128 KB of LDS, one block a CU), A/B
-    const char* t0e = getenv("MQ_ISORT_TILE0");
-    const int mi0 = t0e && atoi(t0e) == 32 ? 32 : kMI;
-    Seg s0{0, (uint32_t)n, 0, (uint32_t)cdiv(n, (uint64_t)kMT * mi0), 0};
+    Seg s0{0, (uint32_t)n, 0, (uint32_t)cdiv(n, kMTile), 0};
     if (hipMemcpyAsync(sl[0], &s0, sizeof s0, hipMemcpyHostToDevice, st) != hipSuccess)
         return done(set_err(MQ_EHIP, "index sort: upload"));
     uint32_t nseg = 1, ntile = s0.nt;
@@ -682,13 +675,7 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
         if (!fl[level] || !rl[level] || !bl[level]) return done(set_err(MQ_ENOMEM, "index sort: range list"));
         hipLaunchKernelGGL(k_tile_seg, dim3(nseg), dim3(256), 0, st, cur, tseg);
         const bool wide = M >> 32 != 0;
-        if (level == 0 && wide && mi0 == 32)
-            hipLaunchKernelGGL((k_msd_hist<true, true, 32>), dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg,
-                               kmin, M, P, hist);
-        else if (level == 0 && mi0 == 32)
-            hipLaunchKernelGGL((k_msd_hist<true, false, 32>), dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg,
-                               kmin, M, P, hist);
-        else if (level == 0 && wide)
+        if (level == 0 && wide)
             hipLaunchKernelGGL((k_msd_hist<true, true>), dim3(ntile), dim3(kMT), 0, st, col, nullptr, cur, tseg, kmin,
                                M, P, hist);
         else if (level == 0)
@@ -719,14 +706,7 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
         // digits by one v_mul_hi_u32 where the multipliers fit 32 bits (the usual case)
         const u64* lin = level == 0 ? nullptr : wb[dst ^ 1];
         const int* lcol = level == 0 ? col : nullptr;
-        if (level == 0 && mi0 == 32) {
-            if (!wide && !(Mn >> 32))
-                hipLaunchKernelGGL((k_msd_scatter<true, false, false, 32>), dim3(ntile), dim3(kMT), 0, st, lcol, lin,
-                                   cur, tseg, hist, kmin, M, P, Mn, wb[dst], dig);
-            else
-                hipLaunchKernelGGL((k_msd_scatter<true, true, true, 32>), dim3(ntile), dim3(kMT), 0, st, lcol, lin, cur,
-                                   tseg, hist, kmin, M, P, Mn, wb[dst], dig);
-        } else if (!wide && !(Mn >> 32)) {
+        if (!wide && !(Mn >> 32)) {
             if (level == 0)
                 hipLaunchKernelGGL((k_msd_scatter<true, false, false>), dim3(ntile), dim3(kMT), 0, st, lcol, lin, cur,
                                    tseg, hist, kmin, M, P, Mn, wb[dst], dig);
