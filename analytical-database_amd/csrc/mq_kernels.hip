@@ -1057,30 +1057,46 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         const unsigned int tot = __shfl(incl, 63, 64);
         const unsigned long long ol = o + (incl - c);
         const uint64_t row0 = T * 256;
-        if (!PAYLOAD && xmode == 1) {
+        if (xmode == 1) {
             // batched (round 4, the default): tiles' outputs gathered in row order in
             // the wave's LDS ring (free now: its entries went out above), placed so that
             // ring index and output address agree mod 16 bytes, and flushed when the next
             // tile would not fit as 16-byte stores, 64 lanes per instruction. Straight
             // from the lanes' rows (below), every store instruction's addresses have gaps
             // wherever a row does not match. (A first form flushed every tile behind a
-            // wave barrier: slower at 10-50 %.)
-            for (int j = 0; j < 64; j++) {
-                const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
-                if (cj == 0) continue;
-                if (bst + bfill + cj > (uint32_t)BUF) flush();
-                auto rl64 = [&](unsigned long long x) {
-                    return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
-                           ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
-                };
-                const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
-                const int rj = (int)((tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane) + rbase;
-                uint32_t k = bst + bfill + rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
-                if ((x0 >> lane) & 1ull) buf[k++] = rj + 0;
-                if ((x1 >> lane) & 1ull) buf[k++] = rj + 1;
-                if ((x2 >> lane) & 1ull) buf[k++] = rj + 2;
-                if ((x3 >> lane) & 1ull) buf[k++] = rj + 3;
-                bfill += cj;
+            // wave barrier: slower at 10-50 %.) select_result: the payload rows of 4 tiles
+            // are loaded before any of them is placed.
+            constexpr int kPf = PAYLOAD ? 4 : 1;
+            for (int j0 = 0; j0 < 64; j0 += kPf) {
+                int pv[kPf][4];
+                if constexpr (PAYLOAD) {
+#pragma unroll
+                    for (int jj = 0; jj < kPf; jj++) {
+                        const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
+                        const bool any = __builtin_amdgcn_readlane((int)c, j0 + jj) != 0;
+#pragma unroll
+                        for (int e = 0; e < 4; e++) pv[jj][e] = any ? payload[r + e < n ? r + e : n - 1] : 0;
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < kPf; jj++) {
+                    const int j = j0 + jj;
+                    const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
+                    if (cj == 0) continue;
+                    if (bst + bfill + cj > (uint32_t)BUF) flush();
+                    auto rl64 = [&](unsigned long long x) {
+                        return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
+                               ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
+                    };
+                    const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
+                    const int rj = (int)((tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane) + rbase;
+                    uint32_t k = bst + bfill + rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
+                    if ((x0 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][0] : rj + 0;
+                    if ((x1 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][1] : rj + 1;
+                    if ((x2 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][2] : rj + 2;
+                    if ((x3 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][3] : rj + 3;
+                    bfill += cj;
+                }
             }
             o += tot;
             continue;
@@ -1144,7 +1160,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         }
         o += tot;
     }
-    if (!PAYLOAD && xmode == 1 && bfill) flush();
+    if (xmode == 1 && bfill) flush();
 }
 
 // ---------------------------------------------------------------------------
