@@ -55,7 +55,12 @@ constexpr uint32_t kEq = 0xFFFFFFFFu;
 // chain steps walked before pointer doubling takes over (MQ_LQ_CAP)
 constexpr int kChainCap = 512;
 constexpr int kMaxJumps = 64;      // doubling steps per level (2^64 > any chain)
-constexpr int kJumpBatch = 4;      // doubling steps launched per host check
+constexpr int kJumpBatch = 16;     // doubling steps launched per host check (4: 70.5 ms, 8: 69.6, 16: 68.6)
+// Levels of at most kSmallItems items (late levels: few rows, where one walk of up to
+// kChainCap steps set each level's time) walk at most kChainCapSmall steps before
+// doubling: 70.5 -> 69.3 ms (with 8 steps a check, 68.0; profiles/r04_lomuto_knobs2.log)
+constexpr int kChainCapSmall = 64;
+constexpr uint64_t kSmallItems = 2048;
 
 struct LSeg {
     uint32_t lo, hi;
@@ -719,6 +724,12 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     unsigned int* chg = reinterpret_cast<unsigned int*>(ctl + 4);
     static const bool stats = getenv("MQ_LQ_STATS") != nullptr;     // per-level diagnostics (stderr)
     static const int cap = getenv("MQ_LQ_CAP") ? atoi(getenv("MQ_LQ_CAP")) : kChainCap;
+    // A/B knobs (round 4): doubling steps per host check, and a walk limit for levels of
+    // at most MQ_LQ_SMALL_ITEMS items (late levels: a few rows, one long walk)
+    static const int jbatch = getenv("MQ_LQ_JUMPS") ? atoi(getenv("MQ_LQ_JUMPS")) : kJumpBatch;
+    static const int cap_small = getenv("MQ_LQ_CAP_SMALL") ? atoi(getenv("MQ_LQ_CAP_SMALL")) : kChainCapSmall;
+    static const uint64_t small_items =
+        getenv("MQ_LQ_SMALL_ITEMS") ? strtoull(getenv("MQ_LQ_SMALL_ITEMS"), nullptr, 10) : kSmallItems;
     HIPCHK(hipMemsetAsync(ctl, 0, 32, st));  // (ctl32[0] is never reset after this)
     hipLaunchKernelGGL(k_ld_init, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, col, n, V[0], P[0]);
     LAUNCHCHK("k_ld_init");
@@ -755,7 +766,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
         LAUNCHCHK("k_ld_less");
         hipLaunchKernelGGL(k_ld_final<false>, dim3((uint32_t)NI), dim3(kTPB), 0, st, V[cur], P[cur], seg[cur],
                            ioff[cur], imap, segc, cnt, R, V[d], P[d], vout, pout, segflag, flist, ctl32 + 1,
-                           (const uint32_t*)nullptr, 0u, cap);
+                           (const uint32_t*)nullptr, 0u, NI <= small_items ? cap_small : cap);
         LAUNCHCHK("k_ld_final");
         unsigned long long h[2];
         HIPCHK(hipMemcpyAsync(h, ctl, 16, hipMemcpyDeviceToHost, st));
@@ -771,7 +782,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
             HIPCHK(hipStreamSynchronize(st));
             for (;;) {
                 if (jumps >= kMaxJumps) return set_err(MQ_EHIP, "mq_index_build_lomuto: pointer doubling did not converge");
-                for (int k = 0; k < kJumpBatch; k++, jumps++) {
+                for (int k = 0; k < jbatch && jumps < kMaxJumps; k++, jumps++) {
                     hipLaunchKernelGGL(k_ld_jump, dim3(nf), dim3(kTPB), 0, st, seg[cur], flist, fi, F, R, chg, jumps);
                     LAUNCHCHK("k_ld_jump");
                 }
