@@ -1036,17 +1036,31 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
         s_out[i] = global_ptr(outs[i]);
     }
+    // (round 4) the wave's 1024 pairs of the next chunk are loaded while this chunk is
+    // ranked, sorted and written (the loads of a chunk used to open it: 9 chunks a block
+    // at Q = 150, each waiting for its own round trip)
+    uint32_t nx[kSpRounds];
+    auto load_chunk = [&](uint32_t c0) {
+#pragma unroll
+        for (int r = 0; r < kSpRounds; r++) {
+            const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
+            nx[r] = idx < np ? list[idx] : 0u;
+        }
+    };
+    load_chunk(0);
     for (uint32_t c0 = 0; c0 < np; c0 += kSpChunk) {
+        uint32_t cx[kSpRounds];
+#pragma unroll
+        for (int r = 0; r < kSpRounds; r++) cx[r] = nx[r];
+        if (c0 + kSpChunk < np) load_chunk(c0 + kSpChunk);
         for (int i = tid; i < kWaves * kMaxQ; i += kTPB) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
-        // this wave's 1024 pairs of the chunk, kSpBatch rounds' loads at a time
+        // this wave's 1024 pairs of the chunk
+#pragma unroll
         for (int r0 = 0; r0 < kSpRounds; r0 += kSpBatch) {
             uint32_t x[kSpBatch];
 #pragma unroll
-            for (int b = 0; b < kSpBatch; b++) {
-                const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
-                x[b] = idx < np ? list[idx] : 0u;
-            }
+            for (int b = 0; b < kSpBatch; b++) x[b] = cx[r0 + b];
 #pragma unroll
             for (int b = 0; b < kSpBatch; b++) {
                 const uint32_t li = (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
