@@ -106,6 +106,31 @@ def test_select_agg_and_positions_vs_oracle(lib, refcpu, n, pos_impl):
             assert (c, sm) == (a.count, a.sum), (n, off, lo, hi)
 
 
+@pytest.mark.parametrize("out_off", [1, 2, 3])
+def test_positions_into_unaligned_output(lib, refcpu, out_off, pos_impl):
+    """The output pointer 4 / 8 / 12 B past a 16-byte boundary: the batched bitmap
+    expansion (round 4) flushes its LDS ring as 16-byte stores placed by the output
+    address, so a base that is not 16-byte aligned shifts every flush. Dense ranges
+    (bitmap mode) and a sparse one, positions and the payload form."""
+    n = 3_000_017
+    d = _data(n, 77)
+    pay = (np.arange(n, dtype=np.int64) * 7 - 5).astype(np.int32)
+    dd, dp = Dev.of(d), Dev.of(pay)
+    ws = Dev(lib.mq_scan_workspace_bytes(n))
+    out = Dev((n + 8) * 4)
+    cnt = Dev(8)
+    for lo, hi in ((-25, 25), (-10, 10), (0, 0), (24, 24)):
+        want = refcpu.select_scan(d, lo, hi)
+        for payload in (None, dp.ptr):
+            hl, l, hh, h = mq.bounds(lo, hi)
+            mq.check(lib.mq_select_positions(dd.ptr, payload, n, hl, l, hh, h, out.ptr + 4 * out_off, cnt.ptr,
+                                             ws.ptr, ws.nbytes, None))
+            k = int(cnt.get(np.uint64, 1)[0])
+            got = out.get(np.int32, k + out_off)[out_off:]
+            assert k == len(want), (out_off, lo, hi, payload is not None)
+            assert np.array_equal(got, pay[want] if payload else want), (out_off, lo, hi, payload is not None)
+
+
 def _select_sum(L, dcol_ptr, n, lo, hi, ws=None, out=None):
     """mq_select_sum: one launch, partials folded by the last block to arrive."""
     ws = ws or Dev(L.mq_scan_workspace_bytes(n))
