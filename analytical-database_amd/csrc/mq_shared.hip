@@ -251,6 +251,7 @@ constexpr int kEiMinQ = 12;  // measured crossover (count + write, 1e9 rows): Q=
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
+constexpr int kSsPfMinQ = 64;   // k_ssk_count prefetches the next group from this many queries
 constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
 constexpr int kBucketsP = kBuckets / 2;  // k_ssp_count's bucket table (LDS)
 constexpr int kCoarse = 16384;           // k_ssp_count's coverage bitmap cells
@@ -753,7 +754,7 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <bool VEC>
+template <bool PF>
 __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
@@ -894,18 +895,37 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         tail = rest;
     };
     constexpr int kV = kSsUnroll * 4;
-    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
-        int v[kV];
-        const bool whole = t + kWaveTile * kSsUnroll <= e;
-        if (whole) {
+    constexpr uint64_t kG = kWaveTile * kSsUnroll;
+    auto load_group = [&](uint64_t t0, int* x) {
+        if (t0 + kG <= e) {
 #pragma unroll
-            for (int i = 0; i < kV; i++) v[i] = __builtin_nontemporal_load(col + t + (uint64_t)i * 64 + lane);
+            for (int i = 0; i < kV; i++) x[i] = __builtin_nontemporal_load(col + t0 + (uint64_t)i * 64 + lane);
         } else {
 #pragma unroll
             for (int i = 0; i < kV; i++) {
-                const uint64_t row = t + (uint64_t)i * 64 + lane;
-                v[i] = row < e ? col[row] : 0;
+                const uint64_t row = t0 + (uint64_t)i * 64 + lane;
+                x[i] = row < e ? col[row] : 0;
             }
+        }
+    };
+    // PF (round 4): the next group's loads are issued before this group is queued and
+    // drained, so a wave keeps a group in flight while its rounds run (without it the
+    // wave's next loads wait for its whole drain)
+    int v[kV];
+    if (PF && s < e) {
+        load_group(s, v);
+        // the first group waited for here: otherwise the loop entry merges "v pending"
+        // from here with "v copied" from the back edge, and the wait-count pass then
+        // waits inside every iteration for the next group's loads
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    for (uint64_t t = s; t < e; t += kG) {
+        const bool whole = t + kG <= e;
+        int vn[kV];
+        if (PF) {
+            if (t + kG < e) load_group(t + kG, vn);
+        } else {
+            load_group(t, v);
         }
         {  // the previous group's pairs, behind this group's loads
             __builtin_amdgcn_wave_barrier();
@@ -954,6 +974,10 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         }
         pend = fill;
         pend_at = grp_at;
+        if (PF) {
+#pragma unroll
+            for (int i = 0; i < kV; i++) v[i] = vn[i];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
@@ -1118,9 +1142,18 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
         for (int k = 0; k < kSpPer; k++)
             if (pd[k] != 0xFFFFFFFFu) s_buf[pd[k]] = px[k];
         __syncthreads();
-        for (uint32_t i = tid; i < cn; i += kTPB) {
-            const uint32_t y = s_buf[i], qid = y >> 24;
-            s_out[qid][s_run[qid] + (i - s_start[qid])] = (int)(row0 + (y & 0xFFFFFFu)) + base;
+        // (round 4) a fixed 16 stores a thread, the slots past the chunk's end going to a
+        // pair of this chunk already read (the slice is not read again): with a
+        // data-dependent count the wait for the next chunk's loads at the loop's top was
+        // vmcnt(0), i.e. also for every store of this chunk
+        gint* const dummy = (gint*)(const_cast<uint32_t*>(list) + c0);
+#pragma unroll
+        for (int k = 0; k < kSpPer; k++) {
+            const uint32_t i = (uint32_t)(k * kTPB + tid);
+            const bool in = i < cn;
+            const uint32_t y = s_buf[i], qid = in ? y >> 24 : 0u;
+            gint* const dst = in ? s_out[qid] + (s_run[qid] + (i - s_start[qid])) : dummy;
+            *dst = (int)(row0 + (y & 0xFFFFFFu)) + base;
         }
         __syncthreads();
         if (tid < q) s_run[tid] += s_tot[tid];
@@ -1431,7 +1464,13 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     // the single-pass EI path (its LDS allows 3 blocks a CU), else the write pass
     static const bool filt = getenv("MQ_SS_COUNT") && strcmp(getenv("MQ_SS_COUNT"), "filter") == 0;
     const bool kmajor = ei && !filt && getenv("MQ_SS_TWOPASS") == nullptr;
-    const void* fn = kmajor ? (vec ? (const void*)&k_ssk_count<true> : (const void*)&k_ssk_count<false>)
+    // k_ssk_count with the next group's loads issued ahead from kSsPfMinQ queries (1e9
+    // rows, 0.1 % each, alternating on one box: Q = 150 1.85 -> 1.81 ms, Q = 16 0.93 ->
+    // 0.96 ms, where the rounds are few and the stream alone sets the time);
+    // MQ_SS_PF=0 / 1 forces it off / on (A/B)
+    static const char* pfe = getenv("MQ_SS_PF");
+    const bool pf = pfe ? pfe[0] != '0' : qk >= kSsPfMinQ;
+    const void* fn = kmajor ? (pf ? (const void*)&k_ssk_count<true> : (const void*)&k_ssk_count<false>)
                    : ei     ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
                             : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
     uint32_t g = 1;
@@ -1470,7 +1509,7 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
                                        nwc, pr, cap, npr, of);
                 LAUNCHCHK("k_ssp_count");
             } else {
-                if (vec)
+                if (pf)
                     hipLaunchKernelGGL(k_ssk_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
                                        nwc, pr, cap, npr, of);
                 else
