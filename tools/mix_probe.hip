@@ -24,31 +24,38 @@
         }                                                                        \
     } while (0)
 
-// rows per wave = rpw (a multiple of 1024); npg pairs written per 1024-row group
+// rows per wave = rpw (a multiple of 1024); npg pairs written per 1024-row group.
+// B: the pairs of B groups go out together (4 B buffer stores, after the loads of the
+// group that closes the batch); AUX: the stores' cache policy bits (2 = nontemporal)
+template <int B, int AUX>
 __global__ __launch_bounds__(256) void k_mix(const int* __restrict__ col, uint64_t rpw, uint32_t npg,
                                              uint32_t* __restrict__ pairs, uint64_t cap, int* __restrict__ sink) {
     const int lane = threadIdx.x & 63;
     const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int* c = col + w * rpw;
     uint32_t* list = pairs + w * cap;
-    // as k_ssk_count: the previous group's pairs go out after this group's loads, as 4
-    // buffer stores whose range drops the unused lanes (a fixed count per group)
+    // as k_ssk_count: pairs go out after a group's loads, as buffer stores whose range
+    // drops the unused lanes (a fixed count)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
     uint32_t run = 0, pend = 0;
     int acc = 0;
-    for (uint64_t t = 0; t < rpw; t += 1024) {
+    uint64_t g = 0;
+    for (uint64_t t = 0; t < rpw; t += 1024, g++) {
         int v[16];
 #pragma unroll
         for (int i = 0; i < 16; i++) v[i] = __builtin_nontemporal_load(c + t + (uint64_t)i * 64 + lane);
+        if (g % B == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t i = (uint32_t)(k * 64 + lane);
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc + i, rs,
-                                                  i < pend ? (int)((run - pend + i) * 4u) : (int)0x80000000u, 0, 0);
+            for (int k = 0; k < 4 * B; k++) {
+                const uint32_t i = (uint32_t)(k * 64 + lane);
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc + i, rs,
+                                                      i < pend ? (int)((run - pend + i) * 4u) : (int)0x80000000u, 0, AUX);
+            }
+            pend = 0;
         }
 #pragma unroll
         for (int i = 0; i < 16; i++) acc ^= v[i];
-        pend = npg;
+        pend += npg;
         run += npg;
     }
     if (acc == 0x7fffffff) sink[0] = acc;
@@ -83,12 +90,21 @@ int main() {
     CK(hipMalloc(&sink, 64));
     CK(hipMalloc(&pairs, waves * cap * 4));
     CK(hipMemset(col, 1, n * 4));
-    for (uint32_t npg : {0u, 16u, 64u, 154u, 256u}) {
-        const float ms = timed([&] { hipLaunchKernelGGL(k_mix, dim3(1024), dim3(256), 0, 0, col, rpw, npg, pairs, cap, sink); });
+    auto go = [&](const char* form, auto kern, uint32_t npg) {
+        const float ms = timed([&] { hipLaunchKernelGGL(kern, dim3(1024), dim3(256), 0, 0, col, rpw, npg, pairs, cap, sink); });
         const double rb = 4.0 * n, wb = 4.0 * npg * (double)(n / 1024);
-        printf("{\"what\":\"mix\",\"rows\":%llu,\"pairs_per_1024\":%u,\"read_gb\":%.3f,\"write_gb\":%.3f,\"ms\":%.3f,"
-               "\"tbs\":%.2f}\n",
-               (unsigned long long)n, npg, rb / 1e9, wb / 1e9, ms, (rb + wb) / ms / 1e9);
+        printf("{\"what\":\"mix\",\"form\":\"%s\",\"rows\":%llu,\"pairs_per_1024\":%u,\"read_gb\":%.3f,"
+               "\"write_gb\":%.3f,\"ms\":%.3f,\"tbs\":%.2f}\n",
+               form, (unsigned long long)n, npg, rb / 1e9, wb / 1e9, ms, (rb + wb) / ms / 1e9);
+    };
+    const bool all = getenv("MIX_ALL") != nullptr;
+    for (uint32_t npg : {0u, 16u, 64u, 154u, 256u}) go("per_group", k_mix<1, 0>, npg);
+    if (all) {
+        for (uint32_t npg : {16u, 154u}) {
+            go("per_group_nt", k_mix<1, 2>, npg);
+            go("batch4", k_mix<4, 0>, npg);
+            go("batch16", k_mix<16, 0>, npg);
+        }
     }
     return 0;
 }
