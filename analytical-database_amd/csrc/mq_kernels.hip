@@ -2004,8 +2004,8 @@ struct Staging {
 thread_local Staging g_staging[kMaxDev];
 
 // The host side of the staged D2H: each chunk copied out of the pinned buffer by
-// the calling thread and kCopyHelpers helpers (one memcpy thread moved ~10 GB/s,
-// a quarter of the DMA rate). One pool per calling thread (row-shard workers copy
+// the calling thread and MQ_COPY_THREADS - 1 helpers (one memcpy thread moved ~10 GB/s,
+// a quarter of the DMA rate; 6 threads, round 4: see FaultPool). One pool per calling thread (row-shard workers copy
 // concurrently); helpers are started on first use and joined at thread exit.
 struct CopyPool {
     std::vector<std::thread> th;
@@ -2020,7 +2020,7 @@ struct CopyPool {
 
     void start() {
         const char* e = getenv("MQ_COPY_THREADS");
-        parts = e ? atoi(e) : 4;
+        parts = e ? atoi(e) : 6;
         if (parts < 1) parts = 1;
         if (parts > 16) parts = 16;
         for (int i = 1; i < parts; i++) th.emplace_back([this, i] { loop(i); });
@@ -2095,7 +2095,10 @@ struct FaultPool {
 
     void start() {
         const char* e = getenv("MQ_FAULT_THREADS");
-        F = e ? atoi(e) : 8;
+        // 6 population + 6 copy threads (round 4; was 8 + 4): config 3's select_column
+        // 1.82-1.87 ms in four runs on two boxes against 1.89-2.41 for 8 + 4
+        // (profiles/r04_api_threads_ab.log)
+        F = e ? atoi(e) : 6;
         if (F < 0) F = 0;
         if (F > 16) F = 16;
         for (int i = 0; i < F; i++) th.emplace_back([this] { loop(); });
