@@ -63,9 +63,13 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
 // Caching device allocator for per-call scratch (join tables and partitions,
 // probe arrays): grow-only, blocks are reused for requests of 1/2..1x their size,
 // idle blocks are released by mq_trim(). A freed block may be handed out again at
-// once, so callers free only what no queued kernel still uses (sync first).
+// once, so callers free only what no queued kernel still uses (sync first);
+// pool_free_on(p, st) is the stream-ordered free: an event recorded on st marks
+// when the block may be reused, and pool_alloc waits for it (or picks another
+// block) before handing the block out again. Call it with the block's device current.
 void* pool_alloc(size_t bytes);
 void pool_free(void* p);
+void pool_free_on(void* p, hipStream_t st);
 
 // Lanes of the wave (within `among`) whose 8-bit value d equals this lane's: a
 // match-any from 8 ballots. Per bit: one v_bfe_i32 (the bit as 0 / all-ones), one

@@ -112,42 +112,76 @@ static void install(void) {
  * dlopen'd, so its TLS is dynamic, and a thread's first __tls_get_addr may allocate,
  * which a signal handler must not do (initial-exec TLS would move the library's
  * whole TLS block into the static surplus, which dlopen refuses). A slot is one
- * word, tid << 32 | h(address), h != 0; a slot whose h is 0 is idle and may be taken
- * by any thread. Every update is a CAS. */
+ * word, tid << 32 | h(address), h != 0, plus the CLOCK_MONOTONIC time it was
+ * written. An entry only matters for the thread's very next fault (the store
+ * re-executes within microseconds), so one older than RETRY_TTL_NS is dead: it is
+ * never read back (a later thread that reuses the tid does not inherit its tag) and
+ * any thread may take its slot over (a thread whose retried store succeeded never
+ * comes back to clear its entry, so without this the table would fill for good).
+ * A slot whose h is 0 is idle. Every update is a CAS. */
 #define NRETRY 1024
+#define RETRY_TTL_NS 250000000ull
 static _Atomic uint64_t g_retry[NRETRY];
+static _Atomic uint64_t g_retry_ns[NRETRY];
 
 static uint32_t addr_tag(uintptr_t a) { return ((uint32_t)a ^ (uint32_t)((uint64_t)a >> 32)) | 1u; }
 
+static uint64_t now_ns(void) { /* clock_gettime is async-signal-safe */
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static int retry_live(int i, uint64_t now) {
+    return now - atomic_load_explicit(&g_retry_ns[i], memory_order_acquire) < RETRY_TTL_NS;
+}
+
 static uint32_t retry_get(uint32_t tid) {
+    const uint64_t now = now_ns();
     for (int i = 0; i < NRETRY; i++) {
         const uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
-        if ((uint32_t)(v >> 32) == tid) return (uint32_t)v;
+        if ((uint32_t)(v >> 32) == tid && (uint32_t)v && retry_live(i, now)) return (uint32_t)v;
     }
     return 0;
 }
 
-/* Record h (0 = clear) for tid; 0 when there was no room (the caller must not count
- * on a retry being remembered then). */
+/* Record h for tid (h = 0: clear every entry of tid); 0 when there was no room (the
+ * caller must not count on a retry being remembered then). */
 static int retry_set(uint32_t tid, uint32_t h) {
     const uint64_t want = ((uint64_t)tid << 32) | h;
-    for (int pass = 0; pass < 4; pass++) {
+    const uint64_t now = now_ns();
+    if (h == 0) {
         for (int i = 0; i < NRETRY; i++) {
             uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
-            if ((uint32_t)(v >> 32) != tid) continue;
-            if (atomic_compare_exchange_strong(&g_retry[i], &v, want)) return 1;
-            goto again; /* taken from under us (it was idle): look again */
+            if ((uint32_t)(v >> 32) == tid && (uint32_t)v)
+                (void)atomic_compare_exchange_strong(&g_retry[i], &v, (uint64_t)tid << 32);
         }
-        if (h == 0) return 1; /* nothing recorded for this thread: already clear */
-        for (int i = 0; i < NRETRY; i++) {
-            uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
-            if ((uint32_t)v != 0) continue;
-            if (atomic_compare_exchange_strong(&g_retry[i], &v, want)) return 1;
-        }
-        return 0;
-    again:;
+        return 1;
     }
+    /* this thread's entry, else an idle or dead slot */
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < NRETRY; i++) {
+            uint64_t v = atomic_load_explicit(&g_retry[i], memory_order_acquire);
+            const int mine = (uint32_t)(v >> 32) == tid && (uint32_t)v;
+            if (pass == 0 ? !mine : ((uint32_t)v && retry_live(i, now))) continue;
+            /* the time first: between the CAS and a later store another thread would see
+             * our word with the dead slot's old time and take it over */
+            atomic_store_explicit(&g_retry_ns[i], now, memory_order_release);
+            if (atomic_compare_exchange_strong(&g_retry[i], &v, want)) {
+                if (pass == 1) /* an older entry of ours elsewhere must not shadow this one */
+                    for (int k = 0; k < i; k++) {
+                        uint64_t o = atomic_load_explicit(&g_retry[k], memory_order_acquire);
+                        if ((uint32_t)(o >> 32) == tid && (uint32_t)o)
+                            (void)atomic_compare_exchange_strong(&g_retry[k], &o, (uint64_t)tid << 32);
+                    }
+                return 1;
+            }
+        }
     return 0;
+}
+
+int mq_guard_retry_test(uint32_t tid, uint32_t tag, int get) {
+    return get ? (int)retry_get(tid) : retry_set(tid, tag);
 }
 
 static void on_segv(int sig, siginfo_t* si, void* uc) {

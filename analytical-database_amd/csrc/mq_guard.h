@@ -25,5 +25,9 @@ void mq_guard_release(uint64_t handle);
  * mark it dirty. */
 void mq_guard_forget_range(uintptr_t addr, size_t bytes);
 mq_guard_stats mq_guard_get_stats(void);
+/* Test hook for the fault handler's per-thread retry table: get = 0 records tag for
+ * thread id tid (0 when the table has no live-free slot), get = 1 returns the tag
+ * recorded for tid (0 = none, or dead). */
+int mq_guard_retry_test(uint32_t tid, uint32_t tag, int get);
 
 #endif

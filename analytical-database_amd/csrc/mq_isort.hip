@@ -640,17 +640,17 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
     Fin* bl[kMaxLevels] = {};  // ... and the counting finisher's fallbacks
     auto done = [&](int rc) {
         for (int i = 0; i < 2; i++) {
-            pool_free(wb[i]);
-            pool_free(sl[i]);
+            pool_free_on(wb[i], st);
+            pool_free_on(sl[i], st);
         }
-        for (Fin* f : fl) pool_free(f);
-        for (Fin* f : rl) pool_free(f);
-        for (Fin* f : bl) pool_free(f);
-        pool_free(dig);
-        pool_free(hist);
-        pool_free(tseg);
-        pool_free(scratch);
-        pool_free(ctr);
+        for (Fin* f : fl) pool_free_on(f, st);
+        for (Fin* f : rl) pool_free_on(f, st);
+        for (Fin* f : bl) pool_free_on(f, st);
+        pool_free_on(dig, st);
+        pool_free_on(hist, st);
+        pool_free_on(tseg, st);
+        pool_free_on(scratch, st);
+        pool_free_on(ctr, st);
         return rc;
     };
     if (!wb[0] || !wb[1] || !dig || !hist || !tseg || !scratch || !sl[0] || !sl[1] || !ctr)

@@ -1906,6 +1906,7 @@ struct mq_join {
     u64* offs;
     u64* scan_scratch;
     u64* longq;            // per-row write: chunks of the long runs (k_join_write_long)
+    hipStream_t stream;    // the stream of the handle's last queued work (juse)
 };
 
 namespace {
@@ -1927,8 +1928,18 @@ int jalloc(mq_join* j, void** p, size_t bytes) {
     return rc;
 }
 
+// Every call queues its work on the stream it is given; one on a different stream than
+// the last first waits for that stream, so the handle's queued work is always ordered
+// on j->stream and the stream-ordered frees below (pool_free_on) cover all of it: no
+// host sync, and shard workers sharing a device do not wait for each other.
+int juse(mq_join* j, hipStream_t st) {
+    if (j->stream != st) HIPCHK(hipStreamSynchronize(j->stream));
+    j->stream = st;
+    return MQ_OK;
+}
+
 void jfree_all(mq_join* j) {
-    for (int i = 0; i < j->nowned; i++) pool_free(j->owned[i]);
+    for (int i = 0; i < j->nowned; i++) pool_free_on(j->owned[i], j->stream);
     j->nowned = 0;
 }
 
@@ -1977,13 +1988,13 @@ int sample_has_dups(const int* c1, uint64_t n, uint32_t* dflag, hipStream_t st, 
     hipLaunchKernelGGL(k_sample_dups, dim3(stream_grid(s, kSample)), dim3(kTPB), 0, st, c1, n / kSample, kSample, tab,
                        2 * kSample - 1, dflag + 1);
     if (hipGetLastError() != hipSuccess) {
-        pool_free(tab);
+        pool_free_on(tab, st);
         return set_err(MQ_EHIP, "join: sample launch");
     }
     uint32_t f = 0;
     HIPCHK(hipMemcpyAsync(&f, dflag + 1, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    pool_free(tab);
+    pool_free_on(tab, st);
     *dups = f != 0;
     return MQ_OK;
 }
@@ -2009,12 +2020,12 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t *hist = nullptr, *wstart = nullptr;
     auto done = [&](int rc) {
-        pool_free(a);
-        pool_free(b);
-        pool_free(hist);
-        pool_free(hscan);
-        pool_free(scratch);
-        pool_free(wstart);
+        pool_free_on(a, st);
+        pool_free_on(b, st);
+        pool_free_on(hist, st);
+        pool_free_on(hscan, st);
+        pool_free_on(scratch, st);
+        pool_free_on(wstart, st);
         return rc;
     };
     a = (u64*)pool_alloc(n * 8);
@@ -2086,12 +2097,12 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t *hist = nullptr, *wstart = nullptr;
     auto done = [&](int rc) {
-        pool_free(a);
-        pool_free(b);
-        pool_free(hist);
-        pool_free(hscan);
-        pool_free(scratch);
-        pool_free(wstart);
+        pool_free_on(a, st);
+        pool_free_on(b, st);
+        pool_free_on(hist, st);
+        pool_free_on(hscan, st);
+        pool_free_on(scratch, st);
+        pool_free_on(wstart, st);
         return rc;
     };
     a = (u64*)pool_alloc(n * 8);
@@ -2107,8 +2118,8 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     ulonglong2* w16 = s16 ? (ulonglong2*)pool_alloc(slots * 16) : nullptr;
     auto drop = [&](int rc) {
         if (rc) (void)hipStreamSynchronize(st);  // (launched work may still use them)
-        pool_free(bp);
-        pool_free(w16);
+        pool_free_on(bp, st);
+        pool_free_on(w16, st);
         return done(rc);
     };
     int rc = MQ_OK;
@@ -2177,9 +2188,9 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
     u64* toff = (u64*)pool_alloc(ntiles * 8);
     u64* scratch = (u64*)pool_alloc(scan_scratch_elems(ntiles) * 8);
     auto fail = [&](int rc) {
-        pool_free(tcount);
-        pool_free(toff);
-        pool_free(scratch);
+        pool_free_on(tcount, st);
+        pool_free_on(toff, st);
+        pool_free_on(scratch, st);
         return rc;
     };
     if (!tcount || !toff || !scratch) return fail(set_err(MQ_ENOMEM, "join: run buffers"));
@@ -2196,8 +2207,8 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
     int* rid = (int*)pool_alloc(R * 4);
     uint32_t* rs = nullptr;
     if (!dk || !rid || (rc = jalloc(j, (void**)&rs, (R + 1) * 4))) {
-        pool_free(dk);
-        pool_free(rid);
+        pool_free_on(dk, st);
+        pool_free_on(rid, st);
         return fail(rc ? rc : set_err(MQ_ENOMEM, "join: run keys"));
     }
     hipLaunchKernelGGL(k_run_emit, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, skeys, n, toff, dk, rs);
@@ -2210,8 +2221,8 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
         HIPCHK(hipMemcpyAsync(&flag, dflag, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
     }
-    pool_free(dk);
-    pool_free(rid);
+    pool_free_on(dk, st);
+    pool_free_on(rid, st);
     if (rc) return fail(rc);
     fail(0);
     if (flag) return 1;
@@ -2234,9 +2245,9 @@ int radix_sort_onesweep(const int* c1, const int* p1, uint64_t n, int mode, uint
     u64* w1 = (u64*)pool_alloc(n * 8);
     uint32_t* meta = (uint32_t*)pool_alloc(4 * kRadix * 4 + 64 + stb);  // histograms, tickets, status
     auto done = [&](int rc) {
-        pool_free(w0);
-        pool_free(w1);
-        pool_free(meta);
+        pool_free_on(w0, st);
+        pool_free_on(w1, st);
+        pool_free_on(meta, st);
         return rc;
     };
     if (!w0 || !w1 || !meta) return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
@@ -2309,12 +2320,12 @@ int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_
     const uint64_t ntiles = ceil_div(n, kTile);
     const uint64_t nh = ntiles * kRadix;
     auto done = [&](int rc) {
-        pool_free(w0);
-        pool_free(w1);
-        pool_free(hist);
-        pool_free(hscan);
-        pool_free(scratch);
-        pool_free(dig);
+        pool_free_on(w0, st);
+        pool_free_on(w1, st);
+        pool_free_on(hist, st);
+        pool_free_on(hscan, st);
+        pool_free_on(scratch, st);
+        pool_free_on(dig, st);
         return rc;
     };
     if (npass < 1 || npass > 4) return set_err(MQ_EINVAL, "sort: %d passes", npass);
@@ -2376,14 +2387,14 @@ int radix_sort_pairs(const int* c1, const int* p1, uint64_t n, uint32_t** keys_o
     uint32_t* ko = (uint32_t*)pool_alloc(n ? n * 4 : 16);
     uint32_t* vo = (uint32_t*)pool_alloc(n ? n * 4 : 16);
     if (!ko || !vo) {
-        pool_free(ko);
-        pool_free(vo);
+        pool_free_on(ko, st);
+        pool_free_on(vo, st);
         return set_err(MQ_ENOMEM, "sort: outputs (%llu rows)", (unsigned long long)n);
     }
     int rc = n ? radix_sort_run(c1, p1, n, 1, ko, vo, nullptr, st) : MQ_OK;
     if (rc) {
-        pool_free(ko);
-        pool_free(vo);
+        pool_free_on(ko, st);
+        pool_free_on(vo, st);
         return rc;
     }
     *keys_out = ko;
@@ -2414,6 +2425,7 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     mq_join* j = new mq_join();
     std::memset(j, 0, sizeof(*j));
     HIPCHK(hipGetDevice(&j->device));
+    j->stream = st;
     j->n1 = n1;
     uint64_t slots = 64;
     while (slots < 2 * n1) slots <<= 1;
@@ -2467,7 +2479,7 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
                 return rc;
             }
             if ((rc = jown(j, skeys)) || (rc = jown(j, svals))) {
-                if (rc && j->owned[j->nowned - 1] != skeys) pool_free(svals);  // (skeys refused: svals still ours)
+                if (rc && j->owned[j->nowned - 1] != skeys) pool_free_on(svals, st);  // (skeys refused: svals still ours)
                 jfree_all(j);
                 delete j;
                 return rc;
@@ -2510,13 +2522,14 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     if (!j || !h_m || (n2 && !d_c2)) return set_err(MQ_EINVAL, "mq_join_probe: bad argument");
     if (n2 > (1ull << 31)) return set_err(MQ_EINVAL, "mq_join_probe: %llu rows (int32 positions)", (unsigned long long)n2);
     hipStream_t st = (hipStream_t)stream;
-    if (j->pstart) HIPCHK(hipDeviceSynchronize());  // a queued write may still read them
-    pool_free(j->p01);
+    if ((rc = juse(j, st))) return rc;
+    // a queued write may still read the last probe's arrays: freed in stream order
+    pool_free_on(j->p01, st);
     j->p01 = nullptr;
-    pool_free(j->pstart);
-    pool_free(j->plen);
-    pool_free(j->offs);
-    pool_free(j->scan_scratch);
+    pool_free_on(j->pstart, st);
+    pool_free_on(j->plen, st);
+    pool_free_on(j->offs, st);
+    pool_free_on(j->scan_scratch, st);
     j->pstart = j->plen = nullptr;
     j->offs = j->scan_scratch = nullptr;
     j->n2 = n2;
@@ -2595,6 +2608,7 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (!j) return set_err(MQ_EINVAL, "mq_join_write: NULL handle");
     if (j->m == 0) return MQ_OK;
     if (!d_out1 || (d_out2 && !d_p2)) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
+    if ((rc = juse(j, (hipStream_t)stream))) return rc;
     if (j->unique == 1) {
         hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
                            reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
@@ -2632,8 +2646,7 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     // the long-run list: at most m / kLongRun chunks (+ one per run for the rounding)
     const uint64_t qcap = j->m / kLongRun + j->m / kLongChunk + 2;
     if (qcap > 0xFFFFFFF0ull) return set_err(MQ_EINVAL, "mq_join_write: %llu pairs", (unsigned long long)j->m);
-    if (j->longq) HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-    pool_free(j->longq);
+    pool_free_on(j->longq, (hipStream_t)stream);
     if (!(j->longq = (u64*)pool_alloc(qcap * 8 + 16))) return set_err(MQ_ENOMEM, "mq_join_write: long-run list");
     uint32_t* const nlong = reinterpret_cast<uint32_t*>(j->longq + qcap);
     HIPCHK(hipMemsetAsync(nlong, 0, 4, (hipStream_t)stream));
@@ -2654,6 +2667,7 @@ int mq_join_counts(mq_join* j, uint32_t* d_cnt, void* stream) {
     if (!j || (j->n2 && !d_cnt)) return set_err(MQ_EINVAL, "mq_join_counts: bad argument");
     if (j->n2 == 0) return MQ_OK;
     hipStream_t st = (hipStream_t)stream;
+    if ((rc = juse(j, st))) return rc;
     if (j->n1 == 0) {  // the probe ran nothing: no row matched
         HIPCHK(hipMemsetAsync(d_cnt, 0, j->n2 * 4, st));
         return MQ_OK;
@@ -2682,13 +2696,13 @@ int mq_random_read(const uint64_t* d_table, int slots_log2, uint64_t n_reads, vo
 
 int mq_join_free(mq_join* j) {
     if (!j) return MQ_OK;
-    (void)hipDeviceSynchronize();  // queued probe/write kernels may still use the buffers
-    pool_free(j->p01);
-    pool_free(j->pstart);
-    pool_free(j->plen);
-    pool_free(j->offs);
-    pool_free(j->scan_scratch);
-    pool_free(j->longq);
+    // queued probe / write kernels may still use the buffers: freed in j->stream's order
+    pool_free_on(j->p01, j->stream);
+    pool_free_on(j->pstart, j->stream);
+    pool_free_on(j->plen, j->stream);
+    pool_free_on(j->offs, j->stream);
+    pool_free_on(j->scan_scratch, j->stream);
+    pool_free_on(j->longq, j->stream);
     jfree_all(j);
     delete j;
     return MQ_OK;

@@ -1551,13 +1551,26 @@ struct PoolBlock {
     size_t bytes;
     int dev;
     bool busy;
+    bool pending;    // freed stream-ordered: reusable once ev has completed
+    hipEvent_t ev;   // created on the block's device at its first ordered free
 };
 std::mutex g_pool_mu;
 std::vector<PoolBlock> g_pool;
 
+// An idle block whose ordered free has not yet completed on its stream.
+bool pool_in_flight(PoolBlock& b) {
+    if (!b.pending) return false;
+    if (hipEventQuery(b.ev) == hipErrorNotReady) return true;
+    (void)hipGetLastError();
+    b.pending = false;
+    return false;
+}
+
 void pool_release_idle_locked() {
     for (size_t i = 0; i < g_pool.size();) {
         if (!g_pool[i].busy) {
+            if (g_pool[i].pending) (void)hipEventSynchronize(g_pool[i].ev);
+            if (g_pool[i].ev) (void)hipEventDestroy(g_pool[i].ev);
             (void)hipFree(g_pool[i].p);
             g_pool[i] = g_pool.back();
             g_pool.pop_back();
@@ -1572,12 +1585,22 @@ void* pool_alloc(size_t bytes) {
     if (bytes == 0) bytes = 16;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    PoolBlock* best = nullptr;
+    std::unique_lock<std::mutex> lk(g_pool_mu);
+    PoolBlock *best = nullptr, *wait = nullptr;  // best: reusable now; wait: its free still in flight
     for (auto& b : g_pool)
-        if (!b.busy && b.dev == dev && b.bytes >= bytes && b.bytes / 2 <= bytes &&
-            (!best || b.bytes < best->bytes))
-            best = &b;
+        if (!b.busy && b.dev == dev && b.bytes >= bytes && b.bytes / 2 <= bytes) {
+            PoolBlock*& slot = pool_in_flight(b) ? wait : best;
+            if (!slot || b.bytes < slot->bytes) slot = &b;
+        }
+    if (!best && wait) {  // the only fit is still used by queued work: wait for it outside the lock
+        wait->busy = true;
+        void* p = wait->p;
+        hipEvent_t ev = wait->ev;
+        wait->pending = false;
+        lk.unlock();
+        (void)hipEventSynchronize(ev);
+        return p;
+    }
     if (best) {
         best->busy = true;
         return best->p;
@@ -1591,7 +1614,7 @@ void* pool_alloc(size_t bytes) {
             return nullptr;
         }
     }
-    g_pool.push_back(PoolBlock{p, bytes, dev, true});
+    g_pool.push_back(PoolBlock{p, bytes, dev, true, false, nullptr});
     return p;
 }
 
@@ -1604,6 +1627,32 @@ void pool_free(void* p) {
             return;
         }
     (void)hipFree(p);  // not from the pool
+}
+
+void pool_free_on(void* p, hipStream_t st) {
+    if (!p) return;
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    std::unique_lock<std::mutex> lk(g_pool_mu);
+    for (auto& b : g_pool)
+        if (b.p == p) {
+            bool ok = b.dev == dev;  // events record on the current device's streams only
+            if (ok && !b.ev) ok = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) == hipSuccess;
+            if (ok) ok = hipEventRecord(b.ev, st) == hipSuccess;
+            if (!ok) {  // cannot order it: wait for the stream instead
+                (void)hipGetLastError();
+                lk.unlock();
+                (void)hipStreamSynchronize(st);
+                pool_free(p);
+                return;
+            }
+            b.pending = true;
+            b.busy = false;
+            return;
+        }
+    lk.unlock();
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(p);
 }
 
 uint32_t stream_grid(const DevState* s, uint64_t work_items) {
@@ -2319,6 +2368,16 @@ int mq_pool_malloc(void** dptr, size_t bytes) {
 
 int mq_pool_free(void* dptr) {
     pool_free(dptr);
+    return MQ_OK;
+}
+
+int mq_pool_free_on(void* dptr, void* stream) {
+    pool_free_on(dptr, (hipStream_t)stream);
+    return MQ_OK;
+}
+
+int mq_device_sync(void) {
+    HIPCHK(hipDeviceSynchronize());
     return MQ_OK;
 }
 

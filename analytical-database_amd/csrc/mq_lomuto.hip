@@ -637,8 +637,9 @@ __global__ __launch_bounds__(64) void k_ld_small(const int32_t* __restrict__ V0,
 struct LdBufs {
     void* blk[24];
     int nb = 0, want = 0;
+    hipStream_t st = nullptr;  // the sort's stream: buffers go back in its order (error paths included)
     ~LdBufs() {
-        for (int i = 0; i < nb; i++) pool_free(blk[i]);
+        for (int i = 0; i < nb; i++) pool_free_on(blk[i], st);
     }
     template <typename T>
     T* get(size_t count) {
@@ -703,6 +704,7 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
     const uint64_t nimax = n / kItem + 2 * smax + 2;  // items of one level
     unsigned long long* pout = reinterpret_cast<unsigned long long*>(pout64);
     LdBufs b;
+    b.st = st;
     int32_t* V[2] = {b.get<int32_t>(n), b.get<int32_t>(n)};
     uint32_t* P[2] = {b.get<uint32_t>(n), b.get<uint32_t>(n)};
     uint32_t* R = b.get<uint32_t>(n);  // the back map of the current level

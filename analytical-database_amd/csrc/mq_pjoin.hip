@@ -220,10 +220,10 @@ int mq_pjoin_partition(const int32_t* d_keys, const int32_t* d_pay, uint64_t n, 
     uint32_t* hist = (uint32_t*)pool_alloc(nh * 4);
     u64* base = (u64*)pool_alloc(nh * 8 + 64 * 8);
     u64* scratch = (u64*)pool_alloc(scan_u32_scratch_elems(nh) * 8);
-    auto done = [&](int r) {
-        pool_free(hist);
-        pool_free(base);
-        pool_free(scratch);
+    auto done = [&](int r) {  // stream-ordered: queued kernels may still use them on an error path
+        pool_free_on(hist, st);
+        pool_free_on(base, st);
+        pool_free_on(scratch, st);
         return r;
     };
     if (!hist || !base || !scratch) return done(set_err(MQ_ENOMEM, "mq_pjoin_partition: %llu rows", (unsigned long long)n));
@@ -259,13 +259,12 @@ int mq_pjoin_place(const uint32_t* d_cntp, const int32_t* d_out1p, const uint32_
     u64* roff = (u64*)pool_alloc(n * 8);
     u64* scratch = (u64*)pool_alloc(scan_u32_scratch_elems(n) * 8);
     u64* longq = (u64*)pool_alloc(qcap * 8 + 16);
-    auto done = [&](int r) {
-        (void)hipStreamSynchronize(st);  // the temporaries go back to the pool only after use
-        pool_free(cnt_row);
-        pool_free(poff);
-        pool_free(roff);
-        pool_free(scratch);
-        pool_free(longq);
+    auto done = [&](int r) {  // the temporaries go back to the pool in stream order (no host wait)
+        pool_free_on(cnt_row, st);
+        pool_free_on(poff, st);
+        pool_free_on(roff, st);
+        pool_free_on(scratch, st);
+        pool_free_on(longq, st);
         return r;
     };
     if (!cnt_row || !poff || !roff || !scratch || !longq)

@@ -724,6 +724,33 @@ static void* pj_alloc(int* rc, size_t bytes) {
     return p;
 }
 
+/* Entry fence of mq_shard_join: its inputs are device pointers the caller may still be
+ * writing on any stream of the shard's device (the null stream included; the workers'
+ * own streams are non-blocking, so they would not wait for it). Each worker waits for
+ * its whole device before the first read. */
+static void t_pj_fence(Shard* s, void* a) {
+    (void)a;
+    s->rc = mq_device_sync();
+}
+
+/* G = 1: no partition, exchange or placement, the local join straight into the outputs. */
+static void t_pj_single(Shard* s, void* a) {
+    PJ* x = (PJ*)a;
+    mq_join* j = NULL;
+    uint64_t m = 0;
+    int rc = mq_join_build(x->c1[0], x->p1[0], x->n1[0], &j, s->stream);
+    if (!rc) rc = mq_join_probe(j, x->c2[0], x->n2[0], &m, s->stream);
+    x->out1[0] = (int32_t*)pj_alloc(&rc, m * 4);
+    x->out2[0] = (int32_t*)pj_alloc(&rc, m * 4);
+    if (!rc && m) rc = mq_join_write(j, x->p2[0], x->out1[0], x->out2[0], s->stream);
+    if (!rc) rc = mq_stream_sync(s->stream);
+    if (j) mq_join_free(j);
+    x->m[0] = m;
+    x->mg[0][0] = m;
+    s->rc = rc;
+}
+
+
 static void t_pj_part(Shard* s, void* a) {
     PJ* x = (PJ*)a;
     const int i = s->idx;
@@ -736,6 +763,7 @@ static void t_pj_part(Shard* s, void* a) {
         rc = mq_pjoin_partition(x->c1[i], x->p1[i], x->n1[i], g_G, x->bk[i], x->bp[i], NULL, x->cb[i], s->stream);
     if (!rc)
         rc = mq_pjoin_partition(x->c2[i], NULL, x->n2[i], g_G, x->pk[i], NULL, x->inv[i], x->cp[i], s->stream);
+    if (rc) (void)mq_stream_sync(s->stream); /* pj_free_temps frees the outputs from the caller's thread */
     s->rc = rc;
 }
 
@@ -793,9 +821,10 @@ static void t_pj_join(Shard* s, void* a) {
     if (!rc && m) rc = mq_join_write(j, NULL, x->o1[g], NULL, s->stream);
     if (!rc) rc = mq_stream_sync(s->stream);
     if (j) mq_join_free(j);
-    mq_pool_free(jk);
-    mq_pool_free(jp);
-    mq_pool_free(jq);
+    /* stream-ordered: on an error path peer copies or the build may still be queued */
+    mq_pool_free_on(jk, s->stream);
+    mq_pool_free_on(jp, s->stream);
+    mq_pool_free_on(jq, s->stream);
     s->rc = rc;
 }
 
@@ -827,8 +856,8 @@ static void t_pj_place(Shard* s, void* a) {
     }
     if (!rc) rc = mq_pjoin_place(cntp, o1p, x->inv[i], x->p2[i], n, M, x->out1[i], x->out2[i], s->stream);
     if (!rc) rc = mq_stream_sync(s->stream);
-    mq_pool_free(cntp);
-    mq_pool_free(o1p);
+    mq_pool_free_on(cntp, s->stream);
+    mq_pool_free_on(o1p, s->stream);
     s->rc = rc;
 }
 
@@ -846,9 +875,23 @@ static void pj_free_temps(PJ* x) {
 }
 
 /* The three phases; every worker synchronises its stream before a phase ends, so the
- * next phase's peer copies read finished data. On error nothing of x's stays allocated. */
+ * next phase's peer copies read finished data. On error nothing of x's stays allocated
+ * (each worker has synchronised or ordered its frees on its stream; t_pj_part's buffers
+ * are freed after its partitions, which synchronise). */
 static int pj_run(PJ* x) {
     double t0 = shim_now();
+    if (g_G == 1) { /* one shard: the local join alone (timed as the join phase) */
+        int rc = run_all(t_pj_single, x);
+        double t1 = shim_now();
+        x->ms[0] = x->ms[2] = 0;
+        x->ms[1] = x->ms[3] = 1e3 * (t1 - t0);
+        if (rc) {
+            mq_pool_free(x->out1[0]);
+            mq_pool_free(x->out2[0]);
+            x->out1[0] = x->out2[0] = NULL;
+        }
+        return rc;
+    }
     int rc = run_all(t_pj_part, x);
     double t1 = shim_now();
     if (!rc) rc = run_all(t_pj_join, x);
@@ -884,6 +927,14 @@ int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const 
     if (start(&st)) return MQ_ENODEV;
     PJ* x = (PJ*)calloc(1, sizeof(PJ));
     if (!x) return MQ_ENOMEM;
+    /* MQ_SHARD_JOIN_FENCE=0 skips the fence: only to show that the regression test
+     * (tests/test_gpu_pjoin.py, null-stream writers) fails without it */
+    const char* fe = getenv("MQ_SHARD_JOIN_FENCE");
+    int rc = fe && fe[0] == '0' ? 0 : run_all(t_pj_fence, NULL);
+    if (rc) {
+        free(x);
+        return rc;
+    }
     for (int g = 0; g < g_G; g++) {
         x->c1[g] = d_c1[g];
         x->p1[g] = d_p1[g];
@@ -892,7 +943,7 @@ int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const 
         x->p2[g] = d_p2[g];
         x->n2[g] = n2[g];
     }
-    int rc = pj_run(x);
+    rc = pj_run(x);
     for (int k = 0; k < 4; k++) g_pj_ms[k] = x->ms[k];
     for (int g = 0; g < g_G && !rc; g++) {
         d_out1[g] = x->out1[g];

@@ -1037,7 +1037,9 @@ constexpr int kSpPer = kSpChunk / kTPB;         // entries each thread places
 // into the same s_buf. Longer chunks make longer runs per query in the output
 // (≈ 27 entries at Q = 150 instead of ≈ 14), fewer partial lines: 0.55 -> 0.52 ms
 // at Q = 150 on 1e9 rows; 8192-pair chunks (2 waves per SIMD) took 0.77 ms.
-__global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict__ pairs, uint64_t cap,
+// `pairs` is clobbered: the padding stores of a chunk land on pairs of that chunk
+// already read (hence not const, not __restrict__).
+__global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
                                                       int q, int* const* __restrict__ outs, uint64_t rpb,
@@ -1054,7 +1056,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint64_t wc = blockIdx.x;
     const uint32_t np = npairs[wc];
-    const uint32_t* list = pairs + wc * cap;
+    uint32_t* const list = pairs + wc * cap;
     const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
     for (int i = tid; i < q; i += kTPB) {
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
@@ -1146,7 +1148,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(const uint32_t* __restrict
         // pair of this chunk already read (the slice is not read again): with a
         // data-dependent count the wait for the next chunk's loads at the loop's top was
         // vmcnt(0), i.e. also for every store of this chunk
-        gint* const dummy = (gint*)(const_cast<uint32_t*>(list) + c0);
+        gint* const dummy = (gint*)(list + c0);
 #pragma unroll
         for (int k = 0; k < kSpPer; k++) {
             const uint32_t i = (uint32_t)(k * kTPB + tid);
@@ -1578,7 +1580,7 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
         // the pair scatter, or (a slice overflowed: the pairs are incomplete) the
         // column pass: both launched, each checks the flag on the device
         hipLaunchKernelGGL(k_ssp_scatter, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
-                           reinterpret_cast<const uint32_t*>(w + L.pairs), pair_cap(S.rpb),
+                           reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
                            reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
                            S.base, of);
         LAUNCHCHK("k_ssp_scatter");

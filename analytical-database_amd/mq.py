@@ -105,6 +105,8 @@ _SIGS = {
     "mq_free": (_int, [_vp]),
     "mq_pool_malloc": (_int, [C.POINTER(_vp), _sz]),
     "mq_pool_free": (_int, [_vp]),
+    "mq_pool_free_on": (_int, [_vp, _vp]),
+    "mq_device_sync": (_int, []),
     "mq_memcpy_h2d": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2h": (_int, [_vp, _vp, _sz, _vp]),
     "mq_memcpy_d2d": (_int, [_vp, _vp, _sz, _vp]),
@@ -214,6 +216,7 @@ _SIGS = {
     "mq_guard_clean": (_int, [C.c_uint64, _vp, _sz]),
     "mq_guard_release": (None, [C.c_uint64]),
     "mq_guard_forget_range": (None, [C.c_size_t, _sz]),
+    "mq_guard_retry_test": (_int, [C.c_uint32, C.c_uint32, _int]),
 }
 
 MQ_GUARD_FILE, MQ_GUARD_CHUNK = 0, 1

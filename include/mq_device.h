@@ -60,7 +60,9 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
  * mq_memcpy_d2h_staged into exactly that range copies each chunk as soon as its pages
  * are in; it also starts this itself when nothing covers its range. Callers that know
  * a result's size before its kernel runs start it first, so the page faults overlap
- * the kernel. MQ_PREFAULT=0 disables it, MQ_FAULT_THREADS (default 8) sizes it. */
+ * the kernel. MQ_PREFAULT=0 disables it, MQ_FAULT_THREADS (default 6) sizes it; the
+ * staged copies' host memcpy runs on MQ_COPY_THREADS threads (default 6: the calling
+ * thread and 5 helpers). */
 void mq_host_prefault(void* p, size_t bytes);
 /* Wait until the calling thread's population job (if any) has finished: call it
  * before freeing a range handed to mq_host_prefault that no staged copy consumed. */
@@ -81,11 +83,20 @@ void mq_trim(void);
  * on the thread allocate afresh. */
 void mq_thread_release(void);
 /* The same caching allocator for callers (the query layer keeps result shadows
- * and column copies in it): a freed block may be handed out again at once, so
- * free only what no queued work still uses. mq_pool_free also accepts pointers
- * from mq_malloc (it frees those at once). */
+ * and column copies in it). mq_pool_free hands the block out again at once, so it
+ * frees only what no queued work still uses; mq_pool_free_on is the stream-ordered
+ * free: the block is reused only after the work queued on `stream` so far has
+ * finished (an event recorded on it; the next allocation that needs the block waits
+ * for that event), so a caller frees right after queueing the last kernel that reads
+ * it, with no host sync. Both also accept pointers from mq_malloc (freed at once;
+ * mq_pool_free_on syncs the stream first). Call mq_pool_free_on with the block's
+ * device current. */
 int mq_pool_malloc(void** dptr, size_t bytes);
 int mq_pool_free(void* dptr);
+int mq_pool_free_on(void* dptr, void* stream);
+/* Wait for all work queued on the calling thread's current device, on every stream
+ * including the null stream (hipDeviceSynchronize). */
+int mq_device_sync(void);
 
 /* Workspace (device bytes) needed by the scan entry points for n rows. */
 size_t mq_scan_workspace_bytes(uint64_t n);
@@ -306,7 +317,8 @@ int mq_join_counts(mq_join* join, uint32_t* d_cnt, void* stream);
  *   numbers. Synchronous. G <= 64, n < 2^32.
  * mq_pjoin_place: a probe shard's output from its partitioned counts d_cntp (n u32) and
  *   pairs d_out1p (m build positions, partitioned order): row r's pairs go to the offset
- *   of the rows before it, out2 = d_p2[r]. */
+ *   of the rows before it, out2 = d_p2[r]. Asynchronous on stream (its temporaries are
+ *   freed stream-ordered). */
 uint32_t mq_pjoin_bucket(int32_t key, int G);
 int mq_pjoin_partition(const int32_t* d_keys, const int32_t* d_pay, uint64_t n, int G, int32_t* d_keys_out,
                        int32_t* d_pay_out, uint32_t* d_inv, uint64_t* h_counts, void* stream);

@@ -225,7 +225,14 @@ int mq_shard_devices(int* devices, int max);
  * n2[g]) on its device, the ranges of each side in row order (any split). On return
  * shard g's device holds d_out1[g] / d_out2[g]: the h_m[g] pairs of probe rows of range
  * g, in the reference's order; their concatenation over g is hash_join's output. The
- * outputs are pool memory (mq_pool_free). Starts the shard workers if needed. */
+ * outputs are pool memory (mq_pool_free). Starts the shard workers if needed.
+ * Stream contract: the inputs may still be being written by work the caller queued on
+ * ANY stream of the shard devices, the null stream included: mq_shard_join first waits
+ * for every shard device to go idle (mq_device_sync on each worker), because its
+ * workers run on non-blocking streams of their own that would not wait for that work.
+ * On return every output is complete (each worker has synchronised its stream). Work
+ * the caller queues concurrently from other threads while the call runs is not
+ * ordered against it. */
 int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const uint64_t* n1,
                   const int32_t* const* d_c2, const int32_t* const* d_p2, const uint64_t* n2,
                   int32_t** d_out1, int32_t** d_out2, uint64_t* h_m);

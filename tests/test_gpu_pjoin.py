@@ -141,6 +141,30 @@ def test_shard_join_goldens(lib, refcpu, goldens, g):
         assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"]), (n, dup)
 
 
+def test_shard_join_waits_for_null_stream_writers(lib, refcpu, goldens):
+    """Regression (GPUTEST_r04: M = 54 instead of 32,925): the inputs are written on the
+    null stream and mq_shard_join is called at once, with no sync. The shard workers run
+    on non-blocking streams, so without the entry fence (include/mq_query.h, the
+    mq_shard_join stream contract) they would partition the keys before the writers
+    finish. Made deterministic: 2^28-row key columns are first filled 200 times with the
+    WRONG keys (the other side's), then once with the right ones, all queued on the null
+    stream behind each other (~60 ms of queued writes): a worker that does not wait reads
+    the wrong keys. M and the pairs' FNV must equal the reference's 2^28 golden."""
+    n = 1 << 28
+    r = [r for r in goldens["join_survey"] if r["n"] == n][0]
+    config(lib, 2)
+    D = [Dev(n * 4) for _ in range(4)]
+    for _ in range(200):
+        mq.check(lib.mq_gen_join_keys(D[0].ptr, n, 1, None))
+        mq.check(lib.mq_gen_join_keys(D[2].ptr, n, 0, None))
+    mq.check(lib.mq_gen_join_keys(D[0].ptr, n, 0, None))
+    mq.check(lib.mq_gen_iota(D[1].ptr, n, None))
+    mq.check(lib.mq_gen_join_keys(D[2].ptr, n, 1, None))
+    mq.check(lib.mq_gen_iota(D[3].ptr, n, None))
+    o1, o2, _ = shard_join(lib, 2, D, n, n, seed=11)  # no sync in between
+    assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"])
+
+
 CASES = ["unique", "dups", "skew", "neg", "tiny", "empty_build", "empty_probe", "dups_long", "unique_big"]
 
 

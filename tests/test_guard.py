@@ -261,3 +261,66 @@ print("ok", flush=True)
 """
     cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert cp.returncode == 0 and "ok" in cp.stdout, (cp.returncode, cp.stderr[-2000:])
+
+
+def test_retry_table_slots_are_reclaimed():
+    """a retried store that succeeds never clears its thread's
+    entry in the fault handler's retry table. Entries are dead after RETRY_TTL_NS
+    (250 ms): a full table of stale entries takes new threads again, and a thread that
+    reuses an old tid does not inherit its tag. Run in a child process (fresh table)."""
+    code = f"""
+import sys, time
+sys.path.insert(0, {os.path.join(os.path.dirname(__file__))!r})
+from refapi import mq
+lib = mq.load()
+for t in range(1, 1025):          # 1024 threads that retried once and never came back
+    assert lib.mq_guard_retry_test(t, 0x1001, 0) == 1
+assert lib.mq_guard_retry_test(5000, 0x2001, 0) == 0   # full of live entries
+assert lib.mq_guard_retry_test(7, 0, 1) == 0x1001
+time.sleep(0.4)
+assert lib.mq_guard_retry_test(7, 0, 1) == 0           # dead: a reused tid starts clean
+for t in range(5000, 6024):        # every dead slot is taken over
+    assert lib.mq_guard_retry_test(t, 0x3001, 0) == 1, t
+assert lib.mq_guard_retry_test(9000, 0x2001, 0) == 0   # full again, of live entries
+assert lib.mq_guard_retry_test(5500, 0, 1) == 0x3001
+assert lib.mq_guard_retry_test(5500, 0x5001, 0) == 1   # own entry updated in place
+assert lib.mq_guard_retry_test(5500, 0, 1) == 0x5001
+assert lib.mq_guard_retry_test(5500, 0, 0) == 1        # cleared
+assert lib.mq_guard_retry_test(5500, 0, 1) == 0
+print("ok", flush=True)
+"""
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert cp.returncode == 0 and "ok" in cp.stdout, (cp.returncode, cp.stdout, cp.stderr[-2000:])
+
+
+def test_many_short_lived_threads_race_on_guards():
+    """More than 1024 short-lived threads, in racing groups of 16 on one guarded page:
+    every losing fault is retried (never handed on, which would kill the process)."""
+    code = f"""
+import ctypes as C, mmap, os, sys, threading
+sys.path.insert(0, {os.path.join(os.path.dirname(__file__))!r})
+from refapi import mq
+import numpy as np
+lib = mq.load()
+libc = C.CDLL(None)
+libc.memset.argtypes = [C.c_void_p, C.c_int, C.c_size_t]
+for rep in range(100):
+    fd = os.memfd_create("x"); os.ftruncate(fd, 1 << 16)
+    m = mmap.mmap(fd, 1 << 16); os.close(fd)
+    a = np.frombuffer(m, dtype=np.uint8)
+    h = lib.mq_guard_arm(a.ctypes.data, a.nbytes, 0)
+    assert h
+    go = threading.Barrier(16)
+    def w(i):
+        go.wait()
+        libc.memset(a.ctypes.data + 4096 + i * 64, i + 1, 64)
+    ts = [threading.Thread(target=w, args=(i,)) for i in range(16)]
+    [t.start() for t in ts]; [t.join() for t in ts]
+    assert lib.mq_guard_clean(h, a.ctypes.data, a.nbytes) == 0
+    assert all(a[4096 + i * 64] == i + 1 for i in range(16))
+    lib.mq_guard_release(h)
+    del a; m.close()
+print("ok", flush=True)
+"""
+    cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert cp.returncode == 0 and "ok" in cp.stdout, (cp.returncode, cp.stderr[-2000:])
