@@ -39,6 +39,8 @@
 #include <cstring>
 
 #include <cerrno>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 
 #ifndef MADV_POPULATE_WRITE
@@ -897,6 +899,25 @@ __device__ __forceinline__ void stage_tile(StageState& st, int4 v, uint32_t t0, 
     st.nbm = __builtin_amdgcn_readfirstlane(st.nbm + c);
 }
 
+// select_result's payload rows r .. r+3 of a 256-row tile (r = tile * 256 + 4 lane):
+// one nontemporal dwordx4 where the payload is 16-byte aligned and the rows exist (every
+// tile but the column's last), else four dword loads with the indices clamped. Four
+// dword loads per lane issued the same lines as 4 instructions; one dwordx4 moves the
+// wave's 1 KiB in one.
+__device__ __forceinline__ void load_pay4(int (&pv)[4], const int* __restrict__ payload, uint64_t r, uint64_t n,
+                                          bool pal) {
+    if (pal && r + 3 < n) {
+        const int4 x = load4_nt<true>(payload + r);
+        pv[0] = x.x;
+        pv[1] = x.y;
+        pv[2] = x.z;
+        pv[3] = x.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) pv[e] = payload[r + e < n ? r + e : n - 1];
+    }
+}
+
 template <bool PAYLOAD, bool VEC, int BUF = kStBuf>
 __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, uint64_t rw, Pred pred,
@@ -1014,6 +1035,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
     unsigned long long o = D + fill;
     const uint64_t T1 = (E + 255) >> 8;
+    const bool pal = PAYLOAD && ((reinterpret_cast<uintptr_t>(payload) & 15u) == 0);
     // xmode 1: ring entries [bst, bst + bfill) go to out[ob ...]; bst = out + ob's
     // dword offset within its 16 bytes
     unsigned long long ob = o;
@@ -1074,8 +1096,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
                     for (int jj = 0; jj < kPf; jj++) {
                         const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
                         const bool any = __builtin_amdgcn_readlane((int)c, j0 + jj) != 0;
-#pragma unroll
-                        for (int e = 0; e < 4; e++) pv[jj][e] = any ? payload[r + e < n ? r + e : n - 1] : 0;
+                        if (any) load_pay4(pv[jj], payload, r, n, pal);
                     }
                 }
 #pragma unroll
@@ -1119,8 +1140,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
 #pragma unroll
                     for (int jj = 0; jj < kPf; jj++) {
                         const uint64_t rj = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
-#pragma unroll
-                        for (int e = 0; e < 4; e++) pv[jj][e] = payload[rj + e < n ? rj + e : n - 1];
+                        load_pay4(pv[jj], payload, rj, n, pal);
                     }
                 }
 #pragma unroll
@@ -2052,6 +2072,50 @@ struct Staging {
 };
 thread_local Staging g_staging[kMaxDev];
 
+// The CPUs next to the current device (its PCIe root's NUMA node, from sysfs): the staged
+// copies' helper threads run there, so their memcpy out of the pinned buffers and their
+// first touch of a fresh payload (which places its pages) stay on the GPU's socket. On a
+// two-socket host a helper the scheduler put on the far socket copied across the
+// interconnect: select_column's 40 MB D2H took 1.15-1.50 ms from one process to the next.
+// Measured (round 5, 15 reps over 3 processes each, one box, profiles/r05_api_numa_segs.log):
+// bound helpers were slower, select_column 1.86 vs 1.71 ms (4 segments) and 2.03 vs
+// 1.89 ms (one kernel), so binding is opt-in: MQ_NUMA_BIND=1. Empty set: no binding.
+bool device_cpuset(cpu_set_t* set) {
+    static const bool on = getenv("MQ_NUMA_BIND") && getenv("MQ_NUMA_BIND")[0] == '1';
+    CPU_ZERO(set);
+    if (!on) return false;
+    int dev = 0;
+    char bus[64] = {0};
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int)sizeof bus, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    for (char* c = bus; *c; c++) *c = (char)((*c >= 'A' && *c <= 'F') ? *c - 'A' + 'a' : *c);
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/local_cpulist", bus);
+    FILE* f = fopen(path, "r");
+    if (!f) return false;
+    char list[1024] = {0};
+    const bool got = fgets(list, sizeof list, f) != nullptr;
+    fclose(f);
+    if (!got) return false;
+    int n = 0;
+    for (char* q = list; *q && *q != '\n';) {
+        char* end;
+        long a = strtol(q, &end, 10);
+        if (end == q) break;
+        long b = a;
+        if (*end == '-') b = strtol(end + 1, &end, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++, n++) CPU_SET((int)c, set);
+        q = *end == ',' ? end + 1 : end;
+    }
+    return n > 0;
+}
+
+void bind_helper(const cpu_set_t& set, bool ok) {
+    if (ok) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+}
+
 // The host side of the staged D2H: each chunk copied out of the pinned buffer by
 // the calling thread and MQ_COPY_THREADS - 1 helpers (one memcpy thread moved ~10 GB/s,
 // a quarter of the DMA rate; 6 threads, round 4: see FaultPool). One pool per calling thread (row-shard workers copy
@@ -2072,7 +2136,12 @@ struct CopyPool {
         parts = e ? atoi(e) : 6;
         if (parts < 1) parts = 1;
         if (parts > 16) parts = 16;
-        for (int i = 1; i < parts; i++) th.emplace_back([this, i] { loop(i); });
+        cpu_set_t set;
+        const bool ok = device_cpuset(&set);
+        for (int i = 1; i < parts; i++) th.emplace_back([this, i, set, ok] {
+            bind_helper(set, ok);
+            loop(i);
+        });
     }
     void slice(int i) {
         const size_t a = len * (size_t)i / (size_t)parts, b = len * (size_t)(i + 1) / (size_t)parts;
@@ -2150,7 +2219,12 @@ struct FaultPool {
         F = e ? atoi(e) : 6;
         if (F < 0) F = 0;
         if (F > 16) F = 16;
-        for (int i = 0; i < F; i++) th.emplace_back([this] { loop(); });
+        cpu_set_t set;
+        const bool ok = device_cpuset(&set);
+        for (int i = 0; i < F; i++) th.emplace_back([this, set, ok] {
+            bind_helper(set, ok);
+            loop();
+        });
     }
     void work() {
         const size_t pg = 4096;
@@ -2271,6 +2345,76 @@ int mq_memcpy_d2h_staged(void* dst, const void* src, size_t bytes, void* stream)
     return MQ_OK;
 }
 
+// mq_select_positions_download (mq_device.h): segment s's kernel writes its count into
+// pinned, host-coherent memory (no D2H on the compute stream), an event marks its end;
+// the host waits for segment s alone and stages its positions down on the thread's copy
+// stream, overlapping the kernels of segments s+1.. (the SDMA engine reads HBM at the
+// link's 57 GB/s, far below the scan's own traffic). The payload pages of segment s are
+// populated by the staged copy's fault pool as it starts (mq_host_prefault).
+namespace {
+struct SegPipe {
+    hipStream_t copy = nullptr;
+    unsigned long long* cnt = nullptr;  // 64 pinned counts
+    hipEvent_t ev[64];
+    bool ready = false;
+};
+thread_local SegPipe g_segpipe[kMaxDev];
+}  // namespace
+
+int mq_select_positions_download(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                                 int32_t high, int segs, int32_t* d_pos, int32_t* h_dst, uint64_t* h_seg,
+                                 uint64_t* h_rows, void* d_ws, size_t ws_bytes, void* stream) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    if (segs < 1 || segs > 64 || !h_seg || !h_rows || (n && (!d_col || !d_pos || !h_dst)))
+        return set_err(MQ_EINVAL, "mq_select_positions_download: bad argument");
+    int d;
+    if ((rc = current_device(&d))) return rc;
+    SegPipe& P = g_segpipe[d];
+    if (!P.ready) {
+        HIPCHK(hipStreamCreateWithFlags(&P.copy, hipStreamNonBlocking));
+        HIPCHK(hipHostMalloc((void**)&P.cnt, 64 * sizeof(unsigned long long), hipHostMallocCoherent));
+        for (int i = 0; i < 64; i++) HIPCHK(hipEventCreateWithFlags(&P.ev[i], hipEventDisableTiming));
+        P.ready = true;
+    }
+    // segment bounds: whole 1024-row tiles (16-byte aligned slices, as the row shards)
+    h_rows[0] = 0;
+    for (int g = 1; g < segs; g++) {
+        uint64_t b = (uint64_t)(((unsigned __int128)n * (unsigned)g) / (unsigned)segs) & ~(uint64_t)1023;
+        h_rows[g] = b < h_rows[g - 1] ? h_rows[g - 1] : b;
+    }
+    h_rows[segs] = n;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long* dcnt = nullptr;
+    HIPCHK(hipHostGetDevicePointer((void**)&dcnt, P.cnt, 0));
+    for (int g = 0; g < segs; g++) {
+        const uint64_t r0 = h_rows[g], ng = h_rows[g + 1] - r0;
+        P.cnt[g] = 0;
+        if (ng && (rc = mq_select_positions_at(d_col + r0, nullptr, ng, (int32_t)r0, has_low, low, has_high, high,
+                                               d_pos + r0, reinterpret_cast<uint64_t*>(dcnt + g), d_ws, ws_bytes,
+                                               stream)))
+            return rc;
+        HIPCHK(hipEventRecord(P.ev[g], st));
+    }
+    uint64_t off = 0;
+    for (int g = 0; g < segs; g++) {
+        HIPCHK(hipEventSynchronize(P.ev[g]));
+        const uint64_t k = *reinterpret_cast<volatile unsigned long long*>(P.cnt + g);
+        if (k > h_rows[g + 1] - h_rows[g]) {  // the select's own error word (~0): its spin timed out
+            (void)hipStreamSynchronize(st);
+            return set_err(MQ_EHIP, "mq_select_positions_download: segment %d count %llu", g, (unsigned long long)k);
+        }
+        h_seg[g] = k;
+        if (k && (rc = mq_memcpy_d2h_staged(h_dst + off, d_pos + h_rows[g], k * sizeof(int32_t), P.copy))) {
+            (void)hipStreamSynchronize(st);
+            return rc;
+        }
+        off += k;
+    }
+    return MQ_OK;
+}
+
 // mq_thread_release (mq_device.h): the calling thread's pinned staging buffers and
 // their events, on every device it staged through. A thread that exits without it
 // leaks them (thread_local storage is not freed by the runtime).
@@ -2287,6 +2431,15 @@ void mq_thread_release(void) {
             (void)hipHostFree(S.buf[i]);
         }
         S = Staging{};
+    }
+    for (int d = 0; d < kMaxDev; d++) {
+        SegPipe& P = g_segpipe[d];
+        if (!P.ready || hipSetDevice(d) != hipSuccess) continue;
+        (void)hipStreamSynchronize(P.copy);
+        (void)hipStreamDestroy(P.copy);
+        for (int i = 0; i < 64; i++) (void)hipEventDestroy(P.ev[i]);
+        (void)hipHostFree(P.cnt);
+        P = SegPipe{};
     }
     if (have_cur) (void)hipSetDevice(cur);
     mqi::shared_staging_release();

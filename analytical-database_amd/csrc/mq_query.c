@@ -592,12 +592,90 @@ __attribute__((weak)) bool should_use_index(Column* column, int low, int high) {
     return true;
 }
 
+/* Segments of the pipelined select (0 = off): MQ_SELECT_SEGS, default 2, for columns of
+ * at least MQ_SELECT_PIPE_MIN rows (default 2^26). Read per call (tests change them).
+ * Config 3's select_column (1e9 rows, 1 %), 15 reps over 3 processes each, one box
+ * (profiles/r05_api_segs_sweep.log): medians 2 segments 1.54 ms, 4 1.71, 6 2.10; one
+ * kernel then the D2H 1.89 ms (profiles/r05_api_numa_segs.log). Past the first segment
+ * the host side of the staged copy (first touch of the payload, memcpy out of the pinned
+ * buffers, ~35 GB/s) is the bound, so more segments only add launches and copy calls. */
+static int pipe_segments(size_t n) {
+    const char* e = getenv("MQ_SELECT_SEGS");
+    int segs = e ? atoi(e) : 2;
+    if (segs < 0 || segs > 64) segs = 0;
+    const char* m = getenv("MQ_SELECT_PIPE_MIN");
+    const size_t min_rows = m ? (size_t)strtoull(m, NULL, 10) : ((size_t)1 << 26);
+    return segs >= 2 && n >= min_rows && mq_guard_enabled() ? segs : 0;
+}
+
+/* select_column_scan for long columns (round 5): the payload's size is unknown until the
+ * select ends, so the one-kernel path pays select, then the whole D2H. Here the select
+ * runs in `segs` row segments and segment s's positions go down while segments s+1..
+ * scan (mq_select_positions_download). Their host destination must exist before K is
+ * known: the payload is malloc'd for all n rows (an mmap'd chunk: address space, no
+ * pages until written; advised onto huge pages), filled at the running offset, and
+ * shrunk to K rows by realloc afterwards (glibc remaps an mmapped chunk in place, so it
+ * stays guardable). The HBM shadow is the segments' pieces copied together on the device. */
+static Result* scan_positions_piped(const int32_t* dcol, size_t n, int segs, int* low_pointer, int* high_pointer,
+                                    Status* st) {
+    double t0 = now_s();
+    int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
+    if (!host) {
+        fail(st, "payload allocation", MQ_ENOMEM);
+        return NULL;
+    }
+    uint64_t seg[65], rows[65];
+    int rc = mq_stream_sync(g_stream);
+    const double tx = now_s();
+    if (!rc)
+        rc = mq_select_positions_download(dcol, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
+                                          high_pointer != NULL, high_pointer ? *high_pointer : 0, segs,
+                                          (int32_t*)g_scratch, host, seg, rows, g_ws, g_ws_bytes, g_stream);
+    g_xfer_s += now_s() - tx; /* (the kernels overlap the copies: counted as transfer) */
+    if (rc) {
+        free(host);
+        fail(st, "select_column_scan", rc);
+        return NULL;
+    }
+    TRACE("select segments + d2h", t0);
+    size_t k = 0;
+    for (int g = 0; g < segs; g++) k += (size_t)seg[g];
+    const size_t bytes = k * sizeof(int32_t);
+    int32_t* h2 = (int32_t*)realloc(host, bytes ? bytes : 1);
+    if (h2) host = h2;
+    const int keep = bytes >= SHADOW_MIN_BYTES && mq_guard_chunk_ok(host);
+    const uint64_t guard = keep ? mq_guard_arm(host, bytes, MQ_GUARD_CHUNK) : 0;
+    if (guard) {
+        void* dev = NULL;
+        rc = dev_alloc(&dev, bytes);
+        size_t off = 0;
+        for (int g = 0; g < segs && !rc; g++) {
+            rc = mq_memcpy_d2d((int32_t*)dev + off, (const int32_t*)g_scratch + rows[g], seg[g] * sizeof(int32_t),
+                               g_stream);
+            off += seg[g];
+        }
+        if (rc) {
+            mq_guard_release(guard);
+            mq_pool_free(dev);
+            free(host);
+            fail(st, "shadow copy", rc);
+            return NULL;
+        }
+        shadow_put(host, k, dev, guard);
+    }
+    TRACE("shrink + guard + shadow", t0);
+    st->code = OK;
+    return new_result(INT, k, host);
+}
+
 /* query.c:92-137 (the body; shared_select calls it inside its own operator) */
 static Result* scan_positions(Column* column, int* low_pointer, int* high_pointer, Status* ret_status) {
     if (shard_wants(column)) return shard_select(column, low_pointer, high_pointer, ret_status);
     size_t n = column->row_count;
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
+    const int segs = pipe_segments(n);
+    if (segs) return scan_positions_piped(dcol, n, segs, low_pointer, high_pointer, ret_status);
     const double t0 = now_s();
     int rc = mq_select_positions(dcol, NULL, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
                                  high_pointer != NULL, high_pointer ? *high_pointer : 0,
@@ -866,11 +944,14 @@ Result* max(Result* column, Status* ret_status) {
 Result** shared_select(SelectOperator* operators, int query_count, Column* column, Status* ret_status) {
     if (op_begin(ret_status)) return NULL;
     size_t n = column->row_count;
-    if (query_count > 3 && shard_wants(column)) return shard_shared_select(operators, query_count, column, ret_status);
+    if (query_count > 1 && shard_wants(column)) return shard_shared_select(operators, query_count, column, ret_status);
     const int32_t* dcol = NULL;
-    if (query_count > 3 && column_device(column, &dcol, ret_status)) return NULL;
+    if (query_count > 1 && column_device(column, &dcol, ret_status)) return NULL;
     Result** out = (Result**)calloc((size_t)(query_count > 0 ? query_count : 1), sizeof(Result*));
-    if (query_count <= 3) {  /* a few queries: one ordered-compaction pass each is cheaper */
+    /* one query: the ordered-compaction pass. From two the shared pass is cheaper (round
+     * 5: Q = 2 of 0.1 % 0.79 ms on the device against 2 x 0.68 ms; until round 4 the
+     * ballot kernels below Q = 12 made it 0.96 and the split was at Q = 3) */
+    if (query_count <= 1) {
         for (int j = 0; j < query_count; j++) {
             int lo = operators[j].low, hi = operators[j].high;
             if (!(out[j] = scan_positions(column, &lo, &hi, ret_status))) {

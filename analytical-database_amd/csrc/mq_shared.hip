@@ -247,7 +247,14 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
 //          the tile) gives its slot after the query's running offset. Tiles with
 //          many pairs (dense queries) take the per-query ballot loop instead.
 // ---------------------------------------------------------------------------
-constexpr int kEiMinQ = 12;  // measured crossover (count + write, 1e9 rows): Q=8 ballots 2.65 vs 3.25 ms, Q=12 3.63 vs 3.48, Q=16 4.64 vs 3.62
+// Round 2's crossover was Q = 12 (two-pass kernels: Q=8 ballots 2.65 vs 3.25 ms). Against
+// the single-pass k-major count (round 5, 1e9 rows, count + write, one box,
+// profiles/r05_ss_small_q.log) the ballots lose from Q = 2: 0.1 % ranges Q = 2 / 4 / 8
+// 0.96 / 1.38 / 2.38 vs 0.79 / 0.83 / 0.89 ms, 10 % ranges 1.90 / 3.17 / 6.0 vs
+// 1.72 / 2.52 / 4.22 ms; only very dense sets (50 % ranges, a pair per row, the pair
+// slices overflow) keep the ballots ahead (Q = 2 4.77 vs 5.17 ms). The ballot kernels
+// stay as MQ_SS_EI_MIN=N (N > Q) / MQ_SS_IMPL=ballot.
+constexpr int kEiMinQ = 1;
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;

@@ -149,6 +149,8 @@ _SIGS = {
                                       _vp]),
     "mq_select_positions": (_int, [_vp, _vp, _u64, _int, _i32, _int, _i32, _vp, _vp, _vp, _sz,
                                    _vp]),
+    "mq_select_positions_download": (_int, [_vp, _u64, _int, _i32, _int, _i32, _int, _vp, _vp,
+                                            C.POINTER(_u64), C.POINTER(_u64), _vp, _sz, _vp]),
     "mq_index_select": (_int, [_vp, _vp, _u64, _i32, _i32, _vp, _vp, _vp]),
     "mq_fetch": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "mq_index_build": (_int, [_vp, _u64, _vp, _vp, _vp]),
@@ -246,9 +248,11 @@ class MqError(RuntimeError):
     pass
 
 
-def bind(lib: C.CDLL, names=None) -> C.CDLL:
+def bind(lib: C.CDLL, names=None, strict: bool = True) -> C.CDLL:
     for name, (res, args) in _SIGS.items():
         if names is not None and name not in names:
+            continue
+        if not strict and not hasattr(lib, name):  # an older build loaded for an A/B
             continue
         fn = getattr(lib, name)
         fn.restype = res
@@ -265,7 +269,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     if _LIB is None or path != LIB_PATH:
         if not os.path.exists(path):
             raise MqError(f"libmq.so not built at {path}; run __graft_entry__.build()")
-        lib = bind(C.CDLL(path))
+        lib = bind(C.CDLL(path), strict=path == LIB_PATH)
         if path != LIB_PATH:
             return lib
         _LIB = lib

@@ -184,6 +184,19 @@ int mq_select_positions_at(const int32_t* d_col, const int32_t* d_payload, uint6
                            int has_low, int32_t low, int has_high, int32_t high, int32_t* d_pos_out,
                            uint64_t* d_count, void* d_ws, size_t ws_bytes, void* stream);
 
+/* select_column's download pipeline (the API path): the ordered positions
+ * of d_col[0..n) selected in `segs` contiguous row segments (1..64) queued on `stream`,
+ * and each segment's positions downloaded into h_dst as soon as ITS kernel has finished,
+ * through the staged D2H on a copy stream of the calling thread, while the later
+ * segments' kernels still run. h_dst must hold n int32 (the caller's payload; untouched
+ * beyond the K written). d_pos (capacity n) receives segment s's positions from its
+ * first row (d_pos[r_s ...], r_s = h_rows[s]); h_seg[s] receives segment s's count and
+ * h_rows[s] its first row (segs + 1 entries, h_rows[segs] = n). Returns when every
+ * download is complete; the segments' positions in h_dst are contiguous in order. */
+int mq_select_positions_download(const int32_t* d_col, uint64_t n, int has_low, int32_t low, int has_high,
+                                 int32_t high, int segs, int32_t* d_pos, int32_t* h_dst, uint64_t* h_seg,
+                                 uint64_t* h_rows, void* d_ws, size_t ws_bytes, void* stream);
+
 /* ---- S6 select_column_sorted_index (query.c:143-198) ----
  * d_values: n int32 sorted ascending; d_positions: n size_t row ids. Restates the
  * reference's binary_search + run adjustment exactly (including its low == high

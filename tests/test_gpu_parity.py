@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 from devbuf import Dev
-from refapi import Api, make_column, mq
+from refapi import Api, make_column, mq, take
 
 pytestmark = pytest.mark.gpu
 
@@ -496,6 +496,59 @@ def test_query_api_vs_reference(lib, refcpu, n):
 
 
 @needs_ref
+@pytest.mark.parametrize("segs", [2, 3, 7, 64])
+@pytest.mark.parametrize("n", [5, 1025, 100_000, 3_000_017])
+def test_query_api_select_pipelined_vs_reference(lib, refcpu, monkeypatch, n, segs):
+    """select_column's pipelined path (mq_select_positions_download: row segments, each
+    downloaded while the next ones scan, into a payload over-allocated for n rows and
+    shrunk to K) forced on small columns (MQ_SELECT_PIPE_MIN), including segments with
+    no rows (n < 1024 * segs) and the bound matrix; then fetch / sum / select_result on
+    its shadow, all equal to the reference build."""
+    monkeypatch.setenv("MQ_SELECT_PIPE_MIN", "1")
+    monkeypatch.setenv("MQ_SELECT_SEGS", str(segs))
+    ref, mine = Api(refcpu.reference()), Api(lib)
+    d = _data(n, 11 * n + segs)
+    col = make_column(d)
+    for lo, hi in BOUNDS:
+        p_ref, p_mine = ref.select_column(col, lo, hi), mine.select_column(col, lo, hi)
+        assert np.array_equal(p_ref, p_mine), (n, segs, lo, hi)
+        if not len(p_ref):
+            continue
+        v_ref, v_mine = ref.fetch_column(col, p_ref), mine.fetch_column(col, p_mine)
+        assert np.array_equal(v_ref, v_mine)
+        assert ref.sum_result(v_ref) == mine.sum_result(v_mine)
+        assert np.array_equal(ref.select_result(v_ref, p_ref, -3, 3),
+                              mine.select_result(v_mine, p_mine, -3, 3))
+
+
+def test_query_api_select_pipelined_large(lib, refcpu):
+    """The default pipelined select (4 segments from 2^26 rows) on 2^26 + 4097 rows at
+    0.1 %, 1 %, 30 % and 100 %: positions equal the oracle's; the fetch that follows
+    reads the shadow (no result upload)."""
+    n = (1 << 26) + 4097
+    d = refcpu.gen_uniform(n, 42, n)
+    col = make_column(d)
+    api = Api(lib)
+    for sel in (0.001, 0.01, 0.3, 1.0):
+        lo = n // 5
+        hi = lo + int(sel * n) if sel < 1 else n
+        if sel == 1.0:
+            lo = 0
+        p = api.select_column(col, lo, hi)
+        want = refcpu.select_scan(d, lo, hi)
+        assert np.array_equal(p, want), sel
+    up0 = mq.residency(lib)["result_uploads"]
+    s = mq.Status(0, None)
+    lo_c, hi_c = C.pointer(C.c_int(n // 5)), C.pointer(C.c_int(n // 5 + n // 100))
+    r = lib.select_column(C.byref(col), lo_c, hi_c, C.byref(s))
+    f = lib.fetch_column(C.byref(col), r, C.byref(s))
+    assert s.code == mq.OK
+    assert mq.residency(lib)["result_uploads"] == up0
+    pos = take(r)
+    assert np.array_equal(take(f), d[pos])
+
+
+@needs_ref
 def test_query_api_shared_select_vs_reference(lib, refcpu):
     ref, mine = Api(refcpu.reference()), Api(lib)
     n = 50_000
@@ -827,12 +880,17 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
 # ---------------------------------------------------------------------------
 # S11 shared_select (device API): Q predicates, two passes, exact-size outputs
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("ballot", [False, True])
 @pytest.mark.parametrize("twopass", [False, True])
 @pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
-                                 (3_000_017, 20), (2_000_003, 2)])
-def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass):
+                                 (3_000_017, 20), (2_000_003, 2), (2_000_003, 5)])
+def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass, ballot):
+    """Every Q takes the elementary-interval kernels by default (round 5: from Q = 1);
+    ballot = True forces the per-query ballot kernels (MQ_SS_IMPL=ballot)."""
     if twopass:
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
+    if ballot:
+        monkeypatch.setenv("MQ_SS_IMPL", "ballot")
     rng = np.random.default_rng(n + q)
     d = rng.integers(-1000, 1000, n, dtype=np.int32)
     if n > 8:

@@ -188,9 +188,8 @@ def test_fetch_with_foreign_positions(lib, refcpu):
 
 @pytest.mark.parametrize("q", [2, 5, 20, 300])
 def test_shared_select_on_shards(lib, refcpu, q):
-    """shared_select (query.c:439-583) over a 2-way split: Q <= 3 as ordered selects,
-    more as count + write per shard (ballots below 12 queries, elementary intervals
-    above), Q > 256 in chunks."""
+    """shared_select (query.c:439-583) over a 2-way split: one query as an ordered
+    select, more as count + write per shard (elementary intervals), Q > 256 in chunks."""
     config(lib, 2)
     n = 2_500_003
     v = refcpu.gen_uniform(n, 47, 100_000)
