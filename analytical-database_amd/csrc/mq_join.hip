@@ -766,7 +766,8 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
 // the words are sorted by window id, so one binary search per window boundary
 // (nw + 1 threads, ~28 dependent reads whose upper levels sit in L2) instead of a
 // pass over all n words (0.48 ms at 2^28).
-__global__ __launch_bounds__(kTPB) void k_win_bounds(const u64* __restrict__ in, uint64_t n, Win t,
+template <typename T>
+__global__ __launch_bounds__(kTPB) void k_win_bounds(const T* __restrict__ in, uint64_t n, Win t,
                                                      uint32_t nw, uint32_t* __restrict__ wstart) {
     const uint32_t x = blockIdx.x * kTPB + threadIdx.x;
     if (x > nw) return;
@@ -784,6 +785,7 @@ __global__ __launch_bounds__(kTPB) void k_win_bounds(const u64* __restrict__ in,
 // 3.3 ms at 256 threads for 2^28 rows),
 // then store the whole window (coalesced). Duplicates, the empty marker and an
 // overfull window set *general.
+template <bool STORE>
 __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ in,
                                                     const uint32_t* __restrict__ wstart,
                                                     u64* __restrict__ words, Win t,
@@ -837,6 +839,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
             }
         }
     }
+    if constexpr (!STORE) return;  // the check alone (partitioned probe: no global table)
     __syncthreads();
     for (uint32_t bk = threadIdx.x; bk < W / kBucket; bk += kWinTPB) {
         const uint32_t s0 = bk * kBucket;
@@ -847,6 +850,346 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
     __syncthreads();
     u64* dst = words + (uint64_t)w * W;
     for (uint32_t x = threadIdx.x; x < W; x += kWinTPB) dst[x] = tab[x];
+}
+
+// ---- the partitioned unique probe (round 5) ----
+// A probe row's bucket read is a random 128-B line fetch from a table far beyond the
+// Infinity Cache: 2^28 probes moved ~34 GB for 8 GB of buckets (PMC). Instead the probe
+// keys take the build's window partition (the same LSD passes, u32 keys), one block per
+// window builds the window's table in LDS from the build's partitioned words and probes
+// it with the window's probe keys (k_win_join: no global table is ever written or
+// read), and the results go back to probe order by running the passes backwards
+// (k_pwin_gather). Everything moves as streams.
+
+// One LSD pass of the probe keys by window-id digit (k_win_scatter over u32 keys).
+__global__ __launch_bounds__(kTPB) void k_pwin_scatter(const uint32_t* __restrict__ in, uint64_t n, Win t, int shift,
+                                                       const u64* __restrict__ goff, uint32_t ntiles,
+                                                       uint32_t* __restrict__ out) {
+    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    __shared__ uint32_t loff[kRadix];
+    __shared__ u64 gofs[kRadix];
+    __shared__ uint32_t stage[kSortTile];
+    __shared__ uint32_t wsum[kTPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    __syncthreads();
+    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    uint32_t el[kSortItems], dr[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        el[k] = __builtin_nontemporal_load(in + (i < n ? i : n - 1));
+    }
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (win_id(el[k], t) >> shift) & 0xFF;
+        const u64 peers = match_any8(d, __ballot(valid));
+        const uint32_t lt = lanes_below(peers);
+        const uint32_t cur = wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = tot;
+        tot += c;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t excl = incl - tot;
+    for (int w = 0; w < wave; w++) excl += wsum[w];
+    loff[tid] = excl;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++)
+        if (dr[k] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
+            stage[loff[d] + wcnt[wave][d] + r] = el[k];
+        }
+    __syncthreads();
+    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint32_t e = (uint32_t)(k * kTPB + tid);
+        if (e < tn) {
+            const uint32_t v = stage[e];
+            const uint32_t d = (win_id(v, t) >> shift) & 0xFF;
+            out[gofs[d] + (e - loff[d])] = v;
+        }
+    }
+}
+
+// Persistent window kernels (round 5): a window is a small job (8192 slots' worth of
+// build words, ~4096 on average, and ~4096 probe keys) and two 64 KB-LDS blocks share a
+// CU, so a block walks windows w, w + G, ... and issues the next window's loads (its
+// bounds one window earlier still) before the current window's LDS work. kWinPer build
+// words and kJoinPer probe keys a thread cover 8192 / 5120 per window; probe keys past
+// that are loaded in place.
+//
+// In LDS a window is not an open-addressing table but its words grouped by bucket (a
+// counting sort, CSR): kCsrBuckets buckets by hash, one LDS atomic add per word gives
+// its rank, a scan the buckets' starts, a store its place. A lookup reads its bucket's
+// bounds and then the bucket's words (about one), which are independent reads. The
+// table's CAS insert and linear probe were chains of dependent LDS round trips: the
+// first form of these kernels (one window per block, k_win_build's CAS insert) took
+// 1.6 ms for the check and 3.3 ms for the join at 2^28 rows.
+constexpr int kJoinPer = 5;
+constexpr int kWinPer = (1 << kWinLog) / kWinTPB;
+constexpr uint32_t kCsrBuckets = 1u << (kWinLog - 1);        // 4096: about one word a bucket
+constexpr uint32_t kCsrCap = (1u << kWinLog) - (1u << kWinLog) / 4;  // 6144 words: the 3/4 rule
+
+__device__ __forceinline__ uint32_t csr_bucket(uint32_t key, const Win& t) {
+    return (uint32_t)((hash32(key) & t.wmask) >> 1);
+}
+
+__device__ __forceinline__ void win_load(const u64* __restrict__ in, uint32_t b, uint32_t e, u64 (&v)[kWinPer]) {
+#pragma unroll
+    for (int k = 0; k < kWinPer; k++) {
+        const uint32_t i = b + threadIdx.x + (uint32_t)k * kWinTPB;
+        v[k] = i < e ? __builtin_nontemporal_load(in + i) : kEmpty;
+    }
+}
+
+// The window's c words (c <= kCsrCap, threads' words vs[k] = word threadIdx + k * kWinTPB)
+// grouped by bucket into csr; boff[b] .. boff[b + 1] = bucket b's words. Ends synced.
+__device__ __forceinline__ void csr_build(const u64 (&vs)[kWinPer], uint32_t c, const Win& t, u64* csr,
+                                          uint32_t* boff, uint32_t* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t x = tid; x <= kCsrBuckets; x += kWinTPB) boff[x] = 0;
+    __syncthreads();
+    uint32_t rk[kWinPer];
+#pragma unroll
+    for (int k = 0; k < kWinPer; k++) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * kWinTPB;
+        rk[k] = i < c ? atomicAdd(&boff[csr_bucket((uint32_t)vs[k], t)], 1u) : 0u;
+    }
+    __syncthreads();
+    // exclusive scan of the kCsrBuckets counts: 4 consecutive a thread
+    constexpr int kQ = (int)(kCsrBuckets / kWinTPB);
+    uint32_t cnt[kQ], tot = 0;
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+        cnt[q] = boff[tid * kQ + q];
+        tot += cnt[q];
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - tot;
+    for (int w = 0; w < wave; w++) run += wsum[w];
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+        boff[tid * kQ + q] = run;
+        run += cnt[q];
+    }
+    if (tid == kWinTPB - 1) boff[kCsrBuckets] = run;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kWinPer; k++) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * kWinTPB;
+        if (i < c) csr[boff[csr_bucket((uint32_t)vs[k], t)] + rk[k]] = vs[k];
+    }
+    __syncthreads();
+}
+
+// One window at a time per block: the window's build words grouped in LDS, then each of
+// the window's probe keys (partitioned order) looks itself up in its bucket. r[i] =
+// payload << 32 | 1 on a hit, 0 on a miss. The build was not checked: a window over
+// kCsrCap words, or a probe key that finds two build words, sets *flag, and the caller
+// rebuilds without the partition (the table's empty word is an ordinary word here).
+__global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bwords,
+                                                      const uint32_t* __restrict__ bstart,
+                                                      const uint32_t* __restrict__ pkeys,
+                                                      const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
+                                                      u64* __restrict__ r, uint32_t* __restrict__ flag) {
+    __shared__ u64 csr[kCsrCap];
+    __shared__ uint32_t boff[kCsrBuckets + 1];
+    __shared__ uint32_t wsum[kWinTPB / 64];
+    const uint32_t G = gridDim.x;
+    uint32_t w = blockIdx.x;
+    if (w >= nwin) return;
+    auto key_load = [&](uint32_t pb, uint32_t pe, uint32_t (&key)[kJoinPer]) {
+#pragma unroll
+        for (int k = 0; k < kJoinPer; k++) {
+            const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+            key[k] = i < pe ? __builtin_nontemporal_load(pkeys + i) : 0u;
+        }
+    };
+    bool dup = false;
+    // a key on two build words shows up only where a probe key matches it (duplicates no
+    // probe row meets do not change the unique output): then the flag
+    auto lookup = [&](uint32_t key) -> u64 {
+        const uint32_t bk = csr_bucket(key, t);
+        const uint32_t x0 = boff[bk], x1 = boff[bk + 1];
+        u64 out = 0;
+        uint32_t hits = 0;
+        for (uint32_t x = x0; x < x1; x++) {
+            const u64 v = csr[x];
+            if ((uint32_t)v == key) out = (v & 0xFFFFFFFF00000000ull) | 1ull, hits++;
+        }
+        dup |= hits > 1;
+        return out;
+    };
+    uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
+    u64 vs[kWinPer];
+    uint32_t key[kJoinPer];
+    win_load(bwords, b, e, vs);
+    key_load(pb, pe, key);
+    uint32_t bn = 0, en = 0, pbn = 0, pen = 0;
+    if (w + G < nwin) bn = bstart[w + G], en = bstart[w + G + 1], pbn = pstartw[w + G], pen = pstartw[w + G + 1];
+    for (; w < nwin; w += G) {
+        u64 vn[kWinPer];
+        uint32_t keyn[kJoinPer];
+        win_load(bwords, bn, en, vn);
+        key_load(pbn, pen, keyn);
+        uint32_t bnn = 0, enn = 0, pbnn = 0, penn = 0;
+        if (w + 2 * G < nwin)
+            bnn = bstart[w + 2 * G], enn = bstart[w + 2 * G + 1], pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
+        if (e - b > kCsrCap) {  // uniform: an overfull window (the probe's results are dropped)
+            dup = true;
+        } else {
+            csr_build(vs, e - b, t, csr, boff, wsum);
+#pragma unroll
+            for (int k = 0; k < kJoinPer; k++) {
+                const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+                if (i < pe) __builtin_nontemporal_store(lookup(key[k]), r + i);
+            }
+            for (uint32_t i = pb + threadIdx.x + (uint32_t)kJoinPer * kWinTPB; i < pe; i += kWinTPB)
+                __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i)), r + i);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < kWinPer; k++) vs[k] = vn[k];
+#pragma unroll
+        for (int k = 0; k < kJoinPer; k++) key[k] = keyn[k];
+        b = bn, e = en, pb = pbn, pe = pen;
+        bn = bnn, en = enn, pbn = pbnn, pen = penn;
+    }
+    if (dup) *flag = 1;
+}
+
+// The inverse of one k_pwin_scatter pass: keys = that pass's input (tile order), rin =
+// per-row results in its output order; rout[i] = the result of input row i. The tile's
+// rows are ranked exactly as the scatter ranked them, so row i's place in the output is
+// known; each digit's run of the tile is read from rin as a contiguous stretch (staged in
+// LDS by place) and every row takes its own value back. FINAL (the pass over the probe
+// column itself): per row the payload (pstart) and, per 64 rows, the hit word.
+template <bool FINAL>
+__global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict__ keys, uint64_t n, Win t,
+                                                      int shift, const u64* __restrict__ goff, uint32_t ntiles,
+                                                      const u64* __restrict__ rin, u64* __restrict__ rout,
+                                                      uint32_t* __restrict__ pstart, u64* __restrict__ hits) {
+    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    __shared__ uint32_t loff[kRadix];
+    __shared__ u64 gofs[kRadix];
+    __shared__ u64 stage[kSortTile];
+    __shared__ uint8_t sdig[kSortTile];
+    __shared__ uint32_t wsum[kTPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    __syncthreads();
+    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    uint32_t el[kSortItems], dr[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        el[k] = __builtin_nontemporal_load(keys + (i < n ? i : n - 1));
+    }
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (win_id(el[k], t) >> shift) & 0xFF;
+        const u64 peers = match_any8(d, __ballot(valid));
+        const uint32_t lt = lanes_below(peers);
+        const uint32_t cur = wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = tot;
+        tot += c;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t excl = incl - tot;
+    for (int w = 0; w < wave; w++) excl += wsum[w];
+    loff[tid] = excl;
+    __syncthreads();
+    uint32_t sp[kSortItems];  // each row's place in the tile's digit order
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        sp[k] = 0;
+        if (dr[k] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
+            sp[k] = loff[d] + wcnt[wave][d] + r;
+            sdig[sp[k]] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    {
+        u64 v[kSortItems];  // all reads in flight first
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint32_t e = (uint32_t)(k * kTPB + tid);
+            const uint32_t d = e < tn ? sdig[e] : 0u;
+            v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) stage[k * kTPB + tid] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const u64 v = dr[k] != 0xFFFFFFFFu ? stage[sp[k]] : 0ull;
+        if constexpr (FINAL) {
+            const u64 m = __ballot((v & 1ull) != 0);
+            if (i < n) __builtin_nontemporal_store((uint32_t)(v >> 32), pstart + i);
+            if (lane == 0 && i < n) hits[i >> 6] = m;
+        } else {
+            if (i < n) __builtin_nontemporal_store(v, rout + i);
+        }
+    }
 }
 
 // Duplicate keys without a sort (round 3): the build rows are partitioned by window
@@ -1449,6 +1792,50 @@ __global__ __launch_bounds__(kTPB) void k_join_write_hits(const u64* __restrict_
     }
 }
 
+// The same with 4 rows a lane (round 5): payloads and probe positions read as 16-byte
+// loads (p2 and pstart 16-byte aligned; else the 1-row kernel), a lane's hits are 4
+// bits of its word, its output slot the word's offset plus the hits below them. The
+// 1-row form moved its 3 GB at ~3 TB/s (one 4-byte load per thread and iteration).
+__global__ __launch_bounds__(kTPB) void k_join_write_hits4(const u64* __restrict__ hits,
+                                                           const u64* __restrict__ woffs,
+                                                           const uint32_t* __restrict__ pstart,
+                                                           const int* __restrict__ p2, uint64_t n2,
+                                                           int* __restrict__ out1, int* __restrict__ out2) {
+    const uint64_t stride = (uint64_t)gridDim.x * kTPB * 4;
+    for (uint64_t j = ((uint64_t)blockIdx.x * kTPB + threadIdx.x) * 4; j < n2; j += stride) {
+        const u64 m = hits[j >> 6];
+        const uint32_t sh = (uint32_t)(j & 63);
+        const uint32_t bits = (uint32_t)(m >> sh) & 0xFu;
+        if (!bits) continue;
+        u64 o = woffs[j >> 6] + (u64)__popcll(m & ((1ull << sh) - 1));
+        uint4 pv;
+        int4 qv = make_int4(0, 0, 0, 0);
+        if (j + 3 < n2) {
+            pv = *reinterpret_cast<const uint4*>(pstart + j);
+            if (out2 && p2) qv = *reinterpret_cast<const int4*>(p2 + j);
+        } else {
+            pv.x = pstart[j];
+            pv.y = j + 1 < n2 ? pstart[j + 1] : 0u;
+            pv.z = j + 2 < n2 ? pstart[j + 2] : 0u;
+            pv.w = 0u;
+            if (out2 && p2) {
+                qv.x = p2[j];
+                qv.y = j + 1 < n2 ? p2[j + 1] : 0;
+                qv.z = j + 2 < n2 ? p2[j + 2] : 0;
+            }
+        }
+        const uint32_t pa[4] = {pv.x, pv.y, pv.z, pv.w};
+        const int qa[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            if (bits & (1u << e)) {
+                out1[o] = (int)pa[e];
+                if (out2) out2[o] = qa[e];
+                o++;
+            }
+    }
+}
+
 // Diagnostic: k_ht_probe_unique's memory pattern alone (mq_random_read). Read j
 // goes to slot hash32(j) of a 2^k-slot table; 8 reads per lane in flight.
 __global__ __launch_bounds__(kTPB) void k_random_read(const u64* __restrict__ t, uint64_t mask, uint64_t n,
@@ -1892,7 +2279,7 @@ struct mq_join {
     uint32_t* start;
     uint32_t* len;
     const int* bpos;       // build positions in run order (p1 itself, or sorted copy)
-    void* owned[12];       // device allocations owned by the handle
+    void* owned[16];       // device allocations owned by the handle
     int nowned;
     bool pruns;            // the last probe took the per-64-row-word form (packed runs of < 15 rows)
     bool slot16;           // unique == 2: the 16-byte-slot table words16 (k_win_build_runs16), geometry win16
@@ -1907,6 +2294,19 @@ struct mq_join {
     u64* scan_scratch;
     u64* longq;            // per-row write: chunks of the long runs (k_join_write_long)
     hipStream_t stream;    // the stream of the handle's last queued work (juse)
+    // partitioned unique build (round 5): no global table; the build's words partitioned
+    // by window (pwords) and each window's first word (pwstart, nwin + 1 entries); the
+    // probe partitions its keys the same way (passes LSD passes) and joins window by
+    // window in LDS (probe_partitioned). words == nullptr until a probe asks for the table.
+    bool part;
+    const int32_t* c1;     // the build inputs (valid until mq_join_free): a partitioned build
+    const int32_t* p1;     // that meets a duplicate key or an overfull window is rebuilt
+    uint32_t* pflag;       // the window join's flag (a duplicate met, a window overfull)
+    u64* pwords;
+    uint32_t* pwstart;
+    uint32_t nwin;
+    int passes;
+    uint64_t slots;
 };
 
 namespace {
@@ -1941,6 +2341,24 @@ int juse(mq_join* j, hipStream_t st) {
 void jfree_all(mq_join* j) {
     for (int i = 0; i < j->nowned; i++) pool_free_on(j->owned[i], j->stream);
     j->nowned = 0;
+}
+
+// Give one owned allocation back (stream-ordered).
+void jdrop(mq_join* j, void* p) {
+    for (int i = 0; i < j->nowned; i++)
+        if (j->owned[i] == p) {
+            j->owned[i] = j->owned[--j->nowned];
+            pool_free_on(p, j->stream);
+            return;
+        }
+}
+
+// The partitioned probe from this many build rows (MQ_JOIN_PART_MIN; MQ_JOIN_PART=0: off).
+uint64_t part_min_rows() {
+    const char* e = getenv("MQ_JOIN_PART");
+    if (e && e[0] == '0') return ~0ull;
+    const char* m = getenv("MQ_JOIN_PART_MIN");
+    return m ? strtoull(m, nullptr, 10) : (1ull << 20);
 }
 
 // Unique-path build.
@@ -2000,7 +2418,7 @@ int sample_has_dups(const int* c1, uint64_t n, uint32_t* dflag, hipStream_t st, 
 }
 
 int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
-                  uint32_t* general, hipStream_t st, const DevState* s) {
+                  uint32_t* general, hipStream_t st, const DevState* s, bool keep = false) {
     const Win t = j->win;
     j->marks = n >= kWindowBuildRows && !getenv("MQ_JOIN_NOMARKS");
     if (n < kWindowBuildRows) {
@@ -2061,8 +2479,24 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
         src = dst;
         dst = (dst == a) ? b : a;
     }
-    hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
-    hipLaunchKernelGGL(k_win_build, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, t, general);
+    hipLaunchKernelGGL(k_win_bounds<u64>, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
+    if (keep) {  // the partitioned build: the words and window bounds kept (checked by the probe)
+        int rc = jown(j, src);
+        if (rc) return done(rc);  // (jown freed src)
+        if ((rc = jown(j, wstart))) {
+            if (src == a) a = nullptr; else b = nullptr;
+            wstart = nullptr;
+            return done(rc);
+        }
+        j->pwords = src;
+        j->pwstart = wstart;
+        j->nwin = nw;
+        j->passes = passes;
+        if (src == a) a = nullptr; else b = nullptr;
+        wstart = nullptr;
+        return done(MQ_OK);
+    }
+    hipLaunchKernelGGL(k_win_build<true>, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, t, general);
     if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window build"));
     // the temporaries are released only after the build has run
     if (hipStreamSynchronize(st) != hipSuccess) return done(set_err(MQ_EHIP, "join: build sync"));
@@ -2147,7 +2581,7 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     }
     uint32_t flag = 0;
     if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return drop(set_err(MQ_EHIP, "join: memset"));
-    hipLaunchKernelGGL(k_win_bounds, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
+    hipLaunchKernelGGL(k_win_bounds<u64>, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
     if (s16)
         hipLaunchKernelGGL(k_win_build_runs16, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, w16, bp, t, general);
     else
@@ -2412,6 +2846,187 @@ int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, i
 
 }  // namespace mqi
 
+namespace {
+
+// The partitioned unique probe (k_pwin_scatter / k_win_join / k_pwin_gather above):
+// per probe row its payload (pstart) and per 64 rows the hit word, as k_ht_probe_unique
+// leaves them. Temporaries are freed stream-ordered.
+int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
+    const Win t = j->win;
+    const int passes = j->passes;
+    const uint64_t ntiles = ceil_div(n2, kSortTile), nh = ntiles * kRadix;
+    uint32_t* K[4] = {reinterpret_cast<uint32_t*>(const_cast<int32_t*>(d_c2)), nullptr, nullptr, nullptr};
+    u64* hs[3] = {nullptr, nullptr, nullptr};
+    u64* R[2] = {nullptr, nullptr};
+    uint32_t *hist = nullptr, *pws = nullptr;
+    u64* scratch = nullptr;
+    auto done = [&](int rc) {
+        for (int p = 1; p <= passes; p++) pool_free_on(K[p], st);
+        for (int p = 0; p < passes; p++) pool_free_on(hs[p], st);
+        pool_free_on(R[0], st);
+        pool_free_on(R[1], st);
+        pool_free_on(hist, st);
+        pool_free_on(pws, st);
+        pool_free_on(scratch, st);
+        return rc;
+    };
+    bool ok = true;
+    for (int p = 1; p <= passes; p++) ok = ok && (K[p] = (uint32_t*)pool_alloc(n2 * 4));
+    for (int p = 0; p < passes; p++) ok = ok && (hs[p] = (u64*)pool_alloc(nh * 8));
+    ok = ok && (R[0] = (u64*)pool_alloc(n2 * 8)) && (passes < 2 || (R[1] = (u64*)pool_alloc(n2 * 8))) &&
+         (hist = (uint32_t*)pool_alloc(nh * 4)) && (pws = (uint32_t*)pool_alloc(((uint64_t)j->nwin + 1) * 4)) &&
+         (scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8));
+    if (!ok) return done(set_err(MQ_ENOMEM, "join: partitioned probe buffers (%llu rows)", (unsigned long long)n2));
+    for (int p = 0; p < passes; p++) {
+        hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)K[p],
+                           (const u64*)nullptr, n2, t, 8 * p, hist, (uint32_t)ntiles);
+        int rc = scan_exclusive<uint32_t>(hist, hs[p], nh, scratch, st);
+        if (rc) return done(rc);
+        hipLaunchKernelGGL(k_pwin_scatter, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t, 8 * p, hs[p],
+                           (uint32_t)ntiles, K[p + 1]);
+        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe partition"));
+    }
+    hipLaunchKernelGGL(k_win_bounds<uint32_t>, dim3(j->nwin / kTPB + 1), dim3(kTPB), 0, st, K[passes], n2, t,
+                       j->nwin, pws);
+    DevState* s;
+    if (int rc0 = ensure_ready(&s)) return done(rc0);
+    const uint32_t gj = j->nwin < (uint32_t)s->cus * 2 ? j->nwin : (uint32_t)s->cus * 2;
+    hipLaunchKernelGGL(k_win_join, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws, j->nwin,
+                       t, R[0], j->pflag);
+    if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window join"));
+    int cur = 0;
+    for (int p = passes - 1; p >= 0; p--) {
+        if (p == 0)
+            hipLaunchKernelGGL(k_pwin_gather<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t, 0, hs[0],
+                               (uint32_t)ntiles, R[cur], (u64*)nullptr, pstart, hits);
+        else
+            hipLaunchKernelGGL(k_pwin_gather<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t, 8 * p,
+                               hs[p], (uint32_t)ntiles, R[cur], R[cur ^ 1], (uint32_t*)nullptr, (u64*)nullptr);
+        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe unpartition"));
+        cur ^= 1;
+    }
+    return done(MQ_OK);
+}
+
+// The global table of a partitioned build, for a probe too small to pay for its own
+// partition (and the handle's later probes): the checked windows stored as k_win_build
+// stores them.
+// *flagged = 1 when the windows hold a duplicate key, the empty marker or an overfull
+// window: the caller then rebuilds without the partition (rebuild_unpartitioned).
+int materialize_table(mq_join* j, hipStream_t st, bool* flagged) {
+    int rc = jalloc(j, (void**)&j->words, j->slots * 8);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(j->pflag, 0, 4, st));
+    hipLaunchKernelGGL(k_win_build<true>, dim3(j->nwin), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, j->words, j->win,
+                       j->pflag);
+    LAUNCHCHK("k_win_build");
+    uint32_t f = 0;
+    HIPCHK(hipMemcpyAsync(&f, j->pflag, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *flagged = f != 0;
+    jdrop(j, j->pwords);
+    jdrop(j, j->pwstart);
+    j->pwords = nullptr;
+    j->pwstart = nullptr;
+    j->part = false;
+    return MQ_OK;
+}
+
+// The build proper into a fresh handle (device and stream set). allow_part: a unique
+// build of part_min_rows() rows and more keeps its window partition for the
+// partitioned probe instead of building the table (a duplicate key or an overfull
+// window found there later sends it back here with allow_part = false).
+int build_into(mq_join* j, const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, hipStream_t st, DevState* s,
+               bool allow_part) {
+    int rc;
+    j->n1 = n1;
+    j->c1 = d_c1;
+    j->p1 = d_p1;
+    uint64_t slots = 64;
+    while (slots < 2 * n1) slots <<= 1;
+    j->mask = slots - 1;
+    j->win.mask = j->mask;
+    j->win.wlog = 0;
+    while (j->win.wlog < kWinLog && (1ull << (j->win.wlog + 1)) <= slots) j->win.wlog++;
+    j->win.wmask = (1ull << j->win.wlog) - 1;
+    j->slots = slots;
+    // the partitioned build keeps no global table: allocated only if a path needs it
+    const bool part = allow_part && n1 >= kWindowBuildRows && n1 >= part_min_rows() && j->win.wlog == kWinLog;
+    uint32_t* dflag = nullptr;
+    if ((!part && (rc = jalloc(j, (void**)&j->words, slots * 8))) || (rc = jalloc(j, (void**)&dflag, 16)))
+        return rc;
+    j->pflag = dflag + 2;  // (dflag[1] is the sampled duplicate check's)
+    j->bpos = nullptr;  // unique table carries the build positions itself
+    j->unique = 1;
+    if (n1) {
+        HIPCHK(hipMemsetAsync(dflag, 0, 16, st));
+        bool sampled = false;
+        if ((rc = sample_has_dups(d_c1, n1, dflag, st, s, &sampled))) return rc;
+        uint32_t dup = sampled ? 1u : 0u;
+        if (!sampled) {
+            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, part))) return rc;
+            if (part) {  // nothing to read back: the probe checks the windows
+                j->part = true;
+                return MQ_OK;
+            }
+            HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        if (part && (rc = jalloc(j, (void**)&j->words, slots * 8))) return rc;  // (sampled duplicates)
+        if (dup && (rc = build_window_runs(j, d_c1, d_p1, n1, slots, dflag, st, s)) != 1)
+            return rc;  // 0: the windowed runs build took it
+        if (dup) {  // general path: stable sort by key, runs in insertion order
+            j->unique = 0;
+            j->bpos = d_p1;
+            uint32_t *skeys, *svals;
+            if ((rc = radix_sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) return rc;
+            if ((rc = jown(j, skeys)) || (rc = jown(j, svals))) {
+                if (rc && j->owned[j->nowned - 1] != skeys) pool_free_on(svals, st);  // (skeys refused: svals still ours)
+                return rc;
+            }
+            j->bpos = reinterpret_cast<const int*>(svals);
+            if ((rc = build_runs(j, skeys, n1, slots, dflag, st, s)) != 1) return rc;  // 0: done, else an error
+            // a window of the distinct keys overflowed: the global-CAS table of run heads
+            j->unique = 0;
+            if ((rc = jalloc(j, (void**)&j->start, slots * 4)) || (rc = jalloc(j, (void**)&j->len, slots * 4)))
+                return rc;
+            HIPCHK(hipMemsetAsync(j->words, 0, slots * 8, st));
+            hipLaunchKernelGGL(k_ht_insert_heads, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys,
+                               n1, j->words, j->start, j->mask);
+            LAUNCHCHK("k_ht_insert_heads");
+            hipLaunchKernelGGL(k_ht_set_len, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys, n1,
+                               j->words, j->start, j->len, j->mask);
+            LAUNCHCHK("k_ht_set_len");
+        }
+    }
+    return MQ_OK;
+}
+
+// A partitioned build whose windows turned out to hold a duplicate key (or an overfull
+// window, or the table's empty word): everything of the build dropped (stream-ordered)
+// and built again from the inputs the old way. The probe arrays stay.
+int rebuild_unpartitioned(mq_join* j, hipStream_t st) {
+    DevState* s;
+    int rc = ensure_ready(&s);
+    if (rc) return rc;
+    jfree_all(j);
+    const int32_t *c1 = j->c1, *p1 = j->p1;
+    const uint64_t n1 = j->n1;
+    mq_join keep = *j;
+    std::memset(j, 0, sizeof(*j));
+    j->device = keep.device;
+    j->stream = st;
+    j->p01 = keep.p01;
+    j->pstart = keep.pstart;
+    j->plen = keep.plen;
+    j->offs = keep.offs;
+    j->scan_scratch = keep.scan_scratch;
+    j->longq = keep.longq;
+    return build_into(j, c1, p1, n1, st, s, false);
+}
+
+}  // namespace
+
 extern "C" {
 
 int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join** out,
@@ -2426,90 +3041,10 @@ int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join
     std::memset(j, 0, sizeof(*j));
     HIPCHK(hipGetDevice(&j->device));
     j->stream = st;
-    j->n1 = n1;
-    uint64_t slots = 64;
-    while (slots < 2 * n1) slots <<= 1;
-    j->mask = slots - 1;
-    j->win.mask = j->mask;
-    j->win.wlog = 0;
-    while (j->win.wlog < kWinLog && (1ull << (j->win.wlog + 1)) <= slots) j->win.wlog++;
-    j->win.wmask = (1ull << j->win.wlog) - 1;
-    uint32_t* dflag = nullptr;
-    if ((rc = jalloc(j, (void**)&j->words, slots * 8)) || (rc = jalloc(j, (void**)&dflag, 16))) {
+    if ((rc = build_into(j, d_c1, d_p1, n1, st, s, true))) {
         jfree_all(j);
         delete j;
         return rc;
-    }
-    j->bpos = nullptr;  // unique table carries the build positions itself
-    j->unique = 1;
-    if (n1) {
-        HIPCHK(hipMemsetAsync(dflag, 0, 4, st));
-        bool sampled = false;
-        if ((rc = sample_has_dups(d_c1, n1, dflag, st, s, &sampled))) {
-            jfree_all(j);
-            delete j;
-            return rc;
-        }
-        uint32_t dup = sampled ? 1u : 0u;
-        if (!sampled) {
-            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s))) {
-                jfree_all(j);
-                delete j;
-                return rc;
-            }
-            HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-        }
-        if (dup && (rc = build_window_runs(j, d_c1, d_p1, n1, slots, dflag, st, s)) != 1) {
-            if (rc) {  // (0: the windowed runs build took it)
-                jfree_all(j);
-                delete j;
-                return rc;
-            }
-            *out = j;
-            return MQ_OK;
-        }
-        if (dup) {  // general path: stable sort by key, runs in insertion order
-            j->unique = 0;
-            j->bpos = d_p1;
-            uint32_t *skeys, *svals;
-            if ((rc = radix_sort_pairs(d_c1, d_p1, n1, &skeys, &svals, st, s))) {
-                jfree_all(j);
-                delete j;
-                return rc;
-            }
-            if ((rc = jown(j, skeys)) || (rc = jown(j, svals))) {
-                if (rc && j->owned[j->nowned - 1] != skeys) pool_free_on(svals, st);  // (skeys refused: svals still ours)
-                jfree_all(j);
-                delete j;
-                return rc;
-            }
-            j->bpos = reinterpret_cast<const int*>(svals);
-            if ((rc = build_runs(j, skeys, n1, slots, dflag, st, s)) != 1) {  // 0: done, else an error
-                if (rc) {
-                    jfree_all(j);
-                    delete j;
-                    return rc;
-                }
-                *out = j;
-                return MQ_OK;
-            }
-            // a window of the distinct keys overflowed: the global-CAS table of run heads
-            j->unique = 0;
-            if ((rc = jalloc(j, (void**)&j->start, slots * 4)) ||
-                (rc = jalloc(j, (void**)&j->len, slots * 4))) {
-                jfree_all(j);
-                delete j;
-                return rc;
-            }
-            HIPCHK(hipMemsetAsync(j->words, 0, slots * 8, st));
-            hipLaunchKernelGGL(k_ht_insert_heads, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys,
-                               n1, j->words, j->start, j->mask);
-            LAUNCHCHK("k_ht_insert_heads");
-            hipLaunchKernelGGL(k_ht_set_len, dim3(stream_grid(s, n1)), dim3(kTPB), 0, st, skeys, n1,
-                               j->words, j->start, j->len, j->mask);
-            LAUNCHCHK("k_ht_set_len");
-        }
     }
     *out = j;
     return MQ_OK;
@@ -2536,6 +3071,17 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     j->m = 0;
     *h_m = 0;
     if (n2 == 0 || j->n1 == 0) return MQ_OK;
+    // a partitioned build and a probe side too small to pay for its own partition (its
+    // passes and the window join read all n1 build words): the global table, once
+    const uint64_t pdiv = getenv("MQ_JOIN_PART_DIV") ? strtoull(getenv("MQ_JOIN_PART_DIV"), nullptr, 10) : 16;
+    if (j->part && n2 < j->n1 / (pdiv ? pdiv : 1)) {
+        bool flagged = false;
+        if ((rc = materialize_table(j, st, &flagged))) return rc;
+        if (flagged) {
+            if ((rc = rebuild_unpartitioned(j, st))) return rc;
+            return mq_join_probe(j, d_c2, n2, h_m, stream);
+        }
+    }
     const uint64_t nwords = (n2 + 63) / 64;
     // packed runs: per-word lengths. Only for the windowed runs build (rs == nullptr:
     // every run shorter than 15 rows), where a word's 64 rows sum to < 2^10; a sorted
@@ -2576,6 +3122,12 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
                            j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks,
                            (uint32_t*)nullptr, (u64*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
+    } else if (j->unique && j->part) {
+        u64* const hits = reinterpret_cast<u64*>(j->plen);
+        HIPCHK(hipMemsetAsync(j->pflag, 0, 4, st));
+        if ((rc = probe_partitioned(j, d_c2, n2, j->pstart, hits, st))) return rc;
+        hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
+        LAUNCHCHK("k_hits_count");
     } else if (j->unique) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
         auto kern = k_ht_probe_unique<false>;
@@ -2595,7 +3147,13 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     uint32_t last_len = 0;
     HIPCHK(hipMemcpyAsync(&last_off, j->offs + (nscan - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&last_len, cnt + (nscan - 1), 4, hipMemcpyDeviceToHost, st));
+    uint32_t pf = 0;
+    if (j->part) HIPCHK(hipMemcpyAsync(&pf, j->pflag, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (pf) {  // a probe key met a duplicate build key (or a window overflowed): rebuild
+        if ((rc = rebuild_unpartitioned(j, st))) return rc;
+        return mq_join_probe(j, d_c2, n2, h_m, stream);
+    }
     j->m = last_off + last_len;
     *h_m = j->m;
     return MQ_OK;
@@ -2610,8 +3168,15 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (!d_out1 || (d_out2 && !d_p2)) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
     if ((rc = juse(j, (hipStream_t)stream))) return rc;
     if (j->unique == 1) {
-        hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
-                           reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
+        const bool v4 = ((reinterpret_cast<uintptr_t>(j->pstart) | reinterpret_cast<uintptr_t>(d_p2)) & 15u) == 0 &&
+                        !(getenv("MQ_JOIN_WRITE1") && getenv("MQ_JOIN_WRITE1")[0] == '1');
+        if (v4)
+            hipLaunchKernelGGL(k_join_write_hits4, dim3(stream_grid(s, (j->n2 + 3) / 4)), dim3(kTPB), 0,
+                               (hipStream_t)stream, reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2,
+                               j->n2, d_out1, d_out2);
+        else
+            hipLaunchKernelGGL(k_join_write_hits, dim3(stream_grid(s, j->n2)), dim3(kTPB), 0, (hipStream_t)stream,
+                               reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2, j->n2, d_out1, d_out2);
         LAUNCHCHK("k_join_write_hits");
         return MQ_OK;
     }

@@ -306,7 +306,9 @@ int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base
                               size_t ws_bytes, void* stream);
 
 /* ---- J1 hash_join as three steps on a handle (lets the caller size the output) ----
- * build: table over (c1, p1); p1 must stay valid until mq_join_free.
+ * build: table over (c1, p1); c1 and p1 must stay valid until mq_join_free (a unique
+ *   build of 2^20 rows and more keeps only its window partition, and one whose probe
+ *   meets a duplicate key is built again from them).
  * probe: per-probe match counts + output offsets for keys c2; *h_m = M.
  * write: the M pairs (out1 = build positions, out2 = probe positions p2). */
 typedef struct mq_join mq_join;

@@ -741,6 +741,74 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
             assert np.array_equal(h2, v1) and np.array_equal(h1, v2), case
 
 
+JOIN_PROBE_MODES = {"table": {"MQ_JOIN_PART": "0"},  # the global table + random bucket reads
+                    "part": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000"},
+                    "part_materialized": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1"}}
+
+
+@pytest.mark.parametrize("mode", list(JOIN_PROBE_MODES))
+@pytest.mark.parametrize("case", ["n2_1", "n2_63", "n2_65", "n2_4097", "all_miss", "all_hit_dup_probe",
+                                  "negative_extremes", "one_pass", "two_passes", "marker", "dup_probed",
+                                  "dup_unprobed", "overfull_window"])
+def test_hash_join_partitioned_probe(lib, refcpu, monkeypatch, mode, case):
+    """Unique builds (round 5): the probe keys partitioned by table window like the build
+    rows, each window joined in LDS (k_win_join), the results taken back to probe order
+    by the inverted passes (k_pwin_gather); "part_materialized" makes the probe side too
+    small for that (MQ_JOIN_PART_DIV), so the checked windows are stored as the global
+    table first; "table" is the random-read probe. One LSD pass (build < 2^20 rows: at
+    most 256 windows) and two (2^21 build rows: 512 windows, a second digit); a build row
+    equal to the table's empty word sends the build to the duplicate paths. The build is
+    not checked up front: a probe key that meets a duplicate build key, or a window of
+    more than 6144 build rows, flags, and the join is built again without the partition
+    (dup_probed, overfull_window); a duplicate no probe row meets leaves the output
+    unchanged (dup_unprobed)."""
+    monkeypatch.setenv("MQ_JOIN_SAMPLE", "0")  # (the sampled duplicate check would catch none here)
+    for k, v in JOIN_PROBE_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(abs(hash((case, mode))) % 2 ** 32)
+    n1 = (1 << 21) + 333 if case == "two_passes" else 200_003
+    c1 = rng.permutation(refcpu.gen_join(n1, "build"))
+    if case.startswith("n2_"):
+        n2 = int(case[3:])
+        c2 = np.concatenate([rng.choice(c1, n2 // 2), rng.integers(-2 ** 31, 2 ** 31 - 1, n2 - n2 // 2)])
+        c2 = c2.astype(np.int64).astype(np.int32)[rng.permutation(n2)]
+    elif case == "all_miss":
+        c2 = refcpu.gen_join(n1 * 4, "build")[n1:n1 + 300_000]  # mix31 is a bijection: never built
+        c1 = rng.permutation(refcpu.gen_join(n1 * 4, "build")[:n1])
+    elif case == "all_hit_dup_probe":
+        c2 = rng.choice(c1, 500_000)  # every probe row hits, keys repeat on the probe side
+    elif case == "negative_extremes":
+        c1 = (rng.choice(1 << 32, n1, replace=False).astype(np.int64) - 2 ** 31).astype(np.int32)
+        c1[:2] = [-2 ** 31, 2 ** 31 - 1]
+        c2 = np.concatenate([c1[::5], [-2 ** 31, 2 ** 31 - 1, 0, -1], rng.integers(-100, 100, 1000)]).astype(np.int32)
+    elif case == "marker":  # {key -1, position -1} is the table's empty word
+        c1 = (rng.permutation(n1) - n1 // 2).astype(np.int32)
+        c2 = rng.integers(-n1, n1, 150_000).astype(np.int32)
+    elif case in ("dup_probed", "dup_unprobed"):
+        c1[n1 - 5] = c1[100]  # one key on two build rows
+        c2 = rng.choice(c1, 300_000)
+        c2 = np.where(c2 == c1[100], c1[7], c2) if case == "dup_unprobed" else c2
+        c2 = np.concatenate([c2, [c1[100]]] if case == "dup_probed" else [c2]).astype(np.int32)
+    elif case == "overfull_window":  # 7000 build keys homed in one 8192-slot window
+        slots = 1 << 19  # 200_003 rows: 2^19 slots, 64 windows
+        i = np.arange(7000, dtype=np.uint64)
+        hw = (np.uint64(5) << np.uint64(13)) | (i & np.uint64(8191)) | ((i + np.uint64(1)) << np.uint64(19))
+        crafted = _inv_fmix32(hw & np.uint64(0xFFFFFFFF))
+        c1 = np.unique(np.concatenate([crafted, c1[:n1 - 7000]]))
+        c1 = c1[rng.permutation(len(c1))]
+        c2 = np.concatenate([rng.choice(c1, 100_000), crafted[:500]]).astype(np.int32)
+    else:
+        c2 = np.concatenate([rng.choice(c1, 700_000), refcpu.gen_join(1 << 20, "probe")]).astype(np.int32)
+        c2 = c2[rng.permutation(len(c2))]
+    p1 = rng.integers(-10 ** 7, 10 ** 7, len(c1), dtype=np.int32)
+    p2 = rng.integers(0, 10 ** 7, len(c2), dtype=np.int32)
+    if case == "marker":
+        p1[np.nonzero(c1 == -1)[0][0]] = -1
+    g1, g2 = _dev_join(lib, c1, p1, c2, p2)
+    w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
+    assert np.array_equal(g1, w1) and np.array_equal(g2, w2), (case, mode)
+
+
 def _inv_fmix32(h):
     """Inverse of libmq's table hash (the murmur3 finaliser, mq_join.hip hash32), so a
     test can pick the home slot of every key."""
@@ -754,15 +822,20 @@ def _inv_fmix32(h):
     return x.astype(np.uint32).view(np.int32)
 
 
+@pytest.mark.parametrize("probe", ["table", "part"])
 @pytest.mark.parametrize("dup", [False, True])
 @pytest.mark.parametrize("marks", [True, False])
-def test_hash_join_clustered_window(lib, refcpu, monkeypatch, dup, marks):
+def test_hash_join_clustered_window(lib, refcpu, monkeypatch, dup, marks, probe):
     """One 8192-slot window of the unique table holds a 5000-slot cluster: 5000 keys
     homed in 16 buckets at its start, so probes of those keys (hits) and of other keys
     homed there (misses) follow chains of up to ~5000 slots through the per-wave
     continuation queue (requeued every step, then drained at the end; the in-step
     drain runs when more than 128 rows wait), with and without the overflow marks.
-    dup: every cluster key twice (the runs table behind the same windowed build)."""
+    dup: every cluster key twice (the runs table behind the same windowed build).
+    probe "part": the partitioned probe (unique builds), whose LDS lookups follow the
+    same chains inside the window."""
+    for k, v in JOIN_PROBE_MODES["part" if probe == "part" else "table"].items():
+        monkeypatch.setenv(k, v)
     if not marks:
         monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
     rng = np.random.default_rng(4242)
