@@ -684,7 +684,8 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
                                                       const int* __restrict__ p1,
                                                       const u64* __restrict__ in, uint64_t n, Win t,
                                                       int shift, const u64* __restrict__ goff,
-                                                      uint32_t ntiles, u64* __restrict__ out) {
+                                                      uint32_t ntiles, u64* __restrict__ out,
+                                                      int* __restrict__ pmm = nullptr) {
     __shared__ uint32_t wcnt[kTPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
@@ -706,6 +707,36 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         el[k] = win_elem<FROM_COLS>(c1, p1, in, i < n ? i : n - 1);
+    }
+    if (FROM_COLS && pmm) {
+        // the payloads' range (a value outside it marks a miss, k_win_join): per block,
+        // then one atomic pair into 64 spread slots (one address for every wave made the
+        // pass 5.5x slower); the host folds the slots
+        int mn = INT32_MAX, mx = INT32_MIN;
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {  // (clamped rows repeat row n - 1: harmless)
+            const int v = (int)(el[k] >> 32);
+            mn = v < mn ? v : mn;
+            mx = v > mx ? v : mx;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        __shared__ int smm[2][kTPB / 64];
+        if (lane == 0) smm[0][wave] = mn, smm[1][wave] = mx;
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll
+            for (int w = 1; w < kTPB / 64; w++) {
+                mn = smm[0][w] < mn ? smm[0][w] : mn;
+                mx = smm[1][w] > mx ? smm[1][w] : mx;
+            }
+            atomicMin(pmm + (tile & 63), mn);
+            atomicMax(pmm + 64 + (tile & 63), mx);
+        }
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
@@ -1019,11 +1050,13 @@ __device__ __forceinline__ void csr_build(const u64 (&vs)[kWinPer], uint32_t c, 
 // payload << 32 | 1 on a hit, 0 on a miss. The build was not checked: a window over
 // kCsrCap words, or a probe key that finds two build words, sets *flag, and the caller
 // rebuilds without the partition (the table's empty word is an ordinary word here).
+template <typename RT>
 __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bwords,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ pkeys,
                                                       const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
-                                                      u64* __restrict__ r, uint32_t* __restrict__ flag) {
+                                                      RT* __restrict__ r, uint32_t* __restrict__ flag,
+                                                      uint32_t sentinel) {
     __shared__ u64 csr[kCsrCap];
     __shared__ uint32_t boff[kCsrBuckets + 1];
     __shared__ uint32_t wsum[kWinTPB / 64];
@@ -1040,7 +1073,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
     bool dup = false;
     // a key on two build words shows up only where a probe key matches it (duplicates no
     // probe row meets do not change the unique output): then the flag
-    auto lookup = [&](uint32_t key) -> u64 {
+    auto lookup = [&](uint32_t key) -> RT {
         const uint32_t bk = csr_bucket(key, t);
         const uint32_t x0 = boff[bk], x1 = boff[bk + 1];
         u64 out = 0;
@@ -1050,8 +1083,14 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
             if ((uint32_t)v == key) out = (v & 0xFFFFFFFF00000000ull) | 1ull, hits++;
         }
         dup |= hits > 1;
-        return out;
+        if constexpr (sizeof(RT) == 4) return hits ? (uint32_t)(out >> 32) : sentinel;
+        else return out;
     };
+    // The loads' order decides what the wait-count pass can overlap (it waits for a
+    // register's load with vmcnt(n), n = the younger memory operations, unknown past a
+    // data-dependent number of stores): the next window's build words are issued at the
+    // top and waited for after this window's grouping, the next window's probe keys
+    // after this window's stores; nothing waits on this window's stores.
     uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
     u64 vs[kWinPer];
     uint32_t key[kJoinPer];
@@ -1059,18 +1098,25 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
     key_load(pb, pe, key);
     uint32_t bn = 0, en = 0, pbn = 0, pen = 0;
     if (w + G < nwin) bn = bstart[w + G], en = bstart[w + G + 1], pbn = pstartw[w + G], pen = pstartw[w + G + 1];
+    // the first window waited for here: else the loop entry merges "pending" from here
+    // with "ready" from the back edge and every iteration waits at its first use
+    __builtin_amdgcn_s_waitcnt(0);
     for (; w < nwin; w += G) {
         u64 vn[kWinPer];
-        uint32_t keyn[kJoinPer];
         win_load(bwords, bn, en, vn);
-        key_load(pbn, pen, keyn);
         uint32_t bnn = 0, enn = 0, pbnn = 0, penn = 0;
         if (w + 2 * G < nwin)
             bnn = bstart[w + 2 * G], enn = bstart[w + 2 * G + 1], pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
-        if (e - b > kCsrCap) {  // uniform: an overfull window (the probe's results are dropped)
+        const bool over = e - b > kCsrCap;  // uniform: an overfull window (its results are dropped)
+        if (!over) csr_build(vs, e - b, t, csr, boff, wsum);
+#pragma unroll
+        for (int k = 0; k < kWinPer; k++) {
+            asm volatile("" : "+v"(vn[k]));  // wait for the next words HERE (not at the loop's end, behind the stores)
+            vs[k] = vn[k];
+        }
+        if (over) {
             dup = true;
         } else {
-            csr_build(vs, e - b, t, csr, boff, wsum);
 #pragma unroll
             for (int k = 0; k < kJoinPer; k++) {
                 const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
@@ -1080,14 +1126,76 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
                 __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i)), r + i);
             __syncthreads();
         }
-#pragma unroll
-        for (int k = 0; k < kWinPer; k++) vs[k] = vn[k];
-#pragma unroll
-        for (int k = 0; k < kJoinPer; k++) key[k] = keyn[k];
+        key_load(pbn, pen, key);
         b = bn, e = en, pb = pbn, pe = pen;
         bn = bnn, en = enn, pbn = pbnn, pen = penn;
     }
     if (dup) *flag = 1;
+}
+
+// The partitioned probe of a windowed RUNS table (duplicate keys, k_win_build_runs: the
+// window's slots hold {key, start << 4 | length}): the window's 64 KB slice of the
+// global table is loaded into LDS whole (coalesced) and each of the window's probe keys
+// follows the table's own probe sequence there (home bucket, linear inside the window,
+// an empty slot ends it). r[i] = the slot's packed run, 0 = no match (a run is never
+// empty, so a hit's payload is never 0).
+__global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict__ words,
+                                                           const uint32_t* __restrict__ pkeys,
+                                                           const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
+                                                           uint32_t* __restrict__ r) {
+    __shared__ u64 tab[1 << kWinLog];
+    const uint32_t W = (uint32_t)t.wmask + 1, G = gridDim.x;
+    uint32_t w = blockIdx.x;
+    if (w >= nwin) return;
+    auto key_load = [&](uint32_t pb, uint32_t pe, uint32_t (&key)[kJoinPer]) {
+#pragma unroll
+        for (int k = 0; k < kJoinPer; k++) {
+            const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+            key[k] = i < pe ? __builtin_nontemporal_load(pkeys + i) : 0u;
+        }
+    };
+    auto lookup = [&](uint32_t key) -> uint32_t {
+        uint32_t h = (uint32_t)ht_home(key, t.wmask);
+        for (uint32_t step = 0; step < W; step++) {
+            const u64 v = tab[h];
+            if (v == kEmpty) return 0u;
+            if ((uint32_t)v == key) return (uint32_t)(v >> 32);
+            h = (h + 1) & (W - 1);
+        }
+        return 0u;
+    };
+    uint32_t pb = pstartw[w], pe = pstartw[w + 1];
+    u64 vs[kWinPer];
+    uint32_t key[kJoinPer];
+    win_load(words + (uint64_t)w * W, 0, W, vs);
+    key_load(pb, pe, key);
+    uint32_t pbn = 0, pen = 0;
+    if (w + G < nwin) pbn = pstartw[w + G], pen = pstartw[w + G + 1];
+    __builtin_amdgcn_s_waitcnt(0);  // (see k_win_join)
+    for (; w < nwin; w += G) {
+        u64 vn[kWinPer];
+        win_load(words + (uint64_t)(w + G < nwin ? w + G : w) * W, 0, w + G < nwin ? W : 0, vn);
+        uint32_t pbnn = 0, penn = 0;
+        if (w + 2 * G < nwin) pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
+#pragma unroll
+        for (int k = 0; k < kWinPer; k++) tab[threadIdx.x + (uint32_t)k * kWinTPB] = vs[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kWinPer; k++) {
+            asm volatile("" : "+v"(vn[k]));  // the next slice waited for here, not behind the stores
+            vs[k] = vn[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kJoinPer; k++) {
+            const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+            if (i < pe) __builtin_nontemporal_store(lookup(key[k]), r + i);
+        }
+        for (uint32_t i = pb + threadIdx.x + (uint32_t)kJoinPer * kWinTPB; i < pe; i += kWinTPB)
+            __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i)), r + i);
+        __syncthreads();
+        key_load(pbn, pen, key);
+        pb = pbn, pe = pen, pbn = pbnn, pen = penn;
+    }
 }
 
 // The inverse of one k_pwin_scatter pass: keys = that pass's input (tile order), rin =
@@ -1096,15 +1204,19 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
 // known; each digit's run of the tile is read from rin as a contiguous stretch (staged in
 // LDS by place) and every row takes its own value back. FINAL (the pass over the probe
 // column itself): per row the payload (pstart) and, per 64 rows, the hit word.
-template <bool FINAL>
+// RUNS (with FINAL): rin holds packed runs (0 = no match); per row pstart = the packed
+// run and per 64 rows wcnt = the sum of their run lengths, as k_ht_probe_unique<true>
+// leaves them for the packed-runs write (hits is then that wcnt, as u32).
+template <bool FINAL, typename RT, bool RUNS = false>
 __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict__ keys, uint64_t n, Win t,
                                                       int shift, const u64* __restrict__ goff, uint32_t ntiles,
-                                                      const u64* __restrict__ rin, u64* __restrict__ rout,
-                                                      uint32_t* __restrict__ pstart, u64* __restrict__ hits) {
+                                                      const RT* __restrict__ rin, RT* __restrict__ rout,
+                                                      uint32_t* __restrict__ pstart, u64* __restrict__ hits,
+                                                      uint32_t sentinel) {
     __shared__ uint32_t wcnt[kTPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ u64 stage[kSortTile];
+    __shared__ RT stage[kSortTile];
     __shared__ uint8_t sdig[kSortTile];
     __shared__ uint32_t wsum[kTPB / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1167,12 +1279,12 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
     __syncthreads();
     const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
     {
-        u64 v[kSortItems];  // all reads in flight first
+        RT v[kSortItems];  // all reads in flight first
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
             const uint32_t e = (uint32_t)(k * kTPB + tid);
             const uint32_t d = e < tn ? sdig[e] : 0u;
-            v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : 0ull;
+            v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : (RT)0;
         }
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) stage[k * kTPB + tid] = v[k];
@@ -1181,10 +1293,27 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        const u64 v = dr[k] != 0xFFFFFFFFu ? stage[sp[k]] : 0ull;
-        if constexpr (FINAL) {
-            const u64 m = __ballot((v & 1ull) != 0);
-            if (i < n) __builtin_nontemporal_store((uint32_t)(v >> 32), pstart + i);
+        const bool in = dr[k] != 0xFFFFFFFFu;
+        const RT v = in ? stage[sp[k]] : (RT)0;
+        if constexpr (FINAL && RUNS) {
+            const uint32_t pay = (uint32_t)v;
+            uint32_t L = pay & 15u;  // (a windowed runs table: every run shorter than 15)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+            if (i < n) __builtin_nontemporal_store(pay, pstart + i);
+            if (lane == 0 && i < n) reinterpret_cast<uint32_t*>(hits)[i >> 6] = L;
+        } else if constexpr (FINAL) {
+            bool hit;
+            uint32_t pay;
+            if constexpr (sizeof(RT) == 4) {
+                hit = in && (uint32_t)v != sentinel;
+                pay = (uint32_t)v;
+            } else {
+                hit = ((u64)v & 1ull) != 0;
+                pay = (uint32_t)((u64)v >> 32);
+            }
+            const u64 m = __ballot(hit);
+            if (i < n) __builtin_nontemporal_store(pay, pstart + i);
             if (lane == 0 && i < n) hits[i >> 6] = m;
         } else {
             if (i < n) __builtin_nontemporal_store(v, rout + i);
@@ -2302,6 +2431,8 @@ struct mq_join {
     const int32_t* c1;     // the build inputs (valid until mq_join_free): a partitioned build
     const int32_t* p1;     // that meets a duplicate key or an overfull window is rebuilt
     uint32_t* pflag;       // the window join's flag (a duplicate met, a window overfull)
+    bool narrow;           // the window join's results as u32 payloads, `sentinel` = a miss
+    uint32_t sentinel;     // (a value outside the build payloads' range)
     u64* pwords;
     uint32_t* pwstart;
     uint32_t nwin;
@@ -2418,7 +2549,7 @@ int sample_has_dups(const int* c1, uint64_t n, uint32_t* dflag, hipStream_t st, 
 }
 
 int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
-                  uint32_t* general, hipStream_t st, const DevState* s, bool keep = false) {
+                  uint32_t* general, hipStream_t st, const DevState* s, bool keep = false, int* pmm = nullptr) {
     const Win t = j->win;
     j->marks = n >= kWindowBuildRows && !getenv("MQ_JOIN_NOMARKS");
     if (n < kWindowBuildRows) {
@@ -2469,11 +2600,11 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
         if (rc) return done(rc);
         if (pass == 0) {
             hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
-                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst);
+                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst, keep ? pmm : nullptr);
         } else {
             hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st,
                                (const int*)nullptr, (const int*)nullptr, src, n, t, shift, hscan,
-                               (uint32_t)ntiles, dst);
+                               (uint32_t)ntiles, dst, (int*)nullptr);
         }
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window partition"));
         src = dst;
@@ -2848,16 +2979,14 @@ int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, i
 
 namespace {
 
-// The partitioned unique probe (k_pwin_scatter / k_win_join / k_pwin_gather above):
-// per probe row its payload (pstart) and per 64 rows the hit word, as k_ht_probe_unique
-// leaves them. Temporaries are freed stream-ordered.
-int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
+template <typename RT, bool RUNS = false>
+int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
     const Win t = j->win;
     const int passes = j->passes;
     const uint64_t ntiles = ceil_div(n2, kSortTile), nh = ntiles * kRadix;
     uint32_t* K[4] = {reinterpret_cast<uint32_t*>(const_cast<int32_t*>(d_c2)), nullptr, nullptr, nullptr};
     u64* hs[3] = {nullptr, nullptr, nullptr};
-    u64* R[2] = {nullptr, nullptr};
+    RT* R[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr, *pws = nullptr;
     u64* scratch = nullptr;
     auto done = [&](int rc) {
@@ -2873,7 +3002,7 @@ int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* ps
     bool ok = true;
     for (int p = 1; p <= passes; p++) ok = ok && (K[p] = (uint32_t*)pool_alloc(n2 * 4));
     for (int p = 0; p < passes; p++) ok = ok && (hs[p] = (u64*)pool_alloc(nh * 8));
-    ok = ok && (R[0] = (u64*)pool_alloc(n2 * 8)) && (passes < 2 || (R[1] = (u64*)pool_alloc(n2 * 8))) &&
+    ok = ok && (R[0] = (RT*)pool_alloc(n2 * sizeof(RT))) && (passes < 2 || (R[1] = (RT*)pool_alloc(n2 * sizeof(RT)))) &&
          (hist = (uint32_t*)pool_alloc(nh * 4)) && (pws = (uint32_t*)pool_alloc(((uint64_t)j->nwin + 1) * 4)) &&
          (scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8));
     if (!ok) return done(set_err(MQ_ENOMEM, "join: partitioned probe buffers (%llu rows)", (unsigned long long)n2));
@@ -2891,21 +3020,47 @@ int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* ps
     DevState* s;
     if (int rc0 = ensure_ready(&s)) return done(rc0);
     const uint32_t gj = j->nwin < (uint32_t)s->cus * 2 ? j->nwin : (uint32_t)s->cus * 2;
-    hipLaunchKernelGGL(k_win_join, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws, j->nwin,
-                       t, R[0], j->pflag);
+    if constexpr (RUNS)
+        hipLaunchKernelGGL(k_win_probe_tab, dim3(gj), dim3(kWinTPB), 0, st, (const u64*)j->words, K[passes], pws,
+                           j->nwin, t, reinterpret_cast<uint32_t*>(R[0]));
+    else
+        hipLaunchKernelGGL(k_win_join<RT>, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws,
+                           j->nwin, t, R[0], j->pflag, j->sentinel);
     if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window join"));
     int cur = 0;
     for (int p = passes - 1; p >= 0; p--) {
         if (p == 0)
-            hipLaunchKernelGGL(k_pwin_gather<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t, 0, hs[0],
-                               (uint32_t)ntiles, R[cur], (u64*)nullptr, pstart, hits);
+            hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t,
+                               0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)nullptr, pstart, hits, j->sentinel);
         else
-            hipLaunchKernelGGL(k_pwin_gather<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t, 8 * p,
-                               hs[p], (uint32_t)ntiles, R[cur], R[cur ^ 1], (uint32_t*)nullptr, (u64*)nullptr);
+            hipLaunchKernelGGL((k_pwin_gather<false, RT>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t,
+                               8 * p, hs[p], (uint32_t)ntiles, (const RT*)R[cur], R[cur ^ 1], (uint32_t*)nullptr,
+                               (u64*)nullptr, j->sentinel);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe unpartition"));
         cur ^= 1;
     }
     return done(MQ_OK);
+}
+
+// The partitioned unique probe (k_pwin_scatter / k_win_join / k_pwin_gather above):
+// per probe row its payload (pstart) and per 64 rows the hit word, as k_ht_probe_unique
+// leaves them. Results move as u32 payloads with a sentinel outside the build payloads'
+// range for a miss, or (every int32 is a payload) as u64 {payload, hit}. Temporaries are
+// freed stream-ordered.
+int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
+    return j->narrow ? probe_partitioned_t<uint32_t>(j, d_c2, n2, pstart, hits, st)
+                     : probe_partitioned_t<u64>(j, d_c2, n2, pstart, hits, st);
+}
+
+// The same over a windowed runs table (j->words, built by k_win_build_runs): per row the
+// packed run (pstart) and per 64 rows the run lengths' sum (wcnt).
+int probe_partitioned_runs(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, uint32_t* wcnt,
+                           hipStream_t st) {
+    int lg = 0;
+    while ((1ull << lg) < j->mask + 1) lg++;
+    j->nwin = (uint32_t)((j->mask + 1) >> j->win.wlog);
+    j->passes = (lg - j->win.wlog + 7) / 8;
+    return probe_partitioned_t<uint32_t, true>(j, d_c2, n2, pstart, reinterpret_cast<u64*>(wcnt), st);
 }
 
 // The global table of a partitioned build, for a probe too small to pay for its own
@@ -2953,19 +3108,35 @@ int build_into(mq_join* j, const int32_t* d_c1, const int32_t* d_p1, uint64_t n1
     // the partitioned build keeps no global table: allocated only if a path needs it
     const bool part = allow_part && n1 >= kWindowBuildRows && n1 >= part_min_rows() && j->win.wlog == kWinLog;
     uint32_t* dflag = nullptr;
-    if ((!part && (rc = jalloc(j, (void**)&j->words, slots * 8))) || (rc = jalloc(j, (void**)&dflag, 16)))
+    if ((!part && (rc = jalloc(j, (void**)&j->words, slots * 8))) || (rc = jalloc(j, (void**)&dflag, 16 + 512)))
         return rc;
     j->pflag = dflag + 2;  // (dflag[1] is the sampled duplicate check's)
     j->bpos = nullptr;  // unique table carries the build positions itself
     j->unique = 1;
     if (n1) {
         HIPCHK(hipMemsetAsync(dflag, 0, 16, st));
+        int* pmm = reinterpret_cast<int*>(dflag + 4);  // the payloads' range: 64 min, 64 max slots
+        if (part) {  // (bounds at least as wide as the range: 0x7F7F7F7F / 0x80808080 start)
+            HIPCHK(hipMemsetAsync(pmm, 0x7F, 64 * 4, st));
+            HIPCHK(hipMemsetAsync(pmm + 64, 0x80, 64 * 4, st));
+        }
         bool sampled = false;
         if ((rc = sample_has_dups(d_c1, n1, dflag, st, s, &sampled))) return rc;
         uint32_t dup = sampled ? 1u : 0u;
         if (!sampled) {
-            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, part))) return rc;
-            if (part) {  // nothing to read back: the probe checks the windows
+            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, part, pmm))) return rc;
+            if (part) {  // the probe checks the windows; the payloads' range picks the result width
+                int sl[128];
+                HIPCHK(hipMemcpyAsync(sl, pmm, sizeof sl, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                int mm[2] = {INT32_MAX, INT32_MIN};
+                for (int q = 0; q < 64; q++) {
+                    mm[0] = sl[q] < mm[0] ? sl[q] : mm[0];
+                    mm[1] = sl[64 + q] > mm[1] ? sl[64 + q] : mm[1];
+                }
+                const char* nw = getenv("MQ_JOIN_NARROW");
+                j->narrow = !(nw && nw[0] == '0') && (mm[1] < INT32_MAX || mm[0] > INT32_MIN);
+                j->sentinel = (uint32_t)(mm[1] < INT32_MAX ? INT32_MAX : INT32_MIN);
                 j->part = true;
                 return MQ_OK;
             }
@@ -3110,6 +3281,9 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
                            (u64*)nullptr, j->rs, (uint32_t*)nullptr,
                            true, j->marks, cnt, j->p01);
         LAUNCHCHK("k_ht_probe_unique");
+    } else if (pruns && j->win.wlog == kWinLog && j->n1 >= part_min_rows() && n2 >= j->n1 / (pdiv ? pdiv : 1)) {
+        // packed runs, partitioned: the probe keys by window, each window's table slice in LDS
+        if ((rc = probe_partitioned_runs(j, d_c2, n2, j->pstart, cnt, st))) return rc;
     } else if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,

@@ -660,7 +660,11 @@ def _dev_join(lib, c1, p1, c2, p2):
 
 
 JOIN_PATHS = {"winruns": {}, "winruns16": {"MQ_JOIN_SLOT16": "1"}, "sorted": {"MQ_JOIN_WINRUNS": "0"},
-              "cas": {"MQ_JOIN_RUNS": "0"}}
+              "cas": {"MQ_JOIN_RUNS": "0"},
+              # the windowed runs table probed by random bucket reads / window by window in LDS
+              # (round 5: the default from 2^20 build rows, forced here from 2^16)
+              "winruns_table": {"MQ_JOIN_PART": "0"},
+              "winruns_part": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000"}}
 
 
 @pytest.mark.parametrize("path", list(JOIN_PATHS))
@@ -743,17 +747,20 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
 
 JOIN_PROBE_MODES = {"table": {"MQ_JOIN_PART": "0"},  # the global table + random bucket reads
                     "part": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000"},
+                    "part_wide": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000", "MQ_JOIN_NARROW": "0"},
                     "part_materialized": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1"}}
 
 
 @pytest.mark.parametrize("mode", list(JOIN_PROBE_MODES))
 @pytest.mark.parametrize("case", ["n2_1", "n2_63", "n2_65", "n2_4097", "all_miss", "all_hit_dup_probe",
                                   "negative_extremes", "one_pass", "two_passes", "marker", "dup_probed",
-                                  "dup_unprobed", "overfull_window"])
+                                  "dup_unprobed", "overfull_window", "payload_extremes"])
 def test_hash_join_partitioned_probe(lib, refcpu, monkeypatch, mode, case):
     """Unique builds (round 5): the probe keys partitioned by table window like the build
     rows, each window joined in LDS (k_win_join), the results taken back to probe order
-    by the inverted passes (k_pwin_gather); "part_materialized" makes the probe side too
+    by the inverted passes (k_pwin_gather), as u32 payloads with a miss marker outside the
+    payloads' range ("part_wide": MQ_JOIN_NARROW=0, u64 {payload, hit}, also what a build
+    whose payloads hold both INT32 extremes takes); "part_materialized" makes the probe side too
     small for that (MQ_JOIN_PART_DIV), so the checked windows are stored as the global
     table first; "table" is the random-read probe. One LSD pass (build < 2^20 rows: at
     most 256 windows) and two (2^21 build rows: 512 windows, a second digit); a build row
@@ -804,6 +811,10 @@ def test_hash_join_partitioned_probe(lib, refcpu, monkeypatch, mode, case):
     p2 = rng.integers(0, 10 ** 7, len(c2), dtype=np.int32)
     if case == "marker":
         p1[np.nonzero(c1 == -1)[0][0]] = -1
+    if case == "payload_extremes":  # no int32 is free to mark a miss: the u64 results
+        p1[:2] = [-2 ** 31, 2 ** 31 - 1]
+    if case == "two_passes":  # a payload of INT32_MAX: the miss marker becomes INT32_MIN
+        p1[3] = 2 ** 31 - 1
     g1, g2 = _dev_join(lib, c1, p1, c2, p2)
     w1, w2 = refcpu.hash_join(c1, p1, c2, p2)
     assert np.array_equal(g1, w1) and np.array_equal(g2, w2), (case, mode)
