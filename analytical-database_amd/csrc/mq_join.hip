@@ -1139,10 +1139,17 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
 // follows the table's own probe sequence there (home bucket, linear inside the window,
 // an empty slot ends it). r[i] = the slot's packed run, 0 = no match (a run is never
 // empty, so a hit's payload is never 0).
+// RT = u64 (run2): a run of one or two rows carries its build positions (read from the
+// run array, whose window slice stays in the XCD's L2 while the block works on it), so
+// the write streams instead of fetching a random run line per row: {p0, p1} with p1 =
+// S (the sentinel, outside the payloads) for one row, {S, packed} for a longer run,
+// {S, 0} for a miss.
+template <typename RT>
 __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict__ words,
                                                            const uint32_t* __restrict__ pkeys,
                                                            const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
-                                                           uint32_t* __restrict__ r) {
+                                                           RT* __restrict__ r, const int* __restrict__ bpos,
+                                                           uint32_t S) {
     __shared__ u64 tab[1 << kWinLog];
     const uint32_t W = (uint32_t)t.wmask + 1, G = gridDim.x;
     uint32_t w = blockIdx.x;
@@ -1154,15 +1161,26 @@ __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict
             key[k] = i < pe ? __builtin_nontemporal_load(pkeys + i) : 0u;
         }
     };
-    auto lookup = [&](uint32_t key) -> uint32_t {
+    auto lookup = [&](uint32_t key) -> RT {
         uint32_t h = (uint32_t)ht_home(key, t.wmask);
+        uint32_t pk = 0;
         for (uint32_t step = 0; step < W; step++) {
             const u64 v = tab[h];
-            if (v == kEmpty) return 0u;
-            if ((uint32_t)v == key) return (uint32_t)(v >> 32);
+            if (v == kEmpty) break;
+            if ((uint32_t)v == key) {
+                pk = (uint32_t)(v >> 32);
+                break;
+            }
             h = (h + 1) & (W - 1);
         }
-        return 0u;
+        if constexpr (sizeof(RT) == 4) {
+            return pk;
+        } else {
+            const uint32_t L = pk & 15u, a = pk >> 4;
+            if (L == 0u || L > 2u) return (u64)S | ((u64)pk << 32);
+            const uint32_t p0 = (uint32_t)bpos[a], p1 = L == 2u ? (uint32_t)bpos[a + 1] : S;
+            return (u64)p0 | ((u64)p1 << 32);
+        }
     };
     uint32_t pb = pstartw[w], pe = pstartw[w + 1];
     u64 vs[kWinPer];
@@ -1295,7 +1313,21 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
         const bool in = dr[k] != 0xFFFFFFFFu;
         const RT v = in ? stage[sp[k]] : (RT)0;
-        if constexpr (FINAL && RUNS) {
+        if constexpr (FINAL && RUNS && sizeof(RT) == 8) {
+            // run2 records: pstart = a packed run (long) or just its length (one or two rows,
+            // whose positions go to rout = p01), as k_join_write_runs16 reads them
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)((u64)v >> 32);
+            const bool direct = lo != sentinel;
+            const uint32_t pk = !in ? 0u : direct ? (hi == sentinel ? 1u : 2u) : hi;
+            uint32_t L = pk & 15u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) L += __shfl_xor(L, o, 64);
+            if (i < n) {
+                __builtin_nontemporal_store(pk, pstart + i);
+                __builtin_nontemporal_store((in && direct) ? (u64)v : 0ull, reinterpret_cast<u64*>(rout) + i);
+            }
+            if (lane == 0 && i < n) reinterpret_cast<uint32_t*>(hits)[i >> 6] = L;
+        } else if constexpr (FINAL && RUNS) {
             const uint32_t pay = (uint32_t)v;
             uint32_t L = pay & 15u;  // (a windowed runs table: every run shorter than 15)
 #pragma unroll
@@ -2432,6 +2464,9 @@ struct mq_join {
     const int32_t* p1;     // that meets a duplicate key or an overfull window is rebuilt
     uint32_t* pflag;       // the window join's flag (a duplicate met, a window overfull)
     bool narrow;           // the window join's results as u32 payloads, `sentinel` = a miss
+    bool run2;             // the last probe left short runs' positions in p01 (k_join_write_runs16)
+    bool rsent_ok;         // windowed runs: `sentinel` is outside the payloads (the partitioned
+                           // runs probe then carries short runs' positions, run2)
     uint32_t sentinel;     // (a value outside the build payloads' range)
     u64* pwords;
     uint32_t* pwstart;
@@ -2639,7 +2674,7 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
 // (j->unique = 2, packed payloads, j->bpos the runs), 1 when it does not apply or a
 // window flagged (the caller takes the sorted-runs build), or an error.
 int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots, uint32_t* general,
-                      hipStream_t st, const DevState* s) {
+                      hipStream_t st, const DevState* s, int* pmm = nullptr) {
     (void)s;
     const char* e = getenv("MQ_JOIN_WINRUNS");  // "0": the sorted-runs build (A/B, tests)
     const char* r = getenv("MQ_JOIN_RUNS");     // "0": the global-CAS run table (tests)
@@ -2702,10 +2737,10 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
         if ((rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st))) return drop(rc);
         if (pass == 0)
             hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
-                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst);
+                               (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst, pmm);
         else
             hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr,
-                               (const int*)nullptr, src, n, t, shift, hscan, (uint32_t)ntiles, dst);
+                               (const int*)nullptr, src, n, t, shift, hscan, (uint32_t)ntiles, dst, (int*)nullptr);
         if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window partition"));
         src = dst;
         dst = (dst == a) ? b : a;
@@ -2718,10 +2753,22 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     else
         hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
     if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window runs build"));
+    int sl[128];
     if (hipMemcpyAsync(&flag, general, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (pmm && hipMemcpyAsync(sl, pmm, sizeof sl, hipMemcpyDeviceToHost, st) != hipSuccess) ||
         hipStreamSynchronize(st) != hipSuccess)
         return drop(set_err(MQ_EHIP, "join: window runs sync"));
     if (flag) return drop(1);
+    if (pmm) {  // a value outside the payloads' range: the partitioned probe's marker (rsent)
+        int mn = INT32_MAX, mx = INT32_MIN;
+        for (int q = 0; q < 64; q++) {
+            mn = sl[q] < mn ? sl[q] : mn;
+            mx = sl[64 + q] > mx ? sl[64 + q] : mx;
+        }
+        const char* nw = getenv("MQ_JOIN_NARROW");
+        j->rsent_ok = !(nw && nw[0] == '0') && (mx < INT32_MAX || mn > INT32_MIN);
+        j->sentinel = (uint32_t)(mx < INT32_MAX ? INT32_MAX : INT32_MIN);
+    }
     int* const bpos = bp;
     bp = nullptr;  // (jown frees it itself when it fails)
     if ((rc = jown(j, bpos))) return drop(rc);
@@ -3021,8 +3068,8 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     if (int rc0 = ensure_ready(&s)) return done(rc0);
     const uint32_t gj = j->nwin < (uint32_t)s->cus * 2 ? j->nwin : (uint32_t)s->cus * 2;
     if constexpr (RUNS)
-        hipLaunchKernelGGL(k_win_probe_tab, dim3(gj), dim3(kWinTPB), 0, st, (const u64*)j->words, K[passes], pws,
-                           j->nwin, t, reinterpret_cast<uint32_t*>(R[0]));
+        hipLaunchKernelGGL(k_win_probe_tab<RT>, dim3(gj), dim3(kWinTPB), 0, st, (const u64*)j->words, K[passes], pws,
+                           j->nwin, t, R[0], j->bpos, j->sentinel);
     else
         hipLaunchKernelGGL(k_win_join<RT>, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws,
                            j->nwin, t, R[0], j->pflag, j->sentinel);
@@ -3031,7 +3078,8 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     for (int p = passes - 1; p >= 0; p--) {
         if (p == 0)
             hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t,
-                               0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)nullptr, pstart, hits, j->sentinel);
+                               0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)(RUNS ? (void*)j->p01 : nullptr),
+                               pstart, hits, j->sentinel);
         else
             hipLaunchKernelGGL((k_pwin_gather<false, RT>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t,
                                8 * p, hs[p], (uint32_t)ntiles, (const RT*)R[cur], R[cur ^ 1], (uint32_t*)nullptr,
@@ -3060,6 +3108,8 @@ int probe_partitioned_runs(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_
     while ((1ull << lg) < j->mask + 1) lg++;
     j->nwin = (uint32_t)((j->mask + 1) >> j->win.wlog);
     j->passes = (lg - j->win.wlog + 7) / 8;
+    if (j->p01)  // run2: the short runs' positions ride along (j->p01, n2 u64)
+        return probe_partitioned_t<u64, true>(j, d_c2, n2, pstart, reinterpret_cast<u64*>(wcnt), st);
     return probe_partitioned_t<uint32_t, true>(j, d_c2, n2, pstart, reinterpret_cast<u64*>(wcnt), st);
 }
 
@@ -3144,7 +3194,11 @@ int build_into(mq_join* j, const int32_t* d_c1, const int32_t* d_p1, uint64_t n1
             HIPCHK(hipStreamSynchronize(st));
         }
         if (part && (rc = jalloc(j, (void**)&j->words, slots * 8))) return rc;  // (sampled duplicates)
-        if (dup && (rc = build_window_runs(j, d_c1, d_p1, n1, slots, dflag, st, s)) != 1)
+        if (dup) {  // the payloads' range for the runs probe's marker (the unique attempt's, if any, is spent)
+            HIPCHK(hipMemsetAsync(pmm, 0x7F, 64 * 4, st));
+            HIPCHK(hipMemsetAsync(pmm + 64, 0x80, 64 * 4, st));
+        }
+        if (dup && (rc = build_window_runs(j, d_c1, d_p1, n1, slots, dflag, st, s, pmm)) != 1)
             return rc;  // 0: the windowed runs build took it
         if (dup) {  // general path: stable sort by key, runs in insertion order
             j->unique = 0;
@@ -3261,6 +3315,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     // (u32 lengths, u64 offsets).
     const bool pruns = j->unique == 2 && j->packed && j->rs == nullptr;
     j->pruns = pruns;
+    j->run2 = false;
     const bool words_scan = j->unique == 1 || pruns;  // per 64-row word; else per row
     j->pstart = (uint32_t*)pool_alloc(n2 * 4);
     j->plen = (uint32_t*)pool_alloc(j->unique == 1 ? nwords * 12 : pruns ? nwords * 4 : n2 * 4);
@@ -3282,7 +3337,10 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
                            true, j->marks, cnt, j->p01);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (pruns && j->win.wlog == kWinLog && j->n1 >= part_min_rows() && n2 >= j->n1 / (pdiv ? pdiv : 1)) {
-        // packed runs, partitioned: the probe keys by window, each window's table slice in LDS
+        // packed runs, partitioned: the probe keys by window, each window's table slice in LDS;
+        // with a marker outside the payloads the short runs' positions ride along (run2)
+        j->run2 = j->rsent_ok && !(getenv("MQ_JOIN_RUN2") && getenv("MQ_JOIN_RUN2")[0] == '0');
+        if (j->run2 && !(j->p01 = (u64*)pool_alloc(n2 * 8))) return set_err(MQ_ENOMEM, "mq_join_probe: positions");
         if ((rc = probe_partitioned_runs(j, d_c2, n2, j->pstart, cnt, st))) return rc;
     } else if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
@@ -3354,7 +3412,7 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         LAUNCHCHK("k_join_write_hits");
         return MQ_OK;
     }
-    if (j->pruns && j->slot16) {
+    if (j->pruns && (j->slot16 || j->run2)) {
         hipLaunchKernelGGL(k_join_write_runs16<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)), dim3(kTPB), 0,
                            (hipStream_t)stream, j->pstart, j->n2, j->offs, d_p2, j->p01, j->bpos, d_out1, d_out2);
         LAUNCHCHK("k_join_write_runs16");

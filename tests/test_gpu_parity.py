@@ -664,7 +664,11 @@ JOIN_PATHS = {"winruns": {}, "winruns16": {"MQ_JOIN_SLOT16": "1"}, "sorted": {"M
               # the windowed runs table probed by random bucket reads / window by window in LDS
               # (round 5: the default from 2^20 build rows, forced here from 2^16)
               "winruns_table": {"MQ_JOIN_PART": "0"},
-              "winruns_part": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000"}}
+              "winruns_part": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000"},
+              # ... with the short runs' build positions carried to the write (run2, the
+              # default) or only the packed runs (MQ_JOIN_RUN2=0: the write reads the runs)
+              "winruns_part_packed": {"MQ_JOIN_PART_MIN": "65536", "MQ_JOIN_PART_DIV": "1000000",
+                                      "MQ_JOIN_RUN2": "0"}}
 
 
 @pytest.mark.parametrize("path", list(JOIN_PATHS))
