@@ -1031,7 +1031,7 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     }
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i = flushed + (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i % (uint32_t)BUF];
-    if (sw >= E) return;
+    if (sw >= E || xmode == 2) return;  // (xmode 2, diagnostic: no bitmap expansion at all)
     // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
     unsigned long long o = D + fill;
     const uint64_t T1 = (E + 255) >> 8;
@@ -1079,6 +1079,11 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
         const unsigned int tot = __shfl(incl, 63, 64);
         const unsigned long long ol = o + (incl - c);
         const uint64_t row0 = T * 256;
+        if (xmode == 3) {  // diagnostic: the bitmap words read and counted, nothing placed
+            o += tot;
+            if (PAYLOAD && __builtin_amdgcn_readfirstlane((int)tot) == -1) out[o] = payload[row0];
+            continue;
+        }
         if (xmode == 1) {
             // batched (round 4, the default): tiles' outputs gathered in row order in
             // the wave's LDS ring (free now: its entries went out above), placed so that
@@ -1931,8 +1936,10 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     // 1.355 / 1.56 ms against 1.064 / 1.475 / 1.84 ms at 10 / 50 / 100 % alternating on
     // one box (profiles/r04_positions_batched_ab.log; a first staged form that flushed
     // every tile lost to the lanes, profiles/r04_positions_ab.log)
+    // (MQ_STAGE_EXPAND=2 / 3: diagnostics only, the output is incomplete: no bitmap
+    // expansion / the bitmap read and counted but nothing placed)
     const char* xe = getenv("MQ_STAGE_EXPAND");
-    const int xmode = xe && xe[0] == '0' ? 0 : 1;
+    const int xmode = xe && xe[0] == '0' ? 0 : xe && xe[0] == '2' ? 2 : xe && xe[0] == '3' ? 3 : 1;
     if (payload) {
         if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
         else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
