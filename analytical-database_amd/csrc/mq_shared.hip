@@ -761,7 +761,13 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <bool PF>
+// P16 (round 5): the list as 16-bit entries, half the bytes of the u32 pairs (the pair
+// stores inside the column read cost the pass far more than their share of its bytes,
+// tools/mix_probe): a pair is query << 7 | the row within its 128-row tile; a token
+// 0x8000 | d, written ahead of a queued row whose tile is d tiles past the previous
+// queued row's (from tile 0 at the wave-chunk's start), gives the tile. cap counts
+// entries. Wave-chunks of at most 2^22 rows (d < 2^15; the host checks).
+template <bool PF, bool P16>
 __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
@@ -799,14 +805,18 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
     const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
+    constexpr uint32_t kEb = P16 ? 2u : 4u;  // bytes per list entry
     uint32_t* list = pairs + wc * cap;
+    uint16_t* list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
     uint32_t* pb = s_pb[wave];
     int32_t* qv = s_qv[wave];
     uint16_t* qe = s_qe[wave];
     uint32_t* qr = s_qr[wave];
-    uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0;
+    uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0, last_tile = 0;
     bool direct = false;
-    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t lrs =
+        __builtin_amdgcn_make_buffer_rsrc(P16 ? (void*)list16 : (void*)list, 0, (int)(cap * kEb), 0x00020000);
+    auto enc = [&](uint32_t qid, uint32_t r) { return P16 ? (qid << 7) | (r & 127u) : (qid << 24) | r; };
     auto round = [&](uint32_t nr) {
         const bool has = (uint32_t)lane < nr;
         uint32_t qa = 0, qn = 0, r = 0;
@@ -840,22 +850,33 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             if (qn) atomicAdd(&hist[wave][ei], 1u);
         }
         head += nr;
+        // P16: a token ahead of a row in another tile than the queued row before it
+        uint32_t tok = 0, delta = 0;
+        if (P16) {
+            const uint32_t tr = r >> 7;
+            uint32_t prev = (uint32_t)__shfl_up((int)tr, 1, 64);
+            if (lane == 0) prev = last_tile;
+            tok = has && tr != prev ? 1u : 0u;
+            delta = tr - prev;
+            last_tile = (uint32_t)__builtin_amdgcn_readlane((int)tr, (int)nr - 1);
+        }
+        const uint32_t ne = qn + tok;  // entries this row writes
         uint32_t pre = 0, tot = 0;
-        const bool single = !__ballot(qn > 1u);
-        if (single) {  // the usual case: at most one query per row
-            const unsigned long long bm = __ballot(qn != 0u);
+        const bool single = !__ballot(ne > 1u);
+        if (single) {  // the usual case: at most one entry per row
+            const unsigned long long bm = __ballot(ne != 0u);
             pre = mbcnt64(bm);
             tot = (uint32_t)__popcll(bm);
-        } else if (!__ballot(qn >= 8u)) {
+        } else if (!__ballot(ne >= 8u)) {
 #pragma unroll
             for (int bit = 0; bit < 3; bit++) {
-                const unsigned long long bm = __ballot((qn >> bit) & 1u);
+                const unsigned long long bm = __ballot((ne >> bit) & 1u);
                 pre += mbcnt64(bm) << bit;
                 tot += (uint32_t)__popcll(bm) << bit;
             }
         } else {
             for (uint32_t t = 1;; t++) {
-                const unsigned long long bm = __ballot(qn >= t);
+                const unsigned long long bm = __ballot(ne >= t);
                 if (!bm) break;
                 pre += mbcnt64(bm);
                 tot += (uint32_t)__popcll(bm);
@@ -872,14 +893,16 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             // pointers and stores through flat)
             auto put = [&](uint32_t i, uint32_t y) {
                 if (!direct) pb[fill + pre + i] = y;
+                else if (P16) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)y, lrs, (int)((run + pre + i) * 2u), 0, 0);
                 else __builtin_amdgcn_raw_buffer_store_b32(y, lrs, (int)((run + pre + i) * 4u), 0, 0);
             };
+            if (P16 && tok) put(0, 0x8000u | delta);
             if (single && ql_lds) {
-                if (qn) put(0, ((uint32_t)s_ql[qa] << 24) | r);
+                if (qn) put(0, enc(s_ql[qa], r));
             } else if (ql_lds) {
-                for (uint32_t i = 0; i < qn; i++) put(i, ((uint32_t)s_ql[qa + i] << 24) | r);
+                for (uint32_t i = 0; i < qn; i++) put(tok + i, enc(s_ql[qa + i], r));
             } else {
-                for (uint32_t i = 0; i < qn; i++) put(i, ((uint32_t)T.qlist[qa + i] << 24) | r);
+                for (uint32_t i = 0; i < qn; i++) put(tok + i, enc(T.qlist[qa + i], r));
             }
             if (!direct) fill += tot;
         }
@@ -939,8 +962,9 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
 #pragma unroll
             for (int k = 0; k < (int)(kPb / 64); k++) {
                 const uint32_t i = (uint32_t)(k * 64 + lane);
-                __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, i < pend ? (int)((pend_at + i) * 4u) : (int)0x80000000u,
-                                                      0, 0);
+                const int off = i < pend ? (int)((pend_at + i) * kEb) : (int)0x80000000u;
+                if (P16) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb[i], lrs, off, 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, off, 0, 0);
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -987,7 +1011,10 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         }
     }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
+    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) {
+        if (P16) list16[pend_at + i] = (uint16_t)pb[i];
+        else list[pend_at + i] = pb[i];
+    }
     __builtin_amdgcn_wave_barrier();
     fill = 0;
     direct = true;
@@ -1046,7 +1073,13 @@ constexpr int kSpPer = kSpChunk / kTPB;         // entries each thread places
 // at Q = 150 on 1e9 rows; 8192-pair chunks (2 waves per SIMD) took 0.77 ms.
 // `pairs` is clobbered: the padding stores of a chunk land on pairs of that chunk
 // already read (hence not const, not __restrict__).
-__global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
+// P16: the 16-bit list of k_ssk_count<*, true> (cap in entries). A round's tokens give
+// each lane's tile by a wave scan of their deltas from the wave's running tile; the pair
+// goes to LDS as the u32 form with its row relative to the wave's part of the chunk,
+// and the part's first tile (the chunk's, plus the deltas of the waves before it) is
+// added when the pairs are placed. Tokens take a list slot but no output slot.
+template <bool P16>
+__global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
                                                       int q, int* const* __restrict__ outs, uint64_t rpb,
@@ -1059,11 +1092,14 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
     __shared__ unsigned long long s_run[kMaxQ];
     __shared__ gint* s_out[kMaxQ];
     __shared__ uint32_t s_wsum[kWaves];
+    __shared__ uint32_t s_wt[kWaves];  // P16: tiles a wave's part of the chunk advances
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint64_t wc = blockIdx.x;
     const uint32_t np = npairs[wc];
-    uint32_t* const list = pairs + wc * cap;
+    uint32_t* const list = pairs + wc * cap;  // (the u32 form only)
+    uint16_t* const list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
+    uint32_t ctile = 0;  // P16: the tile at the chunk's first entry
     const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
     for (int i = tid; i < q; i += kTPB) {
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
@@ -1077,7 +1113,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
 #pragma unroll
         for (int r = 0; r < kSpRounds; r++) {
             const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
-            nx[r] = idx < np ? list[idx] : 0u;
+            nx[r] = idx < np ? (P16 ? (uint32_t)list16[idx] : list[idx]) : 0u;
         }
     };
     load_chunk(0);
@@ -1089,6 +1125,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
         for (int i = tid; i < kWaves * kMaxQ; i += kTPB) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
         // this wave's 1024 pairs of the chunk
+        uint32_t wt = 0;  // P16: tiles advanced so far in this wave's part
 #pragma unroll
         for (int r0 = 0; r0 < kSpRounds; r0 += kSpBatch) {
             uint32_t x[kSpBatch];
@@ -1097,11 +1134,25 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
 #pragma unroll
             for (int b = 0; b < kSpBatch; b++) {
                 const uint32_t li = (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
-                const bool valid = c0 + li < np;
-                const uint32_t qid = x[b] >> 24;
+                bool valid = c0 + li < np;
+                uint32_t qid = x[b] >> 24, y = x[b];
+                if (P16) {
+                    const bool tk = valid && (x[b] & 0x8000u);
+                    uint32_t inc = tk ? (x[b] & 0x7FFFu) : 0u;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+                        if (lane >= o) inc += t;
+                    }
+                    const uint32_t tile = wt + inc;
+                    wt += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+                    valid = valid && !tk;
+                    qid = (x[b] >> 7) & 0xFFu;
+                    y = valid ? (qid << 24) | (tile * 128u + (x[b] & 127u)) : 0xFFFFFFFFu;
+                }
                 const unsigned long long peers = match_any8(qid, __ballot(valid));
                 const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
-                s_buf[li] = x[b];
+                s_buf[li] = y;
                 s_loc[li] = (uint16_t)(before + lanes_below(peers));
                 __builtin_amdgcn_wave_barrier();
                 if (valid && (peers & ~ltmask & ~(1ull << lane)) == 0)
@@ -1109,6 +1160,7 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
                 __builtin_amdgcn_wave_barrier();
             }
         }
+        if (P16 && lane == 0) s_wt[wave] = wt;
         __syncthreads();
         // bucket starts: queries in order, waves in order inside a query
         uint32_t tq = 0;
@@ -1139,12 +1191,28 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
         }
         __syncthreads();
         const uint32_t cn = np - c0 < (uint32_t)kSpChunk ? np - c0 : (uint32_t)kSpChunk;
+        // the chunk's pairs (P16: its entries less the tokens)
+        uint32_t cnv = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) cnv += s_wsum[w];
+        uint32_t wrow[kWaves];  // P16: the first row of each wave's part
+        {
+            uint32_t a = ctile;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) {
+                wrow[w] = a * 128u;
+                if (P16) a += s_wt[w];
+            }
+            ctile = a;
+        }
         uint32_t px[kSpPer], pd[kSpPer];
 #pragma unroll
         for (int k = 0; k < kSpPer; k++) {
             const uint32_t i = (uint32_t)(k * kTPB + tid);
             px[k] = s_buf[i];
-            pd[k] = i < cn ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
+            const bool pair = i < cn && (!P16 || px[k] != 0xFFFFFFFFu);
+            pd[k] = pair ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
+            if (P16 && pair) px[k] += wrow[i / kSpPerWave];
         }
         __syncthreads();
 #pragma unroll
@@ -1155,11 +1223,12 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
         // pair of this chunk already read (the slice is not read again): with a
         // data-dependent count the wait for the next chunk's loads at the loop's top was
         // vmcnt(0), i.e. also for every store of this chunk
-        gint* const dummy = (gint*)(list + c0);
+        // (P16: `list` is not this slice's start, cap counting 16-bit entries)
+        gint* const dummy = P16 ? (gint*)(list16 + c0) : (gint*)(list + c0);
 #pragma unroll
         for (int k = 0; k < kSpPer; k++) {
             const uint32_t i = (uint32_t)(k * kTPB + tid);
-            const bool in = i < cn;
+            const bool in = i < cnv;
             const uint32_t y = s_buf[i], qid = in ? y >> 24 : 0u;
             gint* const dst = in ? s_out[qid] + (s_run[qid] + (i - s_start[qid])) : dummy;
             *dst = (int)(row0 + (y & 0xFFFFFFu)) + base;
@@ -1172,13 +1241,72 @@ __global__ __launch_bounds__(kTPB) void k_ssp_scatter(uint32_t* pairs, uint64_t 
 // totals[j] = offs[j*nwc + nwc-1] + counts[j*nwc + nwc-1] - offs[j*nwc]
 __global__ void k_ss_totals(const uint32_t* __restrict__ counts,
                             const unsigned long long* __restrict__ offs, uint64_t nwc, int q,
-                            const int* __restrict__ slot, uint64_t* __restrict__ totals, int qall) {
+                            const int* __restrict__ slot, uint64_t* __restrict__ totals, int qall,
+                            const unsigned int* __restrict__ flag, uint64_t* __restrict__ flag_out) {
+    if (flag_out && threadIdx.x == 0) *flag_out = *flag;  // the pair slices' overflow word
     for (int i = threadIdx.x; i < qall; i += blockDim.x) {
         const int j = slot[i];
         totals[i] = j < 0 ? 0ull
                           : offs[(uint64_t)j * nwc + nwc - 1] + counts[(uint64_t)j * nwc + nwc - 1] -
                                 offs[(uint64_t)j * nwc];
     }
+}
+
+// The count pass's offsets and totals in one launch (round 5; was a 3-kernel flat scan
+// plus k_ss_totals, ≈ 21 µs): block j scans kernel query j's nwc wave-chunk counts into
+// offsets that start at 0 (every reader subtracts the query's first offset), and writes
+// the total of each query i with slot[i] == j; block 0 also writes the zero totals of
+// the empty queries and, with flag_out, copies the overflow word.
+constexpr int kOffTPB = 1024, kOffPer = 8;
+__global__ __launch_bounds__(kOffTPB) void k_ss_offsets(const uint32_t* __restrict__ counts,
+                                                       unsigned long long* __restrict__ offs, uint64_t nwc,
+                                                       const int* __restrict__ slot, uint64_t* __restrict__ totals,
+                                                       int qall, const unsigned int* __restrict__ flag,
+                                                       uint64_t* __restrict__ flag_out) {
+    __shared__ unsigned long long s_w[kOffTPB / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t j = blockIdx.x;
+    const uint32_t* c = counts + j * nwc;
+    unsigned long long* o = offs + j * nwc;
+    unsigned long long carry = 0;
+    for (uint64_t b0 = 0; b0 < nwc; b0 += (uint64_t)kOffTPB * kOffPer) {
+        const uint64_t i0 = b0 + (uint64_t)tid * kOffPer;
+        uint32_t x[kOffPer];
+#pragma unroll
+        for (int k = 0; k < kOffPer; k++) x[k] = i0 + k < nwc ? c[i0 + k] : 0u;
+        unsigned long long t = 0;
+#pragma unroll
+        for (int k = 0; k < kOffPer; k++) t += x[k];
+        unsigned long long incl = t;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_w[wave] = incl;
+        __syncthreads();
+        unsigned long long before = carry, all = 0;
+#pragma unroll
+        for (int w = 0; w < kOffTPB / 64; w++) {
+            const unsigned long long v = s_w[w];
+            if (w < wave) before += v;
+            all += v;
+        }
+        unsigned long long run = before + incl - t;
+#pragma unroll
+        for (int k = 0; k < kOffPer; k++) {
+            if (i0 + k < nwc) o[i0 + k] = run;
+            run += x[k];
+        }
+        carry += all;
+        __syncthreads();  // s_w is rewritten by the next segment
+    }
+    for (int i = tid; i < qall; i += kOffTPB) {
+        const int sj = slot[i];
+        if (sj == (int)j) totals[i] = carry;
+        else if (sj < 0 && j == 0) totals[i] = 0ull;
+    }
+    if (flag_out && j == 0 && tid == 0) *flag_out = *flag;
 }
 
 struct SsLayout {
@@ -1196,15 +1324,16 @@ SsLayout ss_layout(uint64_t nwc, int q) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     SsLayout L;
     size_t at = 0;
-    // preds, slot, the EI tables and the flag word are one host upload (ss_count)
+    // preds, slot, the flag word and the EI tables are one host upload (ss_count), up to
+    // the last query-list entry in use (the EI tables end with the lists)
     L.preds = at;
     at += al((size_t)kMaxQ * sizeof(Pred));
     L.slot = at;
     at += al((size_t)kMaxQ * sizeof(int));
-    L.ei = at;
-    at += al(kEiBytes);
     L.flag = at;
     at += 256;
+    L.ei = at;
+    at += al(kEiBytes);
     L.outs = at;
     at += al((size_t)kMaxQ * sizeof(int*));
     L.counts = at;
@@ -1230,7 +1359,7 @@ struct Staging {
     hipEvent_t ev = nullptr;
 };
 Staging& staging_slot(int dev, int which) {
-    static thread_local Staging st[kMaxDev][2];
+    static thread_local Staging st[kMaxDev][3];  // count upload, write upload, count download
     return st[dev][which];
 }
 }  // namespace
@@ -1241,7 +1370,7 @@ void shared_staging_release() {
     int cur = 0;
     const bool have_cur = hipGetDevice(&cur) == hipSuccess;
     for (int d = 0; d < kMaxDev; d++)
-        for (int w = 0; w < 2; w++) {
+        for (int w = 0; w < 3; w++) {
             Staging& S = staging_slot(d, w);
             if (!S.p && !S.ev) continue;
             if (hipSetDevice(d) != hipSuccess) continue;
@@ -1307,12 +1436,17 @@ struct SsState {
     EiMeta meta;
     int32_t base;  // first row number of this (row-shard) column
     bool pairs;    // the count pass listed the pairs (single pass)
+    bool p16;      // ... as 16-bit entries (k_ssk_count<*, true>)
+    bool flag_known;  // the host read the overflow word after the count (flag)
+    unsigned int flag;
     int slot[kMaxQ];  // kernel index of query i, or -1
 };
 
 // Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
-// the bucket table, written to the workspace's EI region (ss_layout).
-int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
+// the bucket table, written to region (pinned staging of the workspace's EI region,
+// ss_layout); *used = the bytes in use from its start (the query lists come last, only
+// `at` entries of them).
+int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used) {
     std::vector<long long> L(qk), H(qk), b;
     b.reserve(2 * qk);
     for (int i = 0; i < qk; i++) {
@@ -1336,25 +1470,36 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
         eb[i] = eof(H[i]) + 1;
         hqab[i] = (uint32_t)ea[i] | ((uint32_t)eb[i] << 16);
     }
-    uint32_t at = 0;
-    for (int e = 0; e <= m; e++) {
-        hqoff[e] = at;
-        for (int i = 0; i < qk; i++)
-            if (ea[i] <= e && e < eb[i]) hql[at++] = (uint16_t)i;
-    }
-    hqoff[m + 1] = at;
+    // per-EI query lists, ascending query index within an EI: counts, offsets, then the
+    // queries in index order (O(q + m + entries); a scan of every (EI, query) pair cost
+    // m x q host steps a call, 45 K at Q = 150)
+    static thread_local uint32_t qfill[kEiMax];
+    std::fill(hqoff, hqoff + m + 2, 0u);
+    for (int i = 0; i < qk; i++)
+        for (int e = ea[i]; e < eb[i]; e++) hqoff[e + 1]++;
+    for (int e = 0; e <= m; e++) hqoff[e + 1] += hqoff[e];
+    const uint32_t at = hqoff[m + 1];
+    std::copy(hqoff, hqoff + m + 1, qfill);
+    for (int i = 0; i < qk; i++)
+        for (int e = ea[i]; e < eb[i]; e++) hql[qfill[e]++] = (uint16_t)i;
     const long long bmin = b[0], bmax = b[m - 1];
     int shift = 0;
     while (((bmax - bmin) >> shift) >= kBuckets) shift++;
-    for (int k = 0; k < kBuckets; k++) {
-        const long long lo = bmin + ((long long)k << shift);
-        if (lo > bmax) {
-            hbkt[k] = (uint32_t)m | ((uint32_t)m << 16);
-            continue;
+    {  // bucket k: e(its first value) | e(its last value) << 16, both monotone in k
+        int el = 0, eh = 0;
+        for (int k = 0; k < kBuckets; k++) {
+            const long long lo = bmin + ((long long)k << shift);
+            if (lo > bmax) {
+                hbkt[k] = (uint32_t)m | ((uint32_t)m << 16);
+                continue;
+            }
+            long long hi = lo + (1ll << shift) - 1;
+            if (hi > bmax) hi = bmax;
+            while (el < m && b[el] <= lo) el++;  // el = eof(lo)
+            if (eh < el) eh = el;
+            while (eh < m && b[eh] <= hi) eh++;  // eh = eof(hi)
+            hbkt[k] = (uint32_t)el | ((uint32_t)eh << 16);
         }
-        long long hi = lo + (1ll << shift) - 1;
-        if (hi > bmax) hi = bmax;
-        hbkt[k] = (uint32_t)eof(lo) | ((uint32_t)eof(hi) << 16);
     }
     // coverage bitmap: cell c (values bmin + [c, c+1) << cshift) is set when a covered
     // EI meets it; EI e (1 <= e < m) holds [b[e-1], b[e]), EI m holds [b[m-1], ...)
@@ -1417,6 +1562,7 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta) {
     o += kEiCovB;
     o += kEiCellB;  // the cell table, written above
     if (at) std::memcpy(region + o, hql, (size_t)at * 2);
+    *used = o + (size_t)at * 2;
     return MQ_OK;
 }
 
@@ -1439,9 +1585,10 @@ EiTables ei_tables(char* region) {
     return T;
 }
 
+// d_totals: q totals, and when flag_out the overflow word after them (d_totals[q])
 int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* h_lows,
              const int32_t* h_highs, int q, uint64_t* d_totals, void* d_ws, size_t ws_bytes, hipStream_t st,
-             SsState* state) {
+             SsState* state, bool flag_out = false) {
     DevState* s;
     int rc = ensure_ready(&s);
     if (rc) return rc;
@@ -1479,7 +1626,13 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     // MQ_SS_PF=0 / 1 forces it off / on (A/B)
     static const char* pfe = getenv("MQ_SS_PF");
     const bool pf = pfe ? pfe[0] != '0' : qk >= kSsPfMinQ;
-    const void* fn = kmajor ? (pf ? (const void*)&k_ssk_count<true> : (const void*)&k_ssk_count<false>)
+    // MQ_SS_P16=1: the k-major pass lists 16-bit entries (k_ssk_count<*, true>). Measured
+    // and not the default: half the list bytes, yet Q = 150 1.76 -> 1.86 ms and Q = 16
+    // 0.87 -> 0.92 (count + write, alternating on one box, profiles/r05_ss_host_ab.log)
+    const char* p16e = getenv("MQ_SS_P16");  // read per call (tests toggle it)
+    const bool p16w = kmajor && p16e && p16e[0] == '1';
+    const void* fn = kmajor ? (pf ? (p16w ? (const void*)&k_ssk_count<true, true> : (const void*)&k_ssk_count<true, false>)
+                                  : (p16w ? (const void*)&k_ssk_count<false, true> : (const void*)&k_ssk_count<false, false>))
                    : ei     ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
                             : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
     uint32_t g = 1;
@@ -1490,6 +1643,8 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     const uint64_t cap = pair_cap(rpb);
     const bool single = n && getenv("MQ_SS_TWOPASS") == nullptr &&
                         ws_bytes >= L.pairs + (size_t)nwc * cap * sizeof(uint32_t) && cap < (1ull << 24);
+    // 16-bit entries: twice as many in the same slice bytes; tile deltas < 2^15
+    const bool p16 = p16w && single && cap <= (1ull << 22);
     // preds, slot, EI tables and the zeroed flag: one upload from pinned staging
     char* up = nullptr;
     if ((rc = staging_get(0, L.outs, &up))) return rc;
@@ -1497,8 +1652,9 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     std::memcpy(up + L.slot, hslot, sizeof(int) * q);
     std::memset(up + L.flag, 0, 4);
     EiMeta meta{0, 0, 0, 0, 0, 0};
-    if (ei && (rc = ei_build(hp, qk, up + L.ei, &meta))) return rc;
-    if ((rc = staging_put(0, w, L.outs, st))) return rc;
+    size_t ei_used = 0;
+    if (ei && (rc = ei_build(hp, qk, up + L.ei, &meta, &ei_used))) return rc;
+    if ((rc = staging_put(0, w, L.ei + ei_used, st))) return rc;
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
     unsigned long long* offs = reinterpret_cast<unsigned long long*>(w + L.offs);
@@ -1518,12 +1674,19 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
                                        nwc, pr, cap, npr, of);
                 LAUNCHCHK("k_ssp_count");
             } else {
-                if (pf)
-                    hipLaunchKernelGGL(k_ssk_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                       nwc, pr, cap, npr, of);
+                const uint64_t ce = p16 ? 2 * cap : cap;  // slice capacity in entries
+                if (pf && p16)
+                    hipLaunchKernelGGL((k_ssk_count<true, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of);
+                else if (pf)
+                    hipLaunchKernelGGL((k_ssk_count<true, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of);
+                else if (p16)
+                    hipLaunchKernelGGL((k_ssk_count<false, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of);
                 else
-                    hipLaunchKernelGGL(k_ssk_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                       nwc, pr, cap, npr, of);
+                    hipLaunchKernelGGL((k_ssk_count<false, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of);
                 LAUNCHCHK("k_ssk_count");
             }
         } else if (ei) {
@@ -1546,13 +1709,16 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
             }
         }
         LAUNCHCHK("k_ss_count");
-        if ((rc = scan_u32_exclusive(counts, offs, (uint64_t)qk * nwc,
-                                     reinterpret_cast<unsigned long long*>(w + L.scratch), st)))
-            return rc;
+        hipLaunchKernelGGL(k_ss_offsets, dim3((uint32_t)qk), dim3(kOffTPB), 0, st, counts, offs, nwc,
+                           reinterpret_cast<const int*>(w + L.slot), d_totals, q,
+                           reinterpret_cast<const unsigned int*>(w + L.flag), flag_out ? d_totals + q : nullptr);
+        LAUNCHCHK("k_ss_offsets");
+    } else {  // every query empty: zero totals
+        hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
+                           reinterpret_cast<const int*>(w + L.slot), d_totals, q,
+                           reinterpret_cast<const unsigned int*>(w + L.flag), flag_out ? d_totals + q : nullptr);
+        LAUNCHCHK("k_ss_totals");
     }
-    hipLaunchKernelGGL(k_ss_totals, dim3(1), dim3(256), 0, st, counts, offs, nwc, qk,
-                       reinterpret_cast<const int*>(w + L.slot), d_totals, q);
-    LAUNCHCHK("k_ss_totals");
     state->g = g;
     state->rpb = rpb;
     state->q = q;
@@ -1563,6 +1729,9 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     state->meta = meta;
     state->base = row_base;
     state->pairs = single && qk > 0;
+    state->p16 = p16 && ei && !filt;
+    state->flag_known = false;
+    state->flag = 0;
     std::memcpy(state->slot, hslot, sizeof(int) * q);
     return MQ_OK;
 }
@@ -1583,15 +1752,25 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
     int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
     const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
-    if (S.pairs) {
-        // the pair scatter, or (a slice overflowed: the pairs are incomplete) the
-        // column pass: both launched, each checks the flag on the device
-        hipLaunchKernelGGL(k_ssp_scatter, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
-                           reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
-                           reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
-                           S.base, of);
+    // the pair scatter, or (a slice overflowed: the pairs are incomplete) the column
+    // pass: both launched, each checks the flag on the device, unless the host read the
+    // flag after the count (mq_shared_select_count), then only the one it selects
+    const bool scatter = S.pairs && !(S.flag_known && S.flag);
+    const bool column = !S.pairs || !S.flag_known || S.flag;
+    if (scatter) {
+        if (S.p16)
+            hipLaunchKernelGGL(k_ssp_scatter<true>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+                               reinterpret_cast<uint32_t*>(w + L.pairs), 2 * pair_cap(S.rpb),
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
+                               S.base, of);
+        else
+            hipLaunchKernelGGL(k_ssp_scatter<false>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+                               reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
+                               S.base, of);
         LAUNCHCHK("k_ssp_scatter");
     }
+    if (!column) return MQ_OK;
     if (S.ei) {
         const EiTables T = ei_tables(w + L.ei);
         if (aligned16(S.col))
@@ -1645,11 +1824,23 @@ int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base
     int dev;
     int rc = current_device(&dev);
     if (rc) return rc;
-    if (!d_tot[dev]) HIPCHK(hipMalloc(&d_tot[dev], kMaxQ * sizeof(uint64_t)));
+    if (!d_tot[dev]) HIPCHK(hipMalloc(&d_tot[dev], (kMaxQ + 1) * sizeof(uint64_t)));
     SsState S;
-    if ((rc = ss_count(d_col, n, row_base, h_lows, h_highs, q, d_tot[dev], d_ws, ws_bytes, st, &S))) return rc;
-    HIPCHK(hipMemcpyAsync(h_counts, d_tot[dev], sizeof(uint64_t) * q, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if ((rc = ss_count(d_col, n, row_base, h_lows, h_highs, q, d_tot[dev], d_ws, ws_bytes, st, &S, true)))
+        return rc;
+    // totals and the overflow word through pinned staging (h_counts is the caller's,
+    // often pageable: a staged copy costs more); write then launches one kernel
+    char* hp = nullptr;
+    if (q > 0) {
+        if ((rc = staging_get(2, sizeof(uint64_t) * (kMaxQ + 1), &hp))) return rc;
+        HIPCHK(hipMemcpyAsync(hp, d_tot[dev], sizeof(uint64_t) * (q + 1), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::memcpy(h_counts, hp, sizeof(uint64_t) * q);
+        uint64_t fl;
+        std::memcpy(&fl, hp + sizeof(uint64_t) * q, sizeof fl);
+        S.flag_known = true;
+        S.flag = (unsigned int)fl;
+    }
     g_last_state = S;
     g_last_ws = d_ws;
     return MQ_OK;

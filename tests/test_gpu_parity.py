@@ -968,17 +968,20 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
 # ---------------------------------------------------------------------------
 # S11 shared_select (device API): Q predicates, two passes, exact-size outputs
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("ballot", [False, True])
+@pytest.mark.parametrize("form", ["ei", "ballot", "ei_p16"])
 @pytest.mark.parametrize("twopass", [False, True])
 @pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
                                  (3_000_017, 20), (2_000_003, 2), (2_000_003, 5)])
-def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass, ballot):
+def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass, form):
     """Every Q takes the elementary-interval kernels by default (round 5: from Q = 1);
-    ballot = True forces the per-query ballot kernels (MQ_SS_IMPL=ballot)."""
+    "ballot" forces the per-query ballot kernels (MQ_SS_IMPL=ballot), "ei_p16" the
+    count pass's 16-bit pair lists (MQ_SS_P16=1, measured, not the default)."""
     if twopass:
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
-    if ballot:
+    if form == "ballot":
         monkeypatch.setenv("MQ_SS_IMPL", "ballot")
+    if form == "ei_p16":
+        monkeypatch.setenv("MQ_SS_P16", "1")
     rng = np.random.default_rng(n + q)
     d = rng.integers(-1000, 1000, n, dtype=np.int32)
     if n > 8:
@@ -1027,7 +1030,7 @@ def _shared_run(lib, d, lows, highs):
     return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
 
 
-@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass"])
+@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_p16"])
 @pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
                                   "mixed256", "narrow_domain"])
 def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
@@ -1042,6 +1045,8 @@ def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
         monkeypatch.setenv("MQ_SS_IMPL", "ballot")
     if impl.endswith("twopass"):
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
+    if impl == "ei_p16":  # the count pass's 16-bit pair lists (not the default)
+        monkeypatch.setenv("MQ_SS_P16", "1")
     rng = np.random.default_rng(hash(case) % 2 ** 32)
     n = 1_000_003
     d = rng.integers(0, 10 ** 6, n).astype(np.int32)

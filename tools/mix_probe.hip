@@ -29,7 +29,8 @@
 // group that closes the batch); AUX: the stores' cache policy bits (2 = nontemporal)
 template <int B, int AUX>
 __global__ __launch_bounds__(256) void k_mix(const int* __restrict__ col, uint64_t rpw, uint32_t npg,
-                                             uint32_t* __restrict__ pairs, uint64_t cap, int* __restrict__ sink) {
+                                             uint32_t* __restrict__ pairs, uint64_t cap, int* __restrict__ sink,
+                                             uint32_t wmask) {
     const int lane = threadIdx.x & 63;
     const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int* c = col + w * rpw;
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void k_mix(const int* __restrict__ col, uint64
             for (int k = 0; k < 4 * B; k++) {
                 const uint32_t i = (uint32_t)(k * 64 + lane);
                 __builtin_amdgcn_raw_buffer_store_b32((uint32_t)acc + i, rs,
-                                                      i < pend ? (int)((run - pend + i) * 4u) : (int)0x80000000u, 0, AUX);
+                                                      i < pend ? (int)(((run - pend + i) & wmask) * 4u) : (int)0x80000000u, 0, AUX);
             }
             pend = 0;
         }
@@ -90,8 +91,11 @@ int main() {
     CK(hipMalloc(&sink, 64));
     CK(hipMalloc(&pairs, waves * cap * 4));
     CK(hipMemset(col, 1, n * 4));
-    auto go = [&](const char* form, auto kern, uint32_t npg) {
-        const float ms = timed([&] { hipLaunchKernelGGL(kern, dim3(1024), dim3(256), 0, 0, col, rpw, npg, pairs, cap, sink); });
+    // wmask: a wave's pairs wrap within its first wmask + 1 entries (MIX_WRAP runs 1 K
+    // entries a wave = 16 MB in all, L2-sized, and 8 K = 128 MB, MALL-sized): whether the
+    // cost of a write stream inside the read stream is in HBM or before it
+    auto go = [&](const char* form, auto kern, uint32_t npg, uint32_t wmask = 0xffffffffu) {
+        const float ms = timed([&] { hipLaunchKernelGGL(kern, dim3(1024), dim3(256), 0, 0, col, rpw, npg, pairs, cap, sink, wmask); });
         const double rb = 4.0 * n, wb = 4.0 * npg * (double)(n / 1024);
         printf("{\"what\":\"mix\",\"form\":\"%s\",\"rows\":%llu,\"pairs_per_1024\":%u,\"read_gb\":%.3f,"
                "\"write_gb\":%.3f,\"ms\":%.3f,\"tbs\":%.2f}\n",
@@ -99,6 +103,13 @@ int main() {
     };
     const bool all = getenv("MIX_ALL") != nullptr;
     for (uint32_t npg : {0u, 16u, 64u, 154u, 256u}) go("per_group", k_mix<1, 0>, npg);
+    if (getenv("MIX_WRAP")) {
+        for (uint32_t npg : {16u, 154u}) {
+            go("wrap_1k", k_mix<1, 0>, npg, 1023u);
+            go("wrap_8k", k_mix<1, 0>, npg, 8191u);
+            go("wrap_1k_nt", k_mix<1, 2>, npg, 1023u);
+        }
+    }
     if (all) {
         for (uint32_t npg : {16u, 154u}) {
             go("per_group_nt", k_mix<1, 2>, npg);

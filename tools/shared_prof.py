@@ -38,4 +38,5 @@ for q in qs:
         mq.check(L.mq_shared_select_write(ws.data_ptr(), ptrs, 0))
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    print(f"q={q} ms={1e3 * min(ts):.3f} k={sum(k)}", flush=True)
+    ts.sort()
+    print(f"q={q} ms={1e3 * ts[0]:.3f} median={1e3 * ts[len(ts) // 2]:.3f} k={sum(k)}", flush=True)
