@@ -1078,12 +1078,20 @@ constexpr int kSpPer = kSpChunk / kTPB;         // entries each thread places
 // goes to LDS as the u32 form with its row relative to the wave's part of the chunk,
 // and the part's first tile (the chunk's, plus the deltas of the waves before it) is
 // added when the pairs are placed. Tokens take a list slot but no output slot.
+// Up to kArgQ output pointers by value (the kernel's argument block): a write that runs
+// only the scatter then needs no upload before it.
+constexpr int kArgQ = 32;
+struct SsArgOuts {
+    int* p[kArgQ];
+};
+
 template <bool P16>
 __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
-                                                      int q, int* const* __restrict__ outs, uint64_t rpb,
-                                                      int32_t base, const unsigned int* __restrict__ overflow) {
+                                                      int q, int* const* __restrict__ outs, SsArgOuts ao,
+                                                      bool by_arg, uint64_t rpb, int32_t base,
+                                                      const unsigned int* __restrict__ overflow) {
     if (*overflow) return;  // a slice overflowed: k_ssi_write's column pass writes
     __shared__ uint32_t s_buf[kSpChunk];
     __shared__ uint16_t s_loc[kSpChunk];
@@ -1103,7 +1111,7 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
     const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
     for (int i = tid; i < q; i += kTPB) {
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
-        s_out[i] = global_ptr(outs[i]);
+        s_out[i] = global_ptr(by_arg ? ao.p[i] : outs[i]);
     }
     // (round 4) the wave's 1024 pairs of the next chunk are loaded while this chunk is
     // ranked, sorted and written (the loads of a chunk used to open it: 9 chunks a block
@@ -1741,33 +1749,42 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     char* w = static_cast<char*>(d_ws);
     const uint64_t nwc = (uint64_t)S.g * kWaves;
     const SsLayout L = ss_layout(nwc, S.qk);
-    char* hp = nullptr;
-    int rc = staging_get(1, sizeof(int*) * kMaxQ, &hp);
-    if (rc) return rc;
-    int32_t** hout = reinterpret_cast<int32_t**>(hp);
-    for (int i = 0; i < S.q; i++)
-        if (S.slot[i] >= 0) hout[S.slot[i]] = d_pos_out[i];
-    if ((rc = staging_put(1, w + L.outs, sizeof(int*) * S.qk, st))) return rc;
-    const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
-    const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
-    int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
-    const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
     // the pair scatter, or (a slice overflowed: the pairs are incomplete) the column
     // pass: both launched, each checks the flag on the device, unless the host read the
     // flag after the count (mq_shared_select_count), then only the one it selects
     const bool scatter = S.pairs && !(S.flag_known && S.flag);
     const bool column = !S.pairs || !S.flag_known || S.flag;
+    // the output pointers: in the scatter's arguments when it runs alone on at most
+    // kArgQ queries, else uploaded to the workspace
+    SsArgOuts ao{};
+    const bool by_arg = scatter && !column && S.qk <= kArgQ;
+    int rc;
+    if (by_arg) {
+        for (int i = 0; i < S.q; i++)
+            if (S.slot[i] >= 0) ao.p[S.slot[i]] = d_pos_out[i];
+    } else {
+        char* hp = nullptr;
+        if ((rc = staging_get(1, sizeof(int*) * kMaxQ, &hp))) return rc;
+        int32_t** hout = reinterpret_cast<int32_t**>(hp);
+        for (int i = 0; i < S.q; i++)
+            if (S.slot[i] >= 0) hout[S.slot[i]] = d_pos_out[i];
+        if ((rc = staging_put(1, w + L.outs, sizeof(int*) * S.qk, st))) return rc;
+    }
+    const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
+    const unsigned long long* offs = reinterpret_cast<const unsigned long long*>(w + L.offs);
+    int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
+    const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
     if (scatter) {
         if (S.p16)
             hipLaunchKernelGGL(k_ssp_scatter<true>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), 2 * pair_cap(S.rpb),
-                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
-                               S.base, of);
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
+                               S.rpb, S.base, of);
         else
             hipLaunchKernelGGL(k_ssp_scatter<false>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
-                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, S.rpb,
-                               S.base, of);
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
+                               S.rpb, S.base, of);
         LAUNCHCHK("k_ssp_scatter");
     }
     if (!column) return MQ_OK;
