@@ -1707,10 +1707,11 @@ bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p) {
 }
 
 // Resident 256-thread blocks per CU for one kernel (cached per device and kernel).
-int blocks_per_cu(const void* fn) {
+int blocks_per_cu(const void* fn, size_t dyn_lds) {
     struct Entry {
         int dev;
         const void* fn;
+        size_t dyn;
         int occ;
     };
     static Entry cache[64];
@@ -1720,18 +1721,20 @@ int blocks_per_cu(const void* fn) {
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     std::lock_guard<std::mutex> lk(mu);
     for (int i = 0; i < ncache; i++)
-        if (cache[i].dev == dev && cache[i].fn == fn) return cache[i].occ;
+        if (cache[i].dev == dev && cache[i].fn == fn && cache[i].dyn == dyn_lds) return cache[i].occ;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kTPB, 0) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kTPB, dyn_lds) != hipSuccess || occ < 1)
         occ = 1;
-    if (ncache < 64) cache[ncache++] = Entry{dev, fn, occ};
+    if (ncache < 64) cache[ncache++] = Entry{dev, fn, dyn_lds, occ};
     return occ;
 }
 
 // One wave of resident blocks, each owning a contiguous chunk of whole tiles.
 void geometry(const DevState* s, uint64_t n, const void* fn, uint32_t* blocks, uint64_t* rpb,
-              uint64_t granule) {
-    uint64_t gmax = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
+              uint64_t granule, size_t dyn_lds, int bpc_cap) {
+    int bpc = blocks_per_cu(fn, dyn_lds);
+    if (bpc_cap > 0 && bpc > bpc_cap) bpc = bpc_cap;
+    uint64_t gmax = (uint64_t)s->cus * (uint64_t)bpc;
     if (gmax > kMaxBlocks) gmax = kMaxBlocks;
     const uint64_t tiles = (n + granule - 1) / granule;
     uint64_t g = tiles < gmax ? tiles : gmax;

@@ -85,11 +85,13 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Fold (has_low, low, has_high, high) into one unsigned range compare; false = empty.
 bool make_pred(int has_low, int32_t low, int has_high, int32_t high, Pred* p);
-// Resident blocks of kTPB threads per CU for one kernel (cached).
-int blocks_per_cu(const void* fn);
-// One wave of resident blocks, each owning a contiguous chunk of whole granules.
+// Resident blocks of kTPB threads per CU for one kernel with dyn_lds bytes of dynamic
+// LDS (cached per kernel and size).
+int blocks_per_cu(const void* fn, size_t dyn_lds = 0);
+// One wave of resident blocks, each owning a contiguous chunk of whole granules
+// (bpc_cap > 0: at most that many blocks a CU).
 void geometry(const DevState* s, uint64_t n, const void* fn, uint32_t* blocks, uint64_t* rpb,
-              uint64_t granule = kTileRows);
+              uint64_t granule = kTileRows, size_t dyn_lds = 0, int bpc_cap = 0);
 // Bytes of the per-block partial slab at the start of every scan workspace.
 size_t partial_bytes();
 

@@ -771,16 +771,22 @@ template <bool PF, bool P16>
 __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
-                                                    uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
+                                                    uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow,
+                                                    uint32_t qlcap) {
     __shared__ uint16_t s_cell[kCells];
-    __shared__ int32_t s_b[kEiMax];
-    __shared__ uint32_t s_qoff[kEiMax];
-    __shared__ uint32_t hist[kWaves][kEiMax];
-    __shared__ uint16_t s_ql[kQlCap];
     __shared__ uint32_t s_pb[kWaves][kPb];
     __shared__ int32_t s_qv[kWaves][kRingK];
-    __shared__ uint16_t s_qe[kWaves][kRingK];
     __shared__ uint32_t s_qr[kWaves][kRingK];
+    // (round 5) the EI-sized tables in dynamic LDS, sized by this launch's m and list
+    // length (ssk_dyn_bytes), and a queued row's cell entry read again from its value
+    // instead of queued: 39.5 KB a block -> 31 KB at Q = 150 (the grid's blocks a CU are
+    // then set by ss_count's policy, not by LDS)
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const uint32_t hs = (uint32_t)M.m + 2u;  // EIs 0 .. m, plus the prefix slot
+    int32_t* const s_b = reinterpret_cast<int32_t*>(s_dyn);
+    uint32_t* const s_qoff = reinterpret_cast<uint32_t*>(s_dyn) + hs;
+    uint32_t* const hist = s_qoff + hs;  // [kWaves][hs]
+    uint16_t* const s_ql = reinterpret_cast<uint16_t*>(hist + kWaves * hs);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     {  // the cell table: 16 u16 per thread, loaded as two 16-byte words before any store
         const uint4* g = reinterpret_cast<const uint4*>(T.cell);
@@ -794,10 +800,10 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
     }
     for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
     for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
-    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
+    for (uint32_t i = tid; i < kWaves * hs; i += kTPB) hist[i] = 0;
     __syncthreads();
     const uint32_t nql = s_qoff[M.m + 1];
-    const bool ql_lds = nql <= (uint32_t)kQlCap;
+    const bool ql_lds = nql <= qlcap;
     if (ql_lds)
         for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
     __syncthreads();
@@ -810,7 +816,6 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
     uint16_t* list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
     uint32_t* pb = s_pb[wave];
     int32_t* qv = s_qv[wave];
-    uint16_t* qe = s_qe[wave];
     uint32_t* qr = s_qr[wave];
     uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0, last_tile = 0;
     bool direct = false;
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         if (has) {
             const uint32_t slot = head + (uint32_t)lane;
             const int32_t x = qv[slot];
-            const uint32_t ent = qe[slot];
+            const uint32_t ent = s_cell[min(((uint32_t)x - bmin) >> xsh, (uint32_t)kCells - 1u)];
             r = qr[slot];
             uint32_t ei = ent - 1u;
             if (ent & 0x8000u) {  // bounds inside the cell: b[e0 ..), e0 = its first EI
@@ -847,7 +852,7 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             }
             qa = s_qoff[ei];
             qn = s_qoff[ei + 1] - qa;
-            if (qn) atomicAdd(&hist[wave][ei], 1u);
+            if (qn) atomicAdd(&hist[wave * hs + ei], 1u);
         }
         head += nr;
         // P16: a token ahead of a row in another tile than the queued row before it
@@ -916,10 +921,10 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         } while (tail - head >= 64u);
         const uint32_t rest = tail - head;
         int32_t mv = 0;
-        uint32_t mr = 0, me = 0;
-        if ((uint32_t)lane < rest) mv = qv[head + lane], me = qe[head + lane], mr = qr[head + lane];
+        uint32_t mr = 0;
+        if ((uint32_t)lane < rest) mv = qv[head + lane], mr = qr[head + lane];
         __builtin_amdgcn_wave_barrier();
-        if ((uint32_t)lane < rest) qv[lane] = mv, qe[lane] = (uint16_t)me, qr[lane] = mr;
+        if ((uint32_t)lane < rest) qv[lane] = mv, qr[lane] = mr;
         __builtin_amdgcn_wave_barrier();
         head = 0;
         tail = rest;
@@ -995,7 +1000,6 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
                 if (cov) {
                     const uint32_t at = tail + mbcnt64(bm);
                     qv[at] = v[i];
-                    qe[at] = (uint16_t)ent[k];
                     qr[at] = r0 + (uint32_t)i * 64u;
                 }
                 tail += (uint32_t)__popcll(bm);
@@ -1027,8 +1031,8 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         if ((uint64_t)run > cap) atomicOr(overflow, 1u);
     }
     __builtin_amdgcn_wave_barrier();
-    uint32_t* h = hist[wave];
-    const int ne = M.m + 2;
+    uint32_t* h = hist + wave * hs;
+    const int ne = (int)hs;
     const int per = (ne + 63) / 64;
     uint32_t loc = 0;
     for (int i = 0; i < per; i++) {
@@ -1450,11 +1454,20 @@ struct SsState {
     int slot[kMaxQ];  // kernel index of query i, or -1
 };
 
+// k_ssk_count's dynamic LDS: bounds and EI offsets (m + 2 words each), the per-wave EI
+// histograms, the query lists when they fit (qlcap u16); rounded up to 1 KB so that the
+// occupancy cache sees few sizes.
+size_t ssk_dyn_bytes(int m, uint32_t qlcap) {
+    const size_t hs = (size_t)m + 2;
+    const size_t b = hs * 4 * 2 + (size_t)kWaves * hs * 4 + (size_t)qlcap * 2;
+    return (b + 1023) & ~(size_t)1023;
+}
+
 // Host side of the EI path: bounds, per-query EI ranges, per-EI query lists and
 // the bucket table, written to region (pinned staging of the workspace's EI region,
 // ss_layout); *used = the bytes in use from its start (the query lists come last, only
 // `at` entries of them).
-int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used) {
+int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used, uint32_t* nql) {
     std::vector<long long> L(qk), H(qk), b;
     b.reserve(2 * qk);
     for (int i = 0; i < qk; i++) {
@@ -1571,6 +1584,7 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used) {
     o += kEiCellB;  // the cell table, written above
     if (at) std::memcpy(region + o, hql, (size_t)at * 2);
     *used = o + (size_t)at * 2;
+    *nql = at;
     return MQ_OK;
 }
 
@@ -1643,9 +1657,31 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
                                   : (p16w ? (const void*)&k_ssk_count<false, true> : (const void*)&k_ssk_count<false, false>))
                    : ei     ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
                             : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
+    // preds, slot, EI tables and the zeroed flag: one upload from pinned staging (their
+    // offsets do not depend on the grid, the EI tables size k_ssk_count's LDS)
+    const SsLayout L0 = ss_layout(1, 1);
+    char* up = nullptr;
+    if ((rc = staging_get(0, L0.outs, &up))) return rc;
+    std::memcpy(up + L0.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1));
+    std::memcpy(up + L0.slot, hslot, sizeof(int) * q);
+    std::memset(up + L0.flag, 0, 4);
+    EiMeta meta{0, 0, 0, 0, 0, 0};
+    size_t ei_used = 0;
+    uint32_t nql = 0;
+    if (ei && (rc = ei_build(hp, qk, up + L0.ei, &meta, &ei_used, &nql))) return rc;
+    const uint32_t qlcap = nql <= (uint32_t)kQlCap ? nql : 0u;
+    const size_t dyn = kmajor ? ssk_dyn_bytes(meta.m, qlcap) : 0;
+    // blocks a CU for the k-major pass: with the tables in dynamic LDS 5-6 fit, but fewer,
+    // longer wave-chunks measured faster (1e9 rows, 0.1 % ranges, count + write, two
+    // alternating rounds on one box, profiles/r05_ss_bpc_sweep.log): 3 blocks for Q <= 8
+    // (Q = 4 / 8: 0.75 / 0.80 ms against 0.78 / 0.82 at 4), 4 above (Q = 16 / 150: 0.86 /
+    // 1.63-1.65 against 0.90 / 1.81 at 3 and 0.89 / 1.65 at the occupancy limit; the
+    // static-LDS pass before: 0.86 / 1.68). MQ_SS_BPC overrides (0: occupancy limit).
+    const char* bpce = getenv("MQ_SS_BPC");
+    const int bpc_cap = bpce ? atoi(bpce) : (qk <= 8 ? 3 : 4);
     uint32_t g = 1;
     uint64_t rpb = kGranule;
-    if (n) geometry(s, n, fn, &g, &rpb, kGranule);
+    if (n) geometry(s, n, fn, &g, &rpb, kGranule, dyn, kmajor ? bpc_cap : 0);
     const uint64_t nwc = (uint64_t)g * kWaves;
     const SsLayout L = ss_layout(nwc, qk > 0 ? qk : 1);
     const uint64_t cap = pair_cap(rpb);
@@ -1653,15 +1689,6 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
                         ws_bytes >= L.pairs + (size_t)nwc * cap * sizeof(uint32_t) && cap < (1ull << 24);
     // 16-bit entries: twice as many in the same slice bytes; tile deltas < 2^15
     const bool p16 = p16w && single && cap <= (1ull << 22);
-    // preds, slot, EI tables and the zeroed flag: one upload from pinned staging
-    char* up = nullptr;
-    if ((rc = staging_get(0, L.outs, &up))) return rc;
-    std::memcpy(up + L.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1));
-    std::memcpy(up + L.slot, hslot, sizeof(int) * q);
-    std::memset(up + L.flag, 0, 4);
-    EiMeta meta{0, 0, 0, 0, 0, 0};
-    size_t ei_used = 0;
-    if (ei && (rc = ei_build(hp, qk, up + L.ei, &meta, &ei_used))) return rc;
     if ((rc = staging_put(0, w, L.ei + ei_used, st))) return rc;
     const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
@@ -1684,17 +1711,17 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
             } else {
                 const uint64_t ce = p16 ? 2 * cap : cap;  // slice capacity in entries
                 if (pf && p16)
-                    hipLaunchKernelGGL((k_ssk_count<true, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of);
+                    hipLaunchKernelGGL((k_ssk_count<true, true>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of, qlcap);
                 else if (pf)
-                    hipLaunchKernelGGL((k_ssk_count<true, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of);
+                    hipLaunchKernelGGL((k_ssk_count<true, false>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of, qlcap);
                 else if (p16)
-                    hipLaunchKernelGGL((k_ssk_count<false, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of);
+                    hipLaunchKernelGGL((k_ssk_count<false, true>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of, qlcap);
                 else
-                    hipLaunchKernelGGL((k_ssk_count<false, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of);
+                    hipLaunchKernelGGL((k_ssk_count<false, false>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
+                                       counts, nwc, pr, ce, npr, of, qlcap);
                 LAUNCHCHK("k_ssk_count");
             }
         } else if (ei) {
