@@ -807,6 +807,17 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout64,
             fprintf(stderr, "lq level %d: large ranges %llu rows %llu items %llu | small so far %u | flagged %u jumps %d\n",
                     level, (unsigned long long)S, (unsigned long long)rows, (unsigned long long)NI, nsmall,
                     F, jumps);
+            if (F) {  // the flagged ranges' shape: rows, "<" side c and ">=" side m = rows - 1 - c
+                std::vector<uint32_t> fl(F), sc(S);
+                HIPCHK(hipMemcpy(fl.data(), flist, F * 4, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(sc.data(), segc, S * 4, hipMemcpyDeviceToHost));
+                for (uint32_t k = 0; k < F; k++) {
+                    const LSeg& g = hs[fl[k]];
+                    const uint64_t r = (uint64_t)g.hi - g.lo + 1, c = sc[fl[k]];
+                    fprintf(stderr, "lq   flagged rows %llu c %llu m %llu\n", (unsigned long long)r,
+                            (unsigned long long)c, (unsigned long long)(r - 1 - c));
+                }
+            }
         }
         S = h[0] >> 40;
         NI = h[0] & ((1ull << 40) - 1);
