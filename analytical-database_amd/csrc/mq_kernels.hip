@@ -1084,6 +1084,26 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
             if (PAYLOAD && __builtin_amdgcn_readfirstlane((int)tot) == -1) out[o] = payload[row0];
             continue;
         }
+        if (xmode == 4) {  // diagnostic: + the payload rows of every tile with a match loaded, nothing placed
+            if constexpr (PAYLOAD) {
+                const bool pal4 = (reinterpret_cast<uintptr_t>(payload) & 15u) == 0;
+                int acc = 0;
+                for (int j0 = 0; j0 < 64; j0 += 4) {
+                    int pv[4][4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) {
+                        const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
+                        pv[jj][0] = pv[jj][1] = pv[jj][2] = pv[jj][3] = 0;
+                        if (__builtin_amdgcn_readlane((int)c, j0 + jj) != 0) load_pay4(pv[jj], payload, r, n, pal4);
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < 4; jj++) acc ^= pv[jj][0] ^ pv[jj][1] ^ pv[jj][2] ^ pv[jj][3];
+                }
+                if (acc == 0x7fffffff && tot == 0) out[o] = acc;
+            }
+            o += tot;
+            continue;
+        }
         if (xmode == 1) {
             // batched (round 4, the default): tiles' outputs gathered in row order in
             // the wave's LDS ring (free now: its entries went out above), placed so that
@@ -1939,10 +1959,11 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     // 1.355 / 1.56 ms against 1.064 / 1.475 / 1.84 ms at 10 / 50 / 100 % alternating on
     // one box (profiles/r04_positions_batched_ab.log; a first staged form that flushed
     // every tile lost to the lanes, profiles/r04_positions_ab.log)
-    // (MQ_STAGE_EXPAND=2 / 3: diagnostics only, the output is incomplete: no bitmap
-    // expansion / the bitmap read and counted but nothing placed)
+    // (MQ_STAGE_EXPAND=2 / 3 / 4: diagnostics only, the output is incomplete: no bitmap
+    // expansion / the bitmap read and counted but nothing placed / + select_result's
+    // payload rows loaded for every tile with a match, nothing placed)
     const char* xe = getenv("MQ_STAGE_EXPAND");
-    const int xmode = xe && xe[0] == '0' ? 0 : xe && xe[0] == '2' ? 2 : xe && xe[0] == '3' ? 3 : 1;
+    const int xmode = xe && xe[0] == '0' ? 0 : xe && xe[0] == '2' ? 2 : xe && xe[0] == '3' ? 3 : xe && xe[0] == '4' ? 4 : 1;
     if (payload) {
         if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
         else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
