@@ -971,7 +971,10 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
 @pytest.mark.parametrize("form", ["ei", "ballot", "ei_p16"])
 @pytest.mark.parametrize("twopass", [False, True])
 @pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
-                                 (3_000_017, 20), (2_000_003, 2), (2_000_003, 5)])
+                                 (3_000_017, 20), (2_000_003, 2), (2_000_003, 5),
+                                 # round-5 boundaries: 3 -> 4 count blocks a CU (Q 8 / 9),
+                                 # output pointers as scatter arguments (Q 32 / 33)
+                                 (1_000_003, 8), (1_000_003, 9), (1_000_003, 32), (1_000_003, 33)])
 def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass, form):
     """Every Q takes the elementary-interval kernels by default (round 5: from Q = 1);
     "ballot" forces the per-query ballot kernels (MQ_SS_IMPL=ballot), "ei_p16" the
