@@ -1066,7 +1066,6 @@ constexpr int kSpChunk = 4096;                  // pairs sorted in LDS at a time
 constexpr int kSpPerWave = kSpChunk / kWaves;   // 1024: 16 rounds of 64
 constexpr int kSpRounds = kSpPerWave / 64;
 constexpr int kSpBatch = 4;                     // rounds whose pairs are loaded together
-constexpr int kSpPer = kSpChunk / kTPB;         // entries each thread places
 
 // Ranks go to LDS as they are made (the pair itself in s_buf, its rank among the
 // wave's earlier pairs of its query in s_loc), not into registers held across the
@@ -1089,22 +1088,25 @@ struct SsArgOuts {
     int* p[kArgQ];
 };
 
-template <bool P16>
-__global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
+template <bool P16, int SW>
+__global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
                                                       int q, int* const* __restrict__ outs, SsArgOuts ao,
                                                       bool by_arg, uint64_t rpb, int32_t base,
                                                       const unsigned int* __restrict__ overflow) {
+    // SW waves a block, 1024 pairs a wave a chunk (round 5: SW = 8 sorts 8192-pair
+    // chunks in 512 threads, same registers a thread, twice the LDS)
+    constexpr int TPB = 64 * SW, CH = kSpPerWave * SW;
     if (*overflow) return;  // a slice overflowed: k_ssi_write's column pass writes
-    __shared__ uint32_t s_buf[kSpChunk];
-    __shared__ uint16_t s_loc[kSpChunk];
-    __shared__ uint32_t s_cnt[kWaves][kMaxQ];
+    __shared__ uint32_t s_buf[CH];
+    __shared__ uint16_t s_loc[CH];
+    __shared__ uint32_t s_cnt[SW][kMaxQ];
     __shared__ uint32_t s_start[kMaxQ], s_tot[kMaxQ];
     __shared__ unsigned long long s_run[kMaxQ];
     __shared__ gint* s_out[kMaxQ];
-    __shared__ uint32_t s_wsum[kWaves];
-    __shared__ uint32_t s_wt[kWaves];  // P16: tiles a wave's part of the chunk advances
+    __shared__ uint32_t s_wsum[SW];
+    __shared__ uint32_t s_wt[SW];  // P16: tiles a wave's part of the chunk advances
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint64_t wc = blockIdx.x;
@@ -1113,7 +1115,7 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
     uint16_t* const list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
     uint32_t ctile = 0;  // P16: the tile at the chunk's first entry
     const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
-    for (int i = tid; i < q; i += kTPB) {
+    for (int i = tid; i < q; i += TPB) {
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
         s_out[i] = global_ptr(by_arg ? ao.p[i] : outs[i]);
     }
@@ -1129,12 +1131,12 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
         }
     };
     load_chunk(0);
-    for (uint32_t c0 = 0; c0 < np; c0 += kSpChunk) {
+    for (uint32_t c0 = 0; c0 < np; c0 += CH) {
         uint32_t cx[kSpRounds];
 #pragma unroll
         for (int r = 0; r < kSpRounds; r++) cx[r] = nx[r];
-        if (c0 + kSpChunk < np) load_chunk(c0 + kSpChunk);
-        for (int i = tid; i < kWaves * kMaxQ; i += kTPB) (&s_cnt[0][0])[i] = 0;
+        if (c0 + CH < np) load_chunk(c0 + CH);
+        for (int i = tid; i < SW * kMaxQ; i += TPB) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
         // this wave's 1024 pairs of the chunk
         uint32_t wt = 0;  // P16: tiles advanced so far in this wave's part
@@ -1178,7 +1180,7 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
         uint32_t tq = 0;
         if (tid < q) {
 #pragma unroll
-            for (int w = 0; w < kWaves; w++) tq += s_cnt[w][tid];
+            for (int w = 0; w < SW; w++) tq += s_cnt[w][tid];
         }
         uint32_t incl = tq;
 #pragma unroll
@@ -1195,32 +1197,32 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
             s_tot[tid] = tq;
             uint32_t a = st0;
 #pragma unroll
-            for (int w = 0; w < kWaves; w++) {
+            for (int w = 0; w < SW; w++) {
                 const uint32_t c = s_cnt[w][tid];
                 s_cnt[w][tid] = a;
                 a += c;
             }
         }
         __syncthreads();
-        const uint32_t cn = np - c0 < (uint32_t)kSpChunk ? np - c0 : (uint32_t)kSpChunk;
+        const uint32_t cn = np - c0 < (uint32_t)CH ? np - c0 : (uint32_t)CH;
         // the chunk's pairs (P16: its entries less the tokens)
         uint32_t cnv = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; w++) cnv += s_wsum[w];
-        uint32_t wrow[kWaves];  // P16: the first row of each wave's part
+        for (int w = 0; w < SW; w++) cnv += s_wsum[w];
+        uint32_t wrow[SW];  // P16: the first row of each wave's part
         {
             uint32_t a = ctile;
 #pragma unroll
-            for (int w = 0; w < kWaves; w++) {
+            for (int w = 0; w < SW; w++) {
                 wrow[w] = a * 128u;
                 if (P16) a += s_wt[w];
             }
             ctile = a;
         }
-        uint32_t px[kSpPer], pd[kSpPer];
+        uint32_t px[(CH / TPB)], pd[(CH / TPB)];
 #pragma unroll
-        for (int k = 0; k < kSpPer; k++) {
-            const uint32_t i = (uint32_t)(k * kTPB + tid);
+        for (int k = 0; k < (CH / TPB); k++) {
+            const uint32_t i = (uint32_t)(k * TPB + tid);
             px[k] = s_buf[i];
             const bool pair = i < cn && (!P16 || px[k] != 0xFFFFFFFFu);
             pd[k] = pair ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
@@ -1228,7 +1230,7 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kSpPer; k++)
+        for (int k = 0; k < (CH / TPB); k++)
             if (pd[k] != 0xFFFFFFFFu) s_buf[pd[k]] = px[k];
         __syncthreads();
         // (round 4) a fixed 16 stores a thread, the slots past the chunk's end going to a
@@ -1238,8 +1240,8 @@ __global__ __launch_bounds__(kTPB, 4) void k_ssp_scatter(uint32_t* pairs, uint64
         // (P16: `list` is not this slice's start, cap counting 16-bit entries)
         gint* const dummy = P16 ? (gint*)(list16 + c0) : (gint*)(list + c0);
 #pragma unroll
-        for (int k = 0; k < kSpPer; k++) {
-            const uint32_t i = (uint32_t)(k * kTPB + tid);
+        for (int k = 0; k < (CH / TPB); k++) {
+            const uint32_t i = (uint32_t)(k * TPB + tid);
             const bool in = i < cnv;
             const uint32_t y = s_buf[i], qid = in ? y >> 24 : 0u;
             gint* const dst = in ? s_out[qid] + (s_run[qid] + (i - s_start[qid])) : dummy;
@@ -1449,8 +1451,9 @@ struct SsState {
     int32_t base;  // first row number of this (row-shard) column
     bool pairs;    // the count pass listed the pairs (single pass)
     bool p16;      // ... as 16-bit entries (k_ssk_count<*, true>)
-    bool flag_known;  // the host read the overflow word after the count (flag)
+    bool flag_known;  // the host read the overflow word after the count (flag) ...
     unsigned int flag;
+    uint64_t pairs_total;  // ... and the totals (their sum)
     int slot[kMaxQ];  // kernel index of query i, or -1
 };
 
@@ -1767,8 +1770,21 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     state->p16 = p16 && ei && !filt;
     state->flag_known = false;
     state->flag = 0;
+    state->pairs_total = 0;
     std::memcpy(state->slot, hslot, sizeof(int) * q);
     return MQ_OK;
+}
+
+// k_ssp_scatter's waves a block: 8 (8192-pair chunks: longer runs per query, half the
+// chunks a slice) where the slices average at least 8192 pairs, else 4 (a half-empty
+// 8192-pair chunk costs more than it saves). 1e9 rows, 0.1 % ranges, count + write,
+// alternating on one box (profiles/r05_ss_scatter_waves_ab.log): Q = 150 1.756 ->
+// 1.668 ms with 8; Q = 16 (3.9 K pairs a slice) 0.866 -> 0.890. MQ_SS_SCATTER_WAVES=4|8
+// forces one (A/B, tests).
+int ss_scatter_waves(const SsState& S, uint64_t nwc) {
+    const char* e = getenv("MQ_SS_SCATTER_WAVES");
+    if (e) return atoi(e) == 8 ? 8 : 4;
+    return S.flag_known && nwc && S.pairs_total / nwc >= 8192 ? 8 : 4;
 }
 
 int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_t st) {
@@ -1803,12 +1819,17 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
     if (scatter) {
         if (S.p16)
-            hipLaunchKernelGGL(k_ssp_scatter<true>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+            hipLaunchKernelGGL((k_ssp_scatter<true, 4>), dim3((uint32_t)nwc), dim3(kTPB), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), 2 * pair_cap(S.rpb),
                                reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
                                S.rpb, S.base, of);
+        else if (ss_scatter_waves(S, nwc) == 8)
+            hipLaunchKernelGGL((k_ssp_scatter<false, 8>), dim3((uint32_t)nwc), dim3(512), 0, st,
+                               reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
+                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
+                               S.rpb, S.base, of);
         else
-            hipLaunchKernelGGL(k_ssp_scatter<false>, dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+            hipLaunchKernelGGL((k_ssp_scatter<false, 4>), dim3((uint32_t)nwc), dim3(kTPB), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
                                reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
                                S.rpb, S.base, of);
@@ -1884,6 +1905,7 @@ int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base
         std::memcpy(&fl, hp + sizeof(uint64_t) * q, sizeof fl);
         S.flag_known = true;
         S.flag = (unsigned int)fl;
+        for (int i = 0; i < q; i++) S.pairs_total += h_counts[i];
     }
     g_last_state = S;
     g_last_ws = d_ws;

@@ -1033,7 +1033,7 @@ def _shared_run(lib, d, lows, highs):
     return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
 
 
-@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_p16"])
+@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_p16", "ei_sw8"])
 @pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
                                   "mixed256", "narrow_domain"])
 def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
@@ -1050,6 +1050,8 @@ def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
     if impl == "ei_p16":  # the count pass's 16-bit pair lists (not the default)
         monkeypatch.setenv("MQ_SS_P16", "1")
+    if impl == "ei_sw8":  # the scatter's 8-wave blocks, which the default takes for long slices only
+        monkeypatch.setenv("MQ_SS_SCATTER_WAVES", "8")
     rng = np.random.default_rng(hash(case) % 2 ** 32)
     n = 1_000_003
     d = rng.integers(0, 10 ** 6, n).astype(np.int32)
