@@ -1779,8 +1779,9 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
 // chunks a slice) where the slices average at least 8192 pairs, else 4 (a half-empty
 // 8192-pair chunk costs more than it saves). 1e9 rows, 0.1 % ranges, count + write,
 // alternating on one box (profiles/r05_ss_scatter_waves_ab.log): Q = 150 1.756 ->
-// 1.668 ms with 8; Q = 16 (3.9 K pairs a slice) 0.866 -> 0.890. MQ_SS_SCATTER_WAVES=4|8
-// forces one (A/B, tests).
+// 1.668 ms with 8; Q = 16 (3.9 K pairs a slice) 0.866 -> 0.890; 16 waves (16384-pair
+// chunks, one block a CU) 1.755 / 0.977 (profiles/r05_ss_scatter_waves16_ab.log).
+// MQ_SS_SCATTER_WAVES=4|8 forces one (A/B, tests).
 int ss_scatter_waves(const SsState& S, uint64_t nwc) {
     const char* e = getenv("MQ_SS_SCATTER_WAVES");
     if (e) return atoi(e) == 8 ? 8 : 4;
