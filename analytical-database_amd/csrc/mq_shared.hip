@@ -1083,7 +1083,7 @@ constexpr int kSpBatch = 4;                     // rounds whose pairs are loaded
 // added when the pairs are placed. Tokens take a list slot but no output slot.
 // Up to kArgQ output pointers by value (the kernel's argument block): a write that runs
 // only the scatter then needs no upload before it.
-constexpr int kArgQ = 32;
+constexpr int kArgQ = kMaxQ;  // 2 KB of arguments (the limit is 4 KB)
 struct SsArgOuts {
     int* p[kArgQ];
 };
@@ -1102,7 +1102,10 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
     __shared__ uint32_t s_buf[CH];
     __shared__ uint16_t s_loc[CH];
     __shared__ uint32_t s_cnt[SW][kMaxQ];
-    __shared__ uint32_t s_start[kMaxQ], s_tot[kMaxQ];
+    __shared__ uint32_t s_tot[kMaxQ];
+    // (round 5) a query's write base for this chunk, out + run - start: one LDS read a
+    // pair in the write instead of three (out, run, start)
+    __shared__ gint* s_dst[kMaxQ];
     __shared__ unsigned long long s_run[kMaxQ];
     __shared__ gint* s_out[kMaxQ];
     __shared__ uint32_t s_wsum[SW];
@@ -1193,7 +1196,7 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
         if (tid < q) {
             uint32_t st0 = incl - tq;
             for (int w = 0; w < wave; w++) st0 += s_wsum[w];
-            s_start[tid] = st0;
+            s_dst[tid] = s_out[tid] + ((long long)s_run[tid] - (long long)st0);
             s_tot[tid] = tq;
             uint32_t a = st0;
 #pragma unroll
@@ -1244,7 +1247,7 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
             const uint32_t i = (uint32_t)(k * TPB + tid);
             const bool in = i < cnv;
             const uint32_t y = s_buf[i], qid = in ? y >> 24 : 0u;
-            gint* const dst = in ? s_out[qid] + (s_run[qid] + (i - s_start[qid])) : dummy;
+            gint* const dst = in ? s_dst[qid] + i : dummy;
             *dst = (int)(row0 + (y & 0xFFFFFFu)) + base;
         }
         __syncthreads();
