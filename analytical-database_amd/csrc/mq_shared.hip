@@ -258,7 +258,11 @@ constexpr int kEiMinQ = 1;
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
-constexpr int kSsPfMinQ = 64;   // k_ssk_count prefetches the next group from this many queries
+// k_ssk_count prefetches the next group from this many queries (round 5, with the
+// dynamic-LDS pass and 4 blocks a CU: off is faster at Q = 16 / 32 / 64 (0.88 / 0.94 /
+// 1.13 against 0.90 / 0.97 / 1.18 ms), on at Q = 150 (1.567 against 1.612), three
+// alternating rounds on one box, profiles/r05_ss_pf_ab.log; was 64)
+constexpr int kSsPfMinQ = 100;
 constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
 constexpr int kBucketsP = kBuckets / 2;  // k_ssp_count's bucket table (LDS)
 constexpr int kCoarse = 16384;           // k_ssp_count's coverage bitmap cells
