@@ -394,7 +394,7 @@ __device__ __forceinline__ bool finish_counting(const u64 (&el)[I], uint32_t len
     return true;
 }
 
-// The counting finisher, second form (round 4, MQ_ISORT_FIN=4): the same sort with
+// The counting finisher, second form (round 4): the same sort with
 // fewer scalar and LDS instructions. The first form's PMC at 1e9 rows: 2.5 G SALU
 // (exec-mask bookkeeping of per-row guards) and 0.71 G LDS instructions with 1.35 G
 // bank-conflict cycles. Here:
@@ -631,10 +631,9 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
     u64* scratch = (u64*)pool_alloc(scan_u32_scratch_elems(tmax * 256) * 8);
     Seg* sl[2] = {(Seg*)pool_alloc(smax * sizeof(Seg)), (Seg*)pool_alloc(smax * sizeof(Seg))};
     Ctr* ctr = (Ctr*)pool_alloc(sizeof(Ctr));
-    // MQ_ISORT_FIN: the counting finisher's shape, 1 = 1024 x 16 with per-row guards,
-    // 2 = 512 x 32 with guards, 3 = 512 x 32 branch-free, 4 = 1024 x 16 second form (A/B)
-    const char* ff = getenv("MQ_ISORT_FIN");
-    const int fin_form = ff ? atoi(ff) : 4;
+    // The counting finisher: 1024 x 16, the second form (V2) where both outputs are
+    // wanted (512 x 32 shapes, with and without per-row guards, measured slower in round 4,
+    // profiles/r04_isort_fin_ab.log, and removed in round 6)
     Fin* fl[kMaxLevels] = {};  // finisher lists of each level: counting
     Fin* rl[kMaxLevels] = {};  // ... ranked
     Fin* bl[kMaxLevels] = {};  // ... and the counting finisher's fallbacks
@@ -725,17 +724,11 @@ int msd_index_sort(const int* col, uint64_t n, uint32_t kmin, u64 R0, int32_t* v
                                ctr, kmin, vout, pout);
         if (hc.nfin) {
             const uint32_t g = hc.nfin < cus ? hc.nfin : cus;
-            if (fin_form == 4 && vout && pout)  // (the second form writes both outputs)
+            if (vout && pout)  // (the second form writes both outputs)
                 hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false, true>), dim3(g), dim3(1024), 0, st, wb[0],
                                    wb[1], fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
-            else if (fin_form == 1 || fin_form == 4)
-                hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false>), dim3(g), dim3(1024), 0, st, wb[0], wb[1],
-                                   fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
-            else if (fin_form == 2)
-                hipLaunchKernelGGL((k_msd_finish_count<512, 32, false>), dim3(g), dim3(512), 0, st, wb[0], wb[1],
-                                   fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
             else
-                hipLaunchKernelGGL((k_msd_finish_count<512, 32, true>), dim3(g), dim3(512), 0, st, wb[0], wb[1],
+                hipLaunchKernelGGL((k_msd_finish_count<1024, 16, false>), dim3(g), dim3(1024), 0, st, wb[0], wb[1],
                                    fl[level], hc.nfin, kmin, vout, pout, bl[level], ctr);
             hipLaunchKernelGGL(k_msd_finish_ranked<true>, dim3(cus), dim3(kFT), 0, st, wb[0], wb[1], bl[level], ctr,
                                kmin, vout, pout);
@@ -759,7 +752,8 @@ int radix_sort_index(const int* col, uint64_t n, int32_t* values, uint64_t* posi
     if (n == 0) return MQ_OK;
     DevState* s;
     if (int rc0 = ensure_ready(&s)) return rc0;
-    // MQ_INDEX_SORT=lsd4: the four-pass LSD sort whatever the range (A/B)
+    // MQ_INDEX_SORT=lsd4 / lsd: the four-pass LSD sort whatever the range, or the LSD form
+    // with the range's passes where the MSD form would run (path-forcing, tests)
     const char* f = getenv("MQ_INDEX_SORT");
     if (f && strcmp(f, "lsd4") == 0) return radix_sort_lsd_index(col, n, 0, 4, values, positions, st);
     void* ws = pool_alloc(mq_scan_workspace_bytes(n));

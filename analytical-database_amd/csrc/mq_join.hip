@@ -333,203 +333,6 @@ __global__ __launch_bounds__(TPB) void k_sortw_scatter(const int* __restrict__ c
 }
 
 // ---------------------------------------------------------------------------
-// Onesweep variant of the same sort (n < 2^30): one read of the keys gives all four
-// digit histograms (k_sort1_hist); each pass is then one kernel whose tiles take a
-// ticket in launch order and learn the count of every digit in the tiles before
-// them by decoupled look-back over per-(tile, digit) status words {flag, count},
-// instead of a histogram pass over the words and a scan per pass: the words are
-// read once per pass, not twice.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kStAgg = 1u << 30, kStPre = 2u << 30, kStVal = (1u << 30) - 1;
-
-__global__ __launch_bounds__(kTPB) void k_sort1_hist(const int* __restrict__ c1, uint64_t n,
-                                                     uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t h[kTPB / 64][4][kRadix];  // per wave: fewer same-address collisions
-    const int tid = threadIdx.x, wave = tid >> 6;
-    for (int i = tid; i < (kTPB / 64) * 4 * kRadix; i += kTPB) (&h[0][0][0])[i] = 0;
-    __syncthreads();
-    const uint64_t step = (uint64_t)gridDim.x * kSortTile;
-    for (uint64_t base = (uint64_t)blockIdx.x * kSortTile; base < n; base += step) {
-        uint32_t key[kSortItems];
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++) {
-            const uint64_t i = base + (uint64_t)k * kTPB + tid;
-            key[k] = (uint32_t)__builtin_nontemporal_load(c1 + (i < n ? i : n - 1)) ^ 0x80000000u;
-        }
-#pragma unroll
-        for (int k = 0; k < kSortItems; k++)
-            if (base + (uint64_t)k * kTPB + tid < n) {
-                atomicAdd(&h[wave][0][key[k] & 0xFF], 1u);
-                atomicAdd(&h[wave][1][(key[k] >> 8) & 0xFF], 1u);
-                atomicAdd(&h[wave][2][(key[k] >> 16) & 0xFF], 1u);
-                atomicAdd(&h[wave][3][key[k] >> 24], 1u);
-            }
-    }
-    __syncthreads();
-    for (int i = tid; i < 4 * kRadix; i += kTPB) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < kTPB / 64; w++) c += (&h[w][0][0])[i];
-        if (c) atomicAdd(&ghist[i], c);
-    }
-}
-
-// ghist[4][256] -> exclusive prefix per pass, in place (one block)
-__global__ __launch_bounds__(kTPB) void k_sort1_base(uint32_t* __restrict__ g) {
-    __shared__ uint32_t wsum[kTPB / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int p = 0; p < 4; p++) {
-        const uint32_t v = g[p * kRadix + tid];
-        uint32_t incl = v;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        if (lane == 63) wsum[wave] = incl;
-        __syncthreads();
-        uint32_t excl = incl - v;
-        for (int w = 0; w < wave; w++) excl += wsum[w];
-        g[p * kRadix + tid] = excl;
-        __syncthreads();
-    }
-}
-
-__device__ __forceinline__ void st_status(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_status(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool FIRST, int LAST>
-__global__ __launch_bounds__(kTPB) void k_sort1_scatter(const int* __restrict__ c1, const int* __restrict__ p1,
-                                                        const u64* __restrict__ in, uint64_t n, int shift,
-                                                        const uint32_t* __restrict__ gbase,
-                                                        uint32_t* __restrict__ status, uint32_t* __restrict__ ticket,
-                                                        u64* __restrict__ out, uint32_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout, u64* __restrict__ pout) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
-    __shared__ uint32_t loff[kRadix];
-    __shared__ u64 gofs[kRadix];
-    __shared__ u64 stage[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
-    __shared__ uint32_t s_tile;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u);  // tiles in launch order: predecessors have started
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
-    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
-    u64 el[kSortItems];
-    uint32_t dr[kSortItems];
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        el[k] = sort_word<FIRST>(c1, p1, in, i < n ? i : n - 1);
-    }
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        const bool valid = i < n;
-        const uint32_t d = ((uint32_t)el[k] >> shift) & 0xFF;
-        const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = lanes_below(peers);
-        const uint32_t cur = wcnt[wave][d];
-        __builtin_amdgcn_wave_barrier();
-        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
-    }
-    // digit tid: publish this tile's count, then look back for the count before it
-    uint32_t* my = status + (uint64_t)tile * kRadix + tid;
-    uint32_t before = 0;
-    if (tile == 0) {
-        st_status(my, kStPre | tot);
-    } else {
-        st_status(my, kStAgg | tot);
-        // kLook predecessors per step, loads in flight together: right after launch
-        // every resident tile looks back over all the others at once, one dependent
-        // load per tile would be ~2000 round trips
-        constexpr int kLook = 8;
-        int64_t t = (int64_t)tile - 1;
-        for (;;) {
-            uint32_t w[kLook];
-#pragma unroll
-            for (int k = 0; k < kLook; k++) w[k] = t - k >= 0 ? ld_status(status + (uint64_t)(t - k) * kRadix + tid) : kStPre;
-            // the nearest inclusive prefix among them ends the walk; every word up to it
-            // must be published (flag set) before it can be used
-            int stop = kLook, ready = kLook;
-#pragma unroll
-            for (int k = kLook - 1; k >= 0; k--) {
-                if (!(w[k] & ~kStVal)) ready = k;
-                if (w[k] & kStPre) stop = k;
-            }
-            if (ready <= stop && ready < kLook) {  // wait for the first unpublished one
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-#pragma unroll
-            for (int k = 0; k < kLook; k++)
-                if (k <= stop && t - k >= 0) before += w[k] & kStVal;
-            if (stop < kLook || t - kLook < 0) break;
-            t -= kLook;
-        }
-        st_status(my, kStPre | (before + tot));
-    }
-    gofs[tid] = (u64)gbase[tid] + before;
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        if (dr[k] != 0xFFFFFFFFu) {
-            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
-            stage[loff[d] + wcnt[wave][d] + r] = el[k];
-        }
-    }
-    __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint32_t e = (uint32_t)(k * kTPB + tid);
-        if (e < tn) {
-            const u64 v = stage[e];
-            const uint32_t d = ((uint32_t)v >> shift) & 0xFF;
-            const u64 dst = gofs[d] + (e - loff[d]);
-            if constexpr (LAST == 1) {
-                kout[dst] = (uint32_t)v;
-                vout[dst] = (uint32_t)(v >> 32);
-            } else if constexpr (LAST == 2) {
-                if (kout) kout[dst] = (uint32_t)v ^ 0x80000000u;
-                if (pout) pout[dst] = v >> 32;
-            } else {
-                out[dst] = v;
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // hash table: 64-bit slot words {key (low 32), occupied (bit 32)}, linear probing
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t hash32(uint32_t k) {  // murmur3 finaliser
@@ -1516,171 +1319,6 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build_runs(const u64* __restric
     for (uint32_t x = tid; x < c; x += kWinTPB) bpos[b + x] = (int)stage[x];
 }
 
-// The same build into 16-byte slots {key | meta << 32, p0 | p1 << 32} (meta = start << 4
-// | length, as the 8-byte table's payload): windows of 4096 slots, buckets of two
-// (32 B, one probe read), and a run of one or two rows carries its build positions
-// in the slot itself, so the probe's bucket read brings them and the write streams
-// them instead of reading the run array at random (longer runs are still looked up
-// there). As many slots as the 8-byte table (2^29 at 2^28 build rows: the 2^27
-// distinct keys of config 5 at load 1/4, 8 GB), windows of 8192 (the same partition;
-// 128 KB of LDS, one block a CU): at load 1/2 (half the slots, windows of 4096) the
-// two-slot buckets sent so many probes on along the window that the probe lost what
-// the write gained (9.9 vs 7.2 ms, write 1.4 vs 3.9). A window of more than 6144
-// distinct keys (3/4 full) flags as well.
-constexpr uint32_t kWin16Log = 13;
-constexpr uint32_t kBucket16 = 2;
-constexpr uint32_t kKeys16 = 6144;
-
-__device__ __forceinline__ uint64_t ht_home16(uint32_t key, uint64_t mask) {
-    return hash32(key) & mask & ~(uint64_t)(kBucket16 - 1);
-}
-
-__global__ __launch_bounds__(kWinTPB) void k_win_build_runs16(const u64* __restrict__ in,
-                                                              const uint32_t* __restrict__ wstart,
-                                                              ulonglong2* __restrict__ slots, int* __restrict__ bpos,
-                                                              Win t, uint32_t* __restrict__ general) {
-    constexpr uint32_t W = 1u << kWin16Log;
-    constexpr int kPer = (int)(kRunRows / kWinTPB);
-    constexpr int kW = kWinTPB / 64;
-    __shared__ uint32_t tab[W];          // keys by slot
-    __shared__ uint32_t c32[W / 2];      // u16 per slot: counts, then run places
-    __shared__ u64 pos2[W];              // a short run's build positions by slot
-    __shared__ uint16_t pidx[kRunRows];  // input index (within the window) by place
-    __shared__ uint8_t ovf[W / kBucket16];
-    __shared__ uint32_t wsum[kW + 2];    // wave totals, the flag, the distinct keys
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t w = blockIdx.x;
-    const uint32_t b = wstart[w], e = wstart[w + 1], c = e - b;
-    if (W != (uint32_t)t.wmask + 1 || c > kRunRows) {
-        if (tid == 0) *general = 1;
-        return;
-    }
-    for (uint32_t x = tid; x < W; x += kWinTPB) tab[x] = kEmpty32, pos2[x] = 0ull;
-    for (uint32_t x = tid; x < W / 2; x += kWinTPB) c32[x] = 0;
-    for (uint32_t x = tid; x < W / kBucket16; x += kWinTPB) ovf[x] = 0;
-    if (tid == 0) wsum[kW] = 0, wsum[kW + 1] = 0;
-    __syncthreads();
-    uint32_t key[kPer], pay[kPer], slot[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        const uint32_t i = (uint32_t)k * kWinTPB + tid;
-        const u64 v = i < c ? in[b + i] : 0ull;
-        key[k] = (uint32_t)v;
-        pay[k] = (uint32_t)(v >> 32);
-    }
-    bool bad = false;
-    uint32_t fresh = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        slot[k] = 0;
-        if ((uint32_t)k * kWinTPB + tid >= c) continue;
-        if (key[k] == kEmpty32) {
-            bad = true;
-            continue;
-        }
-        const uint32_t h0 = (uint32_t)ht_home16(key[k], t.wmask);
-        uint32_t h = h0;
-        for (uint32_t step = 0; step < W; step++) {
-            const uint32_t old = atomicCAS(&tab[h], kEmpty32, key[k]);
-            if (old == kEmpty32 || old == key[k]) {
-                if (old == kEmpty32) {
-                    fresh++;
-                    if (step >= kBucket16) ovf[h0 / kBucket16] = 1;
-                }
-                break;
-            }
-            h = (h + 1) & (W - 1);
-        }
-        slot[k] = h;
-        atomicAdd(&c32[h >> 1], 1u << (16 * (h & 1)));
-    }
-    if (bad) wsum[kW] = 1;
-    if (fresh) atomicAdd(&wsum[kW + 1], fresh);
-    __syncthreads();
-    constexpr int kQ = (int)(W / 2 / kWinTPB);
-    uint32_t* mine = c32 + (uint32_t)tid * kQ;
-    uint32_t tot = 0, mx = 0;
-#pragma unroll
-    for (int j = 0; j < kQ; j++) {
-        const uint32_t cell = mine[j], lo = cell & 0xFFFFu, hi = cell >> 16;
-        mx = lo > mx ? lo : mx;
-        mx = hi > mx ? hi : mx;
-        tot += lo + hi;
-    }
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    if (__ballot(mx >= 15u)) wsum[kW] = 1;
-    __syncthreads();
-    if (wsum[kW] || wsum[kW + 1] > kKeys16) {
-        if (tid == 0) *general = 1;
-        return;
-    }
-    uint32_t run = incl - tot;
-    for (int v = 0; v < wave; v++) run += wsum[v];
-#pragma unroll
-    for (int j = 0; j < kQ; j++) {
-        const uint32_t cell = mine[j], lo = cell & 0xFFFFu;
-        mine[j] = run | ((run + lo) << 16);
-        run += lo + (cell >> 16);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        const uint32_t i = (uint32_t)k * kWinTPB + tid;
-        if (i >= c) continue;
-        const uint32_t h = slot[k], sh = 16 * (h & 1);
-        pidx[(atomicAdd(&c32[h >> 1], 1u << sh) >> sh) & 0xFFFFu] = (uint16_t)i;
-    }
-    __syncthreads();
-    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
-    uint32_t* p32 = reinterpret_cast<uint32_t*>(pos2);
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        const uint32_t i = (uint32_t)k * kWinTPB + tid;
-        if (i >= c) continue;
-        const uint32_t h = slot[k];
-        const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
-        uint32_t r = 0;
-        for (uint32_t q = s0; q < s1; q++) r += pidx[q] < i;
-        if (s1 - s0 <= 2u)
-            p32[2 * h + r] = pay[k];
-        else
-            bpos[b + s0 + r] = (int)pay[k];
-    }
-    __syncthreads();
-    ulonglong2* dst = slots + (uint64_t)w * W;
-    for (uint32_t bk = tid; bk < W / kBucket16; bk += kWinTPB) {
-        ulonglong2 o[kBucket16];
-        bool full = true;
-#pragma unroll
-        for (uint32_t q = 0; q < kBucket16; q++) {
-            const uint32_t h = bk * kBucket16 + q;
-            const uint32_t k = tab[h];
-            if (k == kEmpty32) {
-                o[q].x = kEmpty;
-                o[q].y = 0ull;
-                full = false;
-            } else {
-                const uint32_t s0 = h ? c16[h - 1] : 0u, s1 = c16[h];
-                o[q].x = (u64)k | ((u64)(((b + s0) << 4) | (s1 - s0)) << 32);
-                o[q].y = pos2[h];
-            }
-        }
-        if (full && (((uint32_t)o[0].x > (uint32_t)o[1].x) != (ovf[bk] != 0))) {
-            const ulonglong2 x = o[0];
-            o[0] = o[1];
-            o[1] = x;
-        }
-        dst[bk * kBucket16] = o[0];
-        dst[bk * kBucket16 + 1] = o[1];
-    }
-}
-
 // 2 probes per thread per step: with whole-bucket loads 2 beat 8 (8.25 vs 8.8 ms at
 // 2^28, same box: fewer VGPRs, more waves); with single-slot loads 8 had beaten 1.
 constexpr int kProbeILP = 2;
@@ -1738,18 +1376,15 @@ __device__ __forceinline__ uint32_t run_len(uint32_t payload, const uint32_t* __
 // RUNS (duplicate keys as runs, the payload a packed run, see run_payload): per row
 // the run's start in pstart and its length in cnt (0 = no match) instead of hit
 // words. Row indices and steps are kept as u32 (n2 <= 2^31 rows).
-template <bool RUNS, bool S16 = false>
+template <bool RUNS>
 __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict__ pkeys, uint64_t n2,
                                                           const u64* __restrict__ words, Win t,
                                                           uint32_t* __restrict__ pstart,
                                                           u64* __restrict__ hits, const uint32_t* __restrict__ rs,
                                                           uint32_t* __restrict__ cnt, bool packed, bool marks,
-                                                          uint32_t* __restrict__ wcnt, u64* __restrict__ p01) {
-    // S16: the 16-byte-slot runs table (k_win_build_runs16): buckets of two slots, and a
-    // hit's slot also brings the short run's build positions (p01 per row)
-    constexpr uint32_t kB = S16 ? kBucket16 : kBucket;
-    auto home = [&](uint32_t key) { return S16 ? ht_home16(key, t.mask) : ht_home(key, t.mask); };
-    const ulonglong2* __restrict__ words16 = reinterpret_cast<const ulonglong2*>(words);
+                                                          uint32_t* __restrict__ wcnt) {
+    constexpr uint32_t kB = kBucket;
+    auto home = [&](uint32_t key) { return ht_home(key, t.mask); };
     __shared__ uint32_t q_j[kTPB / 64][kContCap], q_h[kTPB / 64][kContCap], q_k[kTPB / 64][kContCap];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* const qj = q_j[wave];
@@ -1774,7 +1409,7 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
         return (hh & ~t.wmask) | ((hh + ch) & t.wmask);
     };
     // a continuation: row cj at step ch with key ck (lanes < ntake hold one)
-    auto cont_resolve = [&](bool has, uint32_t cj, uint32_t ch, uint32_t ck, u64 c, u64 cy) {
+    auto cont_resolve = [&](bool has, uint32_t cj, uint32_t ch, uint32_t ck, u64 c) {
         // c: the slot's word. Resolved on the key or an empty slot; otherwise requeued.
         bool again = false;
         if (has) {
@@ -1784,7 +1419,6 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
                 if (RUNS || hit) probe_emit<RUNS>(cj, hit, payload, pstart, rs, cnt, packed);
                 if (!RUNS && hit) atomicOr(&hits[cj >> 6], 1ull << (cj & 63));  // word stored in an earlier step
                 if (RUNS && wcnt && hit) atomicAdd(&wcnt[cj >> 6], run_len(payload, rs));  // likewise
-                if (S16) p01[cj] = hit ? cy : 0ull;
             } else {
                 again = true;
             }
@@ -1816,20 +1450,13 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             ck = qk[e];
         }
         nq -= ntake;
-        u64 c = 0, cy = 0;
-        if (has) {
-            if constexpr (S16) {
-                const ulonglong2 v = words16[cont_slot(ck, ch)];
-                c = v.x, cy = v.y;
-            } else {
-                c = words[cont_slot(ck, ch)];
-            }
-        }
+        u64 c = 0;
+        if (has) c = words[cont_slot(ck, ch)];
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             key[u] = knext[u];
             h[u] = home(key[u]);
-            const ulonglong2* q = S16 ? words16 + h[u] : reinterpret_cast<const ulonglong2*>(words + h[u]);
+            const ulonglong2* q = reinterpret_cast<const ulonglong2*>(words + h[u]);
             b0[u] = q[0];
             b1[u] = q[1];
         }
@@ -1838,24 +1465,19 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             const uint64_t j = j0 + stride + (uint64_t)u * kTPB;
             knext[u] = (uint32_t)pkeys[j < n2 ? j : n2 - 1];
         }
-        cont_resolve(has, cj, ch, ck, c, cy);
+        cont_resolve(has, cj, ch, ck, c);
 #pragma unroll
         for (int u = 0; u < kProbeILP; u++) {
             const uint64_t j = j0 + (uint64_t)u * kTPB;
-            // the bucket's slot words (S16: the key words of its two 16-byte slots)
-            const u64 sl[4] = {b0[u].x, S16 ? b1[u].x : b0[u].y, b1[u].x, b1[u].y};
+            const u64 sl[4] = {b0[u].x, b0[u].y, b1[u].x, b1[u].y};
             bool hit = false, done = j >= n2;
             uint32_t payload = 0;
-            u64 py = 0;
 #pragma unroll
             for (uint32_t i = 0; i < kB; i++) {
                 if (done) break;
                 const u64 w = sl[i];
                 if (w == kEmpty) done = true;
-                else if ((uint32_t)w == key[u]) {
-                    hit = done = true, payload = (uint32_t)(w >> 32);
-                    if (S16) py = i ? b1[u].y : b0[u].y;
-                }
+                else if ((uint32_t)w == key[u]) hit = done = true, payload = (uint32_t)(w >> 32);
             }
             // a full bucket without the key: on along the window, unless its mark
             // says no key homed here went on (j < n2 here)
@@ -1869,7 +1491,6 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             }
             nq += (uint32_t)__popcll(dm);
             if (j < n2 && !defer) probe_emit<RUNS>(j, hit, payload, pstart, rs, cnt, packed);
-            if (S16 && j < n2 && !defer) p01[j] = py;
             if (RUNS && wcnt) {
                 // packed runs: the word's run lengths, summed over the wave (a deferred
                 // row adds its own when it resolves), so no pass re-reads the payloads
@@ -1891,19 +1512,14 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
             const uint32_t nt = nq < 64 ? nq : 64;
             const bool hs = (uint32_t)lane < nt;
             uint32_t dj = 0, dh = 0, dk = 0;
-            u64 dc = 0, dy = 0;
+            u64 dc = 0;
             if (hs) {
                 const uint32_t e = nq - nt + (uint32_t)lane;
                 dj = qj[e], dh = qh[e], dk = qk[e];
-                if constexpr (S16) {
-                    const ulonglong2 v = words16[cont_slot(dk, dh)];
-                    dc = v.x, dy = v.y;
-                } else {
-                    dc = words[cont_slot(dk, dh)];
-                }
+                dc = words[cont_slot(dk, dh)];
             }
             nq -= nt;
-            cont_resolve(hs, dj, dh, dk, dc, dy);
+            cont_resolve(hs, dj, dh, dk, dc);
         }
     }
     // the queue's rest
@@ -1911,19 +1527,14 @@ __global__ __launch_bounds__(kTPB) void k_ht_probe_unique(const int* __restrict_
         const uint32_t nt = nq < 64 ? nq : 64;
         const bool hs = (uint32_t)lane < nt;
         uint32_t dj = 0, dh = 0, dk = 0;
-        u64 dc = 0, dy = 0;
+        u64 dc = 0;
         if (hs) {
             const uint32_t e = nq - nt + (uint32_t)lane;
             dj = qj[e], dh = qh[e], dk = qk[e];
-            if constexpr (S16) {
-                const ulonglong2 v = words16[cont_slot(dk, dh)];
-                dc = v.x, dy = v.y;
-            } else {
-                dc = words[cont_slot(dk, dh)];
-            }
+            dc = words[cont_slot(dk, dh)];
         }
         nq -= nt;
-        cont_resolve(hs, dj, dh, dk, dc, dy);
+        cont_resolve(hs, dj, dh, dk, dc);
     }
 }
 
@@ -2139,37 +1750,10 @@ __device__ __forceinline__ void run_decode(uint32_t pk, const uint32_t* __restri
     *L = pk ? l : 0u;
 }
 
-__global__ __launch_bounds__(kTPB) void k_join_write_runs(const uint32_t* __restrict__ pk, uint64_t n2,
-                                                          const uint32_t* __restrict__ rs,
-                                                          const u64* __restrict__ woffs, const int* __restrict__ p2,
-                                                          const int* __restrict__ bpos, int* __restrict__ out1,
-                                                          int* __restrict__ out2) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (n2 + 63) / 64;
-    const uint64_t wstride = (uint64_t)gridDim.x * (kTPB / 64);
-    for (uint64_t w = (uint64_t)blockIdx.x * (kTPB / 64) + (threadIdx.x >> 6); w < nw; w += wstride) {
-        const uint64_t j = w * 64 + (uint64_t)lane;
-        uint32_t a, L;
-        run_decode(j < n2 ? pk[j] : 0u, rs, &a, &L);
-        uint32_t incl = L;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (!L) continue;
-        const u64 o = woffs[w] + (u64)(incl - L);
-        const int pp = (p2 ? p2[j] : 0);
-        for (uint32_t t = 0; t < L; t++) {
-            out1[o + t] = bpos[a + t];
-            if (out2) out2[o + t] = pp;
-        }
-    }
-}
-
-// The same write with more reads in flight: a wave takes kWriteWords words at a time
-// (2^28 many-to-many, alternating on one box: 1 word 4.30, 4 words 4.00 ms; on another
-// 1 / 4 / 8 words 3.63-4.24 / 3.65-4.03 / 3.58-3.94 ms), and every row's first
+// The packed-runs write (a wave's 64 rows = one word; a row's offset = the word's + a
+// wave prefix of the lengths), with more reads in flight: a wave takes kWriteWords words
+// at a time (2^28 many-to-many, alternating on one box: 1 word 4.30, 4 words 4.00 ms; on
+// another 1 / 4 / 8 words 3.63-4.24 / 3.65-4.03 / 3.58-3.94 ms), and every row's first
 // two run positions (all of config 5's runs) are requested for
 // all of them before any pair is stored; longer runs finish in a loop. The run reads
 // are random (one line of the key-sorted positions per hit row), so the kernel is
@@ -2228,9 +1812,9 @@ __global__ __launch_bounds__(kTPB) void k_join_write_runs_mlp(const uint32_t* __
     }
 }
 
-// The write after a 16-byte-slot probe: a run of one or two rows comes from the
-// probe's per-row positions (p01, a stream), a longer one (3..14 rows) from the run
-// array as before.
+// The write after a run2 probe (the partitioned runs probe, k_win_probe_tab<u64>): a run
+// of one or two rows comes from the probe's per-row positions (p01, a stream), a longer
+// one (3..14 rows) from the run array as before.
 template <int kWriteWords>
 __global__ __launch_bounds__(kTPB) void k_join_write_runs16(const uint32_t* __restrict__ pk, uint64_t n2,
                                                             const u64* __restrict__ woffs, const int* __restrict__ p2,
@@ -2443,12 +2027,9 @@ struct mq_join {
     void* owned[16];       // device allocations owned by the handle
     int nowned;
     bool pruns;            // the last probe took the per-64-row-word form (packed runs of < 15 rows)
-    bool slot16;           // unique == 2: the 16-byte-slot table words16 (k_win_build_runs16), geometry win16
-    Win win16;
-    ulonglong2* words16;
     // probe state
     uint64_t n2, m;
-    u64* p01;              // slot16: per probe row, a short run's build positions
+    u64* p01;              // run2: per probe row, a short run's build positions
     uint32_t* pstart;
     uint32_t* plen;
     u64* offs;
@@ -2586,7 +2167,7 @@ int sample_has_dups(const int* c1, uint64_t n, uint32_t* dflag, hipStream_t st, 
 int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t slots,
                   uint32_t* general, hipStream_t st, const DevState* s, bool keep = false, int* pmm = nullptr) {
     const Win t = j->win;
-    j->marks = n >= kWindowBuildRows && !getenv("MQ_JOIN_NOMARKS");
+    j->marks = n >= kWindowBuildRows;
     if (n < kWindowBuildRows) {
         HIPCHK(hipMemsetAsync(j->words, 0xFF, slots * 8, st));
         hipLaunchKernelGGL(k_ht_insert_unique, dim3(stream_grid(s, n)), dim3(kTPB), 0, st, c1, p1,
@@ -2679,13 +2260,6 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     const char* e = getenv("MQ_JOIN_WINRUNS");  // "0": the sorted-runs build (A/B, tests)
     const char* r = getenv("MQ_JOIN_RUNS");     // "0": the global-CAS run table (tests)
     if ((e && e[0] == '0') || (r && r[0] == '0') || n < kWindowBuildRows || n > (1ull << 28) || j->win.wlog != kWinLog) return 1;
-    // MQ_JOIN_SLOT16=1: the 16-byte-slot table (k_win_build_runs16: as many slots, in a
-    // table of their own, same windows and partition). Measured and kept off: at 2^28
-    // many-to-many the write falls 3.93 -> 1.38 ms but the build rises 5.5 -> 7.2 (8 GB
-    // of table, one block a CU) and the probe 7.2 -> 8.4 ms (two-slot buckets): 16.9
-    // against 16.7 ms in total.
-    const char* e16 = getenv("MQ_JOIN_SLOT16");
-    const bool s16 = e16 && e16[0] == '1';
     const Win t = j->win;
     const uint64_t nslot = slots;
     int lg = 0;
@@ -2713,17 +2287,14 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     wstart = (uint32_t*)pool_alloc(((uint64_t)nw + 1) * 4);
     if (!a || (passes > 1 && !b) || !hist || !hscan || !scratch || !wstart)
         return done(set_err(MQ_ENOMEM, "join: window runs buffers (%llu rows)", (unsigned long long)n));
-    // bp and words16 join the handle only when the build takes this path
+    // bp joins the handle only when the build takes this path
     int* bp = (int*)pool_alloc(n * 4);
-    ulonglong2* w16 = s16 ? (ulonglong2*)pool_alloc(slots * 16) : nullptr;
     auto drop = [&](int rc) {
-        if (rc) (void)hipStreamSynchronize(st);  // (launched work may still use them)
-        pool_free_on(bp, st);
-        pool_free_on(w16, st);
+        pool_free_on(bp, st);  // (stream-ordered: launched work may still use it)
         return done(rc);
     };
     int rc = MQ_OK;
-    if (!bp || (s16 && !w16)) return drop(set_err(MQ_ENOMEM, "join: window runs outputs (%llu rows)", (unsigned long long)n));
+    if (!bp) return drop(set_err(MQ_ENOMEM, "join: window runs outputs (%llu rows)", (unsigned long long)n));
     u64* src = nullptr;
     u64* dst = a;
     for (int pass = 0; pass < passes; pass++) {
@@ -2748,10 +2319,7 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     uint32_t flag = 0;
     if (hipMemsetAsync(general, 0, 4, st) != hipSuccess) return drop(set_err(MQ_EHIP, "join: memset"));
     hipLaunchKernelGGL(k_win_bounds<u64>, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
-    if (s16)
-        hipLaunchKernelGGL(k_win_build_runs16, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, w16, bp, t, general);
-    else
-        hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
+    hipLaunchKernelGGL(k_win_build_runs, dim3(nw), dim3(kWinTPB), 0, st, src, wstart, j->words, bp, t, general);
     if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window runs build"));
     int sl[128];
     if (hipMemcpyAsync(&flag, general, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -2772,19 +2340,11 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     int* const bpos = bp;
     bp = nullptr;  // (jown frees it itself when it fails)
     if ((rc = jown(j, bpos))) return drop(rc);
-    if (w16) {
-        ulonglong2* const w = w16;
-        w16 = nullptr;
-        if ((rc = jown(j, w))) return drop(rc);
-        j->words16 = w;
-    }
     j->unique = 2;
     j->packed = true;
-    j->slot16 = s16;
-    j->win16 = t;
     j->rs = nullptr;  // packed lengths stay below 15: no run is looked up
     j->bpos = bpos;
-    j->marks = !getenv("MQ_JOIN_NOMARKS");
+    j->marks = true;
     return done(0);
 }
 
@@ -2848,72 +2408,16 @@ int build_runs(mq_join* j, const uint32_t* skeys, uint64_t n, uint64_t slots, ui
 
 namespace mqi {
 
-// The 4 passes; the last writes per `mode` (see k_sortw_scatter's LAST).
-int radix_sort_onesweep(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
-                        u64* pout, hipStream_t st, const DevState* s) {
-    const uint64_t ntiles = ceil_div(n, kSortTile);
-    const size_t stb = (size_t)ntiles * kRadix * 4;  // status words of one pass
-    u64* w0 = (u64*)pool_alloc(n * 8);
-    u64* w1 = (u64*)pool_alloc(n * 8);
-    uint32_t* meta = (uint32_t*)pool_alloc(4 * kRadix * 4 + 64 + stb);  // histograms, tickets, status
-    auto done = [&](int rc) {
-        pool_free_on(w0, st);
-        pool_free_on(w1, st);
-        pool_free_on(meta, st);
-        return rc;
-    };
-    if (!w0 || !w1 || !meta) return done(set_err(MQ_ENOMEM, "sort: buffers (%llu rows)", (unsigned long long)n));
-    uint32_t* gh = meta;
-    uint32_t* tickets = meta + 4 * kRadix;  // 4 passes
-    uint32_t* status = meta + 4 * kRadix + 16;
-    if (hipMemsetAsync(meta, 0, 4 * kRadix * 4 + 64, st) != hipSuccess) return done(set_err(MQ_EHIP, "sort: memset"));
-    hipLaunchKernelGGL(k_sort1_hist, dim3(stream_grid(s, ceil_div(n, kSortItems))), dim3(kTPB), 0, st, c1, n, gh);
-    hipLaunchKernelGGL(k_sort1_base, dim3(1), dim3(kTPB), 0, st, gh);
-    const dim3 g((uint32_t)ntiles), b(kTPB);
-    for (int pass = 0; pass < 4; pass++) {
-        const int shift = 8 * pass;
-        const uint32_t* gb = gh + pass * kRadix;
-        uint32_t* tk = tickets + pass;
-        if (hipMemsetAsync(status, 0, stb, st) != hipSuccess) return done(set_err(MQ_EHIP, "sort: memset"));
-        if (pass == 0)
-            hipLaunchKernelGGL((k_sort1_scatter<true, 0>), g, b, 0, st, c1, p1, nullptr, n, shift, gb, status, tk,
-                               w1, nullptr, nullptr, nullptr);
-        else if (pass < 3)
-            hipLaunchKernelGGL((k_sort1_scatter<false, 0>), g, b, 0, st, nullptr, nullptr, w0, n, shift, gb, status,
-                               tk, w1, nullptr, nullptr, nullptr);
-        else if (mode == 1)
-            hipLaunchKernelGGL((k_sort1_scatter<false, 1>), g, b, 0, st, nullptr, nullptr, w0, n, shift, gb, status,
-                               tk, nullptr, kout, vout, nullptr);
-        else
-            hipLaunchKernelGGL((k_sort1_scatter<false, 2>), g, b, 0, st, nullptr, nullptr, w0, n, shift, gb, status,
-                               tk, nullptr, kout, nullptr, pout);
-        if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "sort: launch"));
-        u64* t = w0;
-        w0 = w1;
-        w1 = t;
-    }
-    if (hipStreamSynchronize(st) != hipSuccess) return done(set_err(MQ_EHIP, "sort: sync"));
-    return done(MQ_OK);
-}
-
 template <int TPB, int IT>
 int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_t kmin, int npass, uint32_t* kout,
                      uint32_t* vout, u64* pout, hipStream_t st);
 
 int radix_sort_run(const int* c1, const int* p1, uint64_t n, int mode, uint32_t* kout, uint32_t* vout,
                    u64* pout, hipStream_t st) {
-    // MQ_SORT_IMPL=onesweep: decoupled look-back instead of a histogram pass per pass.
-    // Measured slower here (1e9-row index 27.9 vs 22.3 ms: its scatter passes 6.3-7.1
-    // ms against 3.7-4.4 ms + 1.6 ms of histogram; right after launch every resident
-    // tile walks back over ~2000 unfinished predecessors through cross-XCD status
-    // loads), so the histogram + scan form stays the default.
-    const char* impl = getenv("MQ_SORT_IMPL");
-    if (n < (1ull << 30) && impl && strcmp(impl, "onesweep") == 0) {
-        DevState* s;
-        int rc = ensure_ready(&s);
-        if (rc) return rc;
-        return radix_sort_onesweep(c1, p1, n, mode, kout, vout, pout, st, s);
-    }
+    // (A onesweep form, decoupled look-back instead of a histogram pass per pass, measured
+    // slower and was removed in round 6: 1e9-row index 27.9 vs 22.3 ms, its scatter passes
+    // 6.3-7.1 ms against 3.7-4.4 + 1.6 ms of histogram; right after launch every resident
+    // tile walked back over ~2000 unfinished predecessors through cross-XCD status loads.)
     // tiles of 512 x 16 words: 18.7 ms for the 1e9-row index, against 21.6 with
     // 256 x 16 (digit runs of 16 words leave the block as 128-B pieces), 25.9 with
     // 1024 x 8 and 22.3 with 512 x 8 (tools/sorttpb_cmd.sh)
@@ -2942,8 +2446,7 @@ int radix_sort_tiles(const int* c1, const int* p1, uint64_t n, int mode, uint32_
     };
     if (npass < 1 || npass > 4) return set_err(MQ_EINVAL, "sort: %d passes", npass);
     w0 = (u64*)pool_alloc(n * 8);
-    const char* de = getenv("MQ_SORT_DIGITS");
-    const bool use_dig = npass > 1 && !(de && de[0] == '0');
+    const bool use_dig = npass > 1;
     if (use_dig) dig = (uint8_t*)pool_alloc(n + 16);
     w1 = (u64*)pool_alloc(n * 8);
     hist = (uint32_t*)pool_alloc(nh * 4);
@@ -3328,15 +2831,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     const uint64_t nw = (n2 + 63) / 64;
     const uint64_t nscan = words_scan ? nw : n2;
     uint32_t* const cnt = j->unique == 1 ? j->plen + 2 * nw : j->plen;
-    if (pruns && j->slot16) {  // 16-byte slots: payloads, short runs' positions, word run lengths
-        if (!(j->p01 = (u64*)pool_alloc(n2 * 8))) return set_err(MQ_ENOMEM, "mq_join_probe: positions");
-        auto kern = k_ht_probe_unique<true, true>;
-        hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB),
-                           0, st, d_c2, n2, reinterpret_cast<const u64*>(j->words16), j->win16, j->pstart,
-                           (u64*)nullptr, j->rs, (uint32_t*)nullptr,
-                           true, j->marks, cnt, j->p01);
-        LAUNCHCHK("k_ht_probe_unique");
-    } else if (pruns && j->win.wlog == kWinLog && j->n1 >= part_min_rows() && n2 >= j->n1 / (pdiv ? pdiv : 1)) {
+    if (pruns && j->win.wlog == kWinLog && j->n1 >= part_min_rows() && n2 >= j->n1 / (pdiv ? pdiv : 1)) {
         // packed runs, partitioned: the probe keys by window, each window's table slice in LDS;
         // with a marker outside the payloads the short runs' positions ride along (run2)
         j->run2 = j->rsent_ok && !(getenv("MQ_JOIN_RUN2") && getenv("MQ_JOIN_RUN2")[0] == '0');
@@ -3345,14 +2840,13 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     } else if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
-                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks, cnt,
-                           (u64*)nullptr);
+                           j->words, j->win, j->pstart, (u64*)nullptr, j->rs, (uint32_t*)nullptr, true, j->marks, cnt);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique == 2) {  // runs: each row's run start and length straight from the probe
         auto kern = k_ht_probe_unique<true>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks,
-                           (uint32_t*)nullptr, (u64*)nullptr);
+                           (uint32_t*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
     } else if (j->unique && j->part) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
@@ -3365,7 +2859,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
         auto kern = k_ht_probe_unique<false>;
         hipLaunchKernelGGL(kern, dim3(resident_grid(s, (n2 + kProbeILP - 1) / kProbeILP, (const void*)kern)), dim3(kTPB), 0, st, d_c2, n2,
                            j->words, j->win, j->pstart, hits, (const uint32_t*)nullptr, (uint32_t*)nullptr, false, j->marks,
-                           (uint32_t*)nullptr, (u64*)nullptr);
+                           (uint32_t*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
         hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
         LAUNCHCHK("k_hits_count");
@@ -3400,8 +2894,7 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (!d_out1 || (d_out2 && !d_p2)) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
     if ((rc = juse(j, (hipStream_t)stream))) return rc;
     if (j->unique == 1) {
-        const bool v4 = ((reinterpret_cast<uintptr_t>(j->pstart) | reinterpret_cast<uintptr_t>(d_p2)) & 15u) == 0 &&
-                        !(getenv("MQ_JOIN_WRITE1") && getenv("MQ_JOIN_WRITE1")[0] == '1');
+        const bool v4 = ((reinterpret_cast<uintptr_t>(j->pstart) | reinterpret_cast<uintptr_t>(d_p2)) & 15u) == 0;
         if (v4)
             hipLaunchKernelGGL(k_join_write_hits4, dim3(stream_grid(s, (j->n2 + 3) / 4)), dim3(kTPB), 0,
                                (hipStream_t)stream, reinterpret_cast<const u64*>(j->plen), j->offs, j->pstart, d_p2,
@@ -3412,31 +2905,15 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         LAUNCHCHK("k_join_write_hits");
         return MQ_OK;
     }
-    if (j->pruns && (j->slot16 || j->run2)) {
+    if (j->pruns && j->run2) {
         hipLaunchKernelGGL(k_join_write_runs16<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)), dim3(kTPB), 0,
                            (hipStream_t)stream, j->pstart, j->n2, j->offs, d_p2, j->p01, j->bpos, d_out1, d_out2);
         LAUNCHCHK("k_join_write_runs16");
         return MQ_OK;
     }
     if (j->pruns) {
-        // MQ_JOIN_WRITE (A/B): "1" one word per wave at a time, "4" four, "16" sixteen
-        // (176 VGPRs, two waves a SIMD; not measured yet), default eight
-        const char* wf = getenv("MQ_JOIN_WRITE");
-        if (wf && wf[0] == '1' && wf[1] == 0)
-            hipLaunchKernelGGL(k_join_write_runs, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64)), dim3(kTPB), 0,
-                               (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
-        else if (wf && wf[0] == '1' && wf[1] == '6')
-            hipLaunchKernelGGL(k_join_write_runs_mlp<16>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 16)),
-                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
-                               d_out1, d_out2);
-        else if (wf && wf[0] == '4')
-            hipLaunchKernelGGL(k_join_write_runs_mlp<4>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 4)),
-                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
-                               d_out1, d_out2);
-        else
-            hipLaunchKernelGGL(k_join_write_runs_mlp<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)),
-                               dim3(kTPB), 0, (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos,
-                               d_out1, d_out2);
+        hipLaunchKernelGGL(k_join_write_runs_mlp<8>, dim3(stream_grid(s, ((j->n2 + 63) / 64) * 64 / 8)), dim3(kTPB), 0,
+                           (hipStream_t)stream, j->pstart, j->n2, j->rs, j->offs, d_p2, j->bpos, d_out1, d_out2);
         LAUNCHCHK("k_join_write_runs");
         return MQ_OK;
     }

@@ -59,9 +59,6 @@ namespace {
 
 using namespace mqi;
 
-constexpr int kCompactTPB = 1024;         // compaction block: 16 wave64
-constexpr int kCompactWaves = kCompactTPB / 64;
-
 __device__ __forceinline__ void store_agent(unsigned long long* p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -214,37 +211,23 @@ __device__ __forceinline__ void block_combine(const Partial* __restrict__ part, 
 // k_scan: one streaming pass over a contiguous chunk of the column.
 //   kSum   : count + int64 sum of the matching values (select + sum, the metric)
 //   kAgg   : count + sum + min + max                       (query.c:306-354, 392-437)
-//   kAux   : the same aggregates of aux[row] over the rows whose col[row] matches
-//            (select -> fetch -> agg fused, config 3; query.c:92-137 + 223-243)
-//   kMask  : count per block + one predicate bit per row (first half of the
-//            ordered compaction)
+// (select -> fetch -> agg fused, config 3, is k_scan_gather below.)
 // Loads are non-temporal dwordx4 (global_load_dwordx4 ... nt): the column is read
 // once, and keeping it out of the caches measured 0.586 vs 0.631 ms per 1e9 rows.
 // Arithmetic runs on d = v - low (unsigned): a row matches iff d <= wm1, so
 //   sum = sum(d) + count * low,  min = low + min(d),  max = low + wm1 - min(wm1 - d)
 // where the min()s run over ALL rows of a full tile unmasked: a non-matching row
 // has d > wm1 and wm1 - d > wm1, so it can never win.
-// Mask word layout: masks[(tile*4 + wave)*4 + e] bit l = row tile*1024 + wave*256
-// + 4*l + e, so a chunk's 256-row groups are contiguous 32-byte records.
 // ---------------------------------------------------------------------------
-enum ScanMode { kSum = 0, kAgg = 1, kAux = 2, kMask = 3 };
-
-// Mask layout: per 8192-row super-tile S and wave w, a 32-word (256-B) record;
-// word u*4 + e, bit l <-> row S*8192 + u*1024 + w*256 + 4*l + e. Returns the record
-// start for the super-tile holding 1024-row tile T.
-__device__ __forceinline__ uint64_t mask_word(uint64_t T, int wave) {
-    return ((T >> 3) * kWaves + (uint64_t)wave) * 32;
-}
+enum ScanMode { kSum = 0, kAgg = 1 };
 
 template <int MODE>
 struct ScanTraits {
-    static constexpr int kUnrollM = MODE == kAux ? 4 : (MODE == kAgg ? 6 : kUnroll);
-    static constexpr int kMinWaves = MODE == kAux ? 4 : 8;
+    static constexpr int kUnrollM = MODE == kAgg ? 6 : kUnroll;
 };
 
 template <int MODE, bool VEC>
-__global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(const int* __restrict__ col,
-                                               const int* __restrict__ aux, uint64_t n,
+__global__ __launch_bounds__(kTPB, 8) void k_scan(const int* __restrict__ col, uint64_t n,
                                                uint64_t rows_per_block, Pred pred,
                                                Partial* __restrict__ part,
                                                mq_agg* __restrict__ out, unsigned int* __restrict__ arrive) {
@@ -258,8 +241,6 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
     unsigned long long sumd = 0;       // kSum/kAgg: sum of d over matches
     uint32_t mind = 0xFFFFFFFFu;       // kAgg: min d
     uint32_t maxr = 0xFFFFFFFFu;       // kAgg: min (wm1 - d)
-    long long sumv = 0;                // kAux: sum of aux values
-    int mnv = INT_MAX, mxv = INT_MIN;  // kAux
 
     // FULL: all 4 rows valid (no per-row bound check, unmasked min()s)
     auto consume = [&](int4 v, uint64_t tile_row, bool full) {
@@ -274,26 +255,16 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
             p3 = p3 && (row + 3 < end);
         }
         cnt += (unsigned)p0 + (unsigned)p1 + (unsigned)p2 + (unsigned)p3;
-        if constexpr (MODE == kAux) {
-            const int a0 = p0 ? aux[row + 0] : 0, a1 = p1 ? aux[row + 1] : 0,
-                      a2 = p2 ? aux[row + 2] : 0, a3 = p3 ? aux[row + 3] : 0;
-            sumv += (long long)a0 + (long long)a1 + (long long)a2 + (long long)a3;
-            mnv = min(mnv, min(min(p0 ? a0 : INT_MAX, p1 ? a1 : INT_MAX),
-                               min(p2 ? a2 : INT_MAX, p3 ? a3 : INT_MAX)));
-            mxv = max(mxv, max(max(p0 ? a0 : INT_MIN, p1 ? a1 : INT_MIN),
-                               max(p2 ? a2 : INT_MIN, p3 ? a3 : INT_MIN)));
-        } else {
-            sumd += (unsigned long long)(p0 ? d0 : 0u) + (unsigned long long)(p1 ? d1 : 0u) +
-                    (unsigned long long)(p2 ? d2 : 0u) + (unsigned long long)(p3 ? d3 : 0u);
-            if constexpr (MODE == kAgg) {
-                if (full) {
-                    mind = min(mind, min(min(d0, d1), min(d2, d3)));
-                    maxr = min(maxr, min(min(wm1 - d0, wm1 - d1), min(wm1 - d2, wm1 - d3)));
-                } else {
-                    mind = min(mind, min(min(p0 ? d0 : ~0u, p1 ? d1 : ~0u), min(p2 ? d2 : ~0u, p3 ? d3 : ~0u)));
-                    maxr = min(maxr, min(min(p0 ? wm1 - d0 : ~0u, p1 ? wm1 - d1 : ~0u),
-                                         min(p2 ? wm1 - d2 : ~0u, p3 ? wm1 - d3 : ~0u)));
-                }
+        sumd += (unsigned long long)(p0 ? d0 : 0u) + (unsigned long long)(p1 ? d1 : 0u) +
+                (unsigned long long)(p2 ? d2 : 0u) + (unsigned long long)(p3 ? d3 : 0u);
+        if constexpr (MODE == kAgg) {
+            if (full) {
+                mind = min(mind, min(min(d0, d1), min(d2, d3)));
+                maxr = min(maxr, min(min(wm1 - d0, wm1 - d1), min(wm1 - d2, wm1 - d3)));
+            } else {
+                mind = min(mind, min(min(p0 ? d0 : ~0u, p1 ? d1 : ~0u), min(p2 ? d2 : ~0u, p3 ? d3 : ~0u)));
+                maxr = min(maxr, min(min(p0 ? wm1 - d0 : ~0u, p1 ? wm1 - d1 : ~0u),
+                                     min(p2 ? wm1 - d2 : ~0u, p3 ? wm1 - d3 : ~0u)));
             }
         }
     };
@@ -324,18 +295,11 @@ __global__ __launch_bounds__(kTPB, ScanTraits<MODE>::kMinWaves) void k_scan(cons
         consume(v, t, row + 3 < end);
     }
     // Back from d-space to values (exact: low + d never wraps for a matching row).
-    long long sum;
+    const long long sum = (long long)sumd + (long long)cnt * (long long)(int32_t)lo;
     int mn = INT_MAX, mx = INT_MIN;
-    if constexpr (MODE == kAux) {
-        sum = sumv;
-        mn = mnv;
-        mx = mxv;
-    } else {
-        sum = (long long)sumd + (long long)cnt * (long long)(int32_t)lo;
-        if (MODE == kAgg && cnt) {
-            mn = (int)(lo + mind);
-            mx = (int)(lo + (wm1 - maxr));
-        }
+    if (MODE == kAgg && cnt) {
+        mn = (int)(lo + mind);
+        mx = (int)(lo + (wm1 - maxr));
     }
     // out != nullptr: the last block to finish folds all partials (no k_final launch)
     if (out) {
@@ -373,85 +337,6 @@ __global__ __launch_bounds__(kTPB, 8) void k_stream_read(const int* __restrict__
     if ((tid & 63) == 0) atomicXor(out + blockIdx.x, x);
 }
 
-// ---------------------------------------------------------------------------
-// k_mask: first half of the ordered compaction. Streams the chunk like k_scan
-// (nt dwordx4, 8 tiles in flight) and writes one predicate bit per row plus a
-// count per block. Per 8-tile super-tile the wave's 32 row compares (tile u, row
-// e of each lane's dwordx4) are 32 ballots; ballot 4u+e is placed in lane 4u+e
-// with v_writelane, and the wave stores its 256-byte record with one instruction.
-// (Packing bits per lane and transposing them with 32 more ballots cost 48 us per
-// 1e9 rows; writelane removes the pack and the transpose.)
-// ---------------------------------------------------------------------------
-
-template <bool VEC>
-__global__ __launch_bounds__(kTPB, 8) void k_mask(const int* __restrict__ col, uint64_t n,
-                                                  uint64_t rows_per_block, Pred pred,
-                                                  Partial* __restrict__ part,
-                                                  unsigned long long* __restrict__ masks) {
-    const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
-    uint64_t end = start + rows_per_block;
-    if (end > n) end = n;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t lo = pred.lo, wm1 = pred.wm1;
-    unsigned int cnt = 0;
-    uint64_t t = start;  // 8192-row aligned (geometry granule)
-    // The record of super-tile i is stored after super-tile i+1's loads are issued:
-    // vmcnt counts stores and loads in order, so a store issued before the loads
-    // would add its write round trip to every iteration.
-    unsigned long long pending = 0;
-    uint64_t pending_at = ~0ull;
-    for (; t + 8ull * kTileRows <= end; t += 8ull * kTileRows) {
-        int4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kTileRows + (uint64_t)tid * 4);
-        if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;
-        // the row compares are the record words: ballot (u, e) goes to lane 4u + e
-        int wlo = 0, whi = 0;
-        unsigned int c = 0;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const unsigned long long m0 = __ballot(((uint32_t)v[u].x - lo) <= wm1),
-                                     m1 = __ballot(((uint32_t)v[u].y - lo) <= wm1),
-                                     m2 = __ballot(((uint32_t)v[u].z - lo) <= wm1),
-                                     m3 = __ballot(((uint32_t)v[u].w - lo) <= wm1);
-            c += (unsigned)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
-            wlo = mq_writelane((int)m0, 4 * u + 0, wlo);
-            whi = mq_writelane((int)(m0 >> 32), 4 * u + 0, whi);
-            wlo = mq_writelane((int)m1, 4 * u + 1, wlo);
-            whi = mq_writelane((int)(m1 >> 32), 4 * u + 1, whi);
-            wlo = mq_writelane((int)m2, 4 * u + 2, wlo);
-            whi = mq_writelane((int)(m2 >> 32), 4 * u + 2, whi);
-            wlo = mq_writelane((int)m3, 4 * u + 3, wlo);
-            whi = mq_writelane((int)(m3 >> 32), 4 * u + 3, whi);
-        }
-        if (lane == 0) cnt += c;  // c is wave-uniform: count it once per wave
-        pending = (unsigned long long)(uint32_t)wlo | ((unsigned long long)(uint32_t)whi << 32);
-        pending_at = mask_word(t / kTileRows, wave);
-    }
-    if (pending_at != ~0ull && lane < 32) masks[pending_at + lane] = pending;
-    for (; t < end; t += kTileRows) {  // the last chunk's tail, tile by tile
-        const uint64_t row = t + (uint64_t)tid * 4;
-        int4 v;
-        v.x = row + 0 < end ? col[row + 0] : 0;
-        v.y = row + 1 < end ? col[row + 1] : 0;
-        v.z = row + 2 < end ? col[row + 2] : 0;
-        v.w = row + 3 < end ? col[row + 3] : 0;
-        const bool p0 = ((uint32_t)v.x - lo) <= wm1 && row + 0 < end,
-                   p1 = ((uint32_t)v.y - lo) <= wm1 && row + 1 < end,
-                   p2 = ((uint32_t)v.z - lo) <= wm1 && row + 2 < end,
-                   p3 = ((uint32_t)v.w - lo) <= wm1 && row + 3 < end;
-        cnt += (unsigned)p0 + (unsigned)p1 + (unsigned)p2 + (unsigned)p3;
-        const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1), m2 = __ballot(p2),
-                                 m3 = __ballot(p3);
-        const uint64_t T = t / kTileRows;
-        if (lane < 4)
-            masks[mask_word(T, wave) + (T & 7) * 4 + lane] =
-                lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
-    }
-    block_store_partial(cnt, 0, INT_MAX, INT_MIN, part);
-}
-
 // One block combines the per-block partials into the final aggregate.
 __global__ __launch_bounds__(kTPB) void k_final(const Partial* __restrict__ part, uint32_t nparts,
                                                 mq_agg* __restrict__ out) {
@@ -486,304 +371,6 @@ __global__ __launch_bounds__(kTPB) void k_final(const Partial* __restrict__ part
         out->min = r.mn;
         out->max = r.mx;
         out->_pad = 0;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_compact: predicate bits -> ascending position list (second half of the
-// ordered compaction). Block b re-walks the chunk of scan block b; its output
-// base is the sum of the counts of blocks 0..b-1. One LANE per 256-row group:
-// the lane loads its group's four mask words (32 contiguous bytes), a block-wide
-// scan of the popcounts gives each group's offset, and the lane emits its rows in
-// ascending order (row = group + 4*l + e for bit l of word e). The mask stream is
-// N/8 bytes; the work per lane is its group's match count.
-// ---------------------------------------------------------------------------
-template <bool PAYLOAD>
-__global__ __launch_bounds__(kCompactTPB) void k_compact(
-    const unsigned long long* __restrict__ masks, const Partial* __restrict__ part,
-    const int* __restrict__ payload, uint64_t n, uint64_t rows_per_block, int* __restrict__ out,
-    unsigned long long* __restrict__ d_count) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    __shared__ unsigned long long s_red[kCompactWaves];
-    __shared__ unsigned int s_wtot[kCompactWaves];
-
-    unsigned long long acc = 0;
-    for (uint32_t i = tid; i < blockIdx.x; i += kCompactTPB) acc += part[i].count;
-    acc = wave_sum_u64(acc);
-    if (lane == 0) s_red[wave] = acc;
-    __syncthreads();
-    unsigned long long base = 0;
-#pragma unroll
-    for (int w = 0; w < kCompactWaves; w++) base += s_red[w];
-    const unsigned long long mine = part[blockIdx.x].count;
-    if (blockIdx.x == gridDim.x - 1 && tid == 0) *d_count = base + mine;
-    if (mine == 0) return;  // uniform across the block
-
-    const uint64_t start = (uint64_t)blockIdx.x * rows_per_block;
-    uint64_t end = start + rows_per_block;
-    if (end > n) end = n;
-    const uint64_t ngroups = ((end - start + kTileRows - 1) / kTileRows) * kWaves;
-    const uint64_t T0 = start / kTileRows;  // first 1024-row tile of the chunk
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    unsigned long long running = base;
-    for (uint64_t g0 = 0; g0 < ngroups; g0 += kCompactTPB) {
-        // group g (row order) = tile T0 + g/4, wave g%4
-        const uint64_t g = g0 + (uint64_t)tid;
-        unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        if (g < ngroups) {
-            const uint64_t T = T0 + (g >> 2);
-            const unsigned long long* rec = masks + mask_word(T, (int)(g & 3)) + (T & 7) * 4;
-            const ulonglong2 a = reinterpret_cast<const ulonglong2*>(rec)[0];
-            const ulonglong2 b = reinterpret_cast<const ulonglong2*>(rec)[1];
-            w0 = a.x;
-            w1 = a.y;
-            w2 = b.x;
-            w3 = b.y;
-        }
-        const unsigned int c = (unsigned int)(__popcll(w0) + __popcll(w1) + __popcll(w2) + __popcll(w3));
-        unsigned int incl = c;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned int y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        if (lane == 63) s_wtot[wave] = incl;
-        __syncthreads();
-        unsigned long long woff = 0, rtot = 0;
-#pragma unroll
-        for (int w = 0; w < kCompactWaves; w++) {
-            const unsigned int x = s_wtot[w];
-            if (w < wave) woff += x;
-            rtot += x;
-        }
-        __syncthreads();  // s_wtot is rewritten next round
-        const unsigned long long o = running + woff + (incl - c);
-        running += rtot;
-        const uint64_t row0 = start + (g >> 2) * kTileRows + (g & 3) * 256;
-        const unsigned int wave_total = __shfl(incl, 63, 64);
-        if (wave_total > 1024) {
-            // dense: the whole wave writes one group at a time (lane l -> rows 4l+e)
-            for (int j = 0; j < 64; j++) {
-                if (__shfl(c, j, 64) == 0) continue;
-                const unsigned long long x0 = __shfl(w0, j, 64), x1 = __shfl(w1, j, 64),
-                                         x2 = __shfl(w2, j, 64), x3 = __shfl(w3, j, 64);
-                const unsigned long long oj = __shfl(o, j, 64);
-                const uint64_t rj = __shfl(row0, j, 64) + 4 * (uint64_t)lane;
-                const unsigned int pre = (unsigned int)(__popcll(x0 & ltmask) + __popcll(x1 & ltmask) +
-                                                        __popcll(x2 & ltmask) + __popcll(x3 & ltmask));
-                int* q = out + oj + pre;
-                unsigned int k = 0;
-                if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 0] : (int)(rj + 0);
-                if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 1] : (int)(rj + 1);
-                if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 2] : (int)(rj + 2);
-                if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? payload[rj + 3] : (int)(rj + 3);
-            }
-        } else if (c) {
-            // sparse: each lane emits its own group's rows in order
-            unsigned long long oo = o;
-            unsigned long long m = w0 | w1 | w2 | w3;
-            while (m) {
-                const int l = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const uint64_t r = row0 + 4 * (uint64_t)l;
-                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0);
-                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1);
-                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2);
-                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3);
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_select_lb: ordered compaction in ONE pass (32768-row tiles read as 8 passes) (select_column_scan / select_result,
-// query.c:38-137) by decoupled look-back over in-order tiles.
-//   * persistent blocks take 8192-row tiles from an atomic ticket, one at a time,
-//     when they can start them; a block only ever waits on tiles with lower
-//     tickets, all held by running blocks, so progress does not depend on how
-//     many blocks are resident;
-//   * each tile publishes its match count as a 64-bit status word {flag:2, value:62}
-//     with one relaxed agent-scope atomic store (the data is the flag: no separate
-//     payload, no fence — MI355X_MICROARCH.md §visibility, granule form);
-//   * wave 0 looks back 64 status words per step (relaxed agent-scope loads) to the
-//     nearest inclusive prefix, then the tile publishes its own inclusive prefix;
-//   * rows are written in ascending order: (sub-tile u, wave, lane, element) order
-//     is row order, ranks come from ballots.
-// HBM traffic 4N (nt loads) + 4K (+ payload gathers for select_result).
-// Spins are bounded (err flag set, never a hang).
-// ---------------------------------------------------------------------------
-constexpr int kLbUnroll = 4;                       // dwordx4 per lane per pass
-constexpr int kLbPassRows = kTPB * 4 * kLbUnroll;  // 4096 rows per pass
-constexpr int kLbPasses = 8;                       // passes per tile (bits kept in LDS)
-constexpr int kLbTileRows = kLbPassRows * kLbPasses;  // 32768 rows per ticket
-constexpr unsigned long long kStA = 1ull << 62;    // aggregate published
-constexpr unsigned long long kStP = 2ull << 62;    // inclusive prefix published
-constexpr unsigned long long kStVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ void st_status(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_status(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One pass = kLbUnroll dwordx4 per lane; bit 4u+e of its predicate word is row
-// pass_base + u*1024 + tid*4 + e.
-template <bool VEC>
-__device__ __forceinline__ void pass_load(int4 (&v)[kLbUnroll], const int* __restrict__ col,
-                                          uint64_t pass_base, uint64_t n, int tid) {
-#pragma unroll
-    for (int u = 0; u < kLbUnroll; u++) {
-        const uint64_t row = pass_base + (uint64_t)u * kTileRows + (uint64_t)tid * 4;
-        if (row + 3 < n) {
-            v[u] = load4_nt<VEC>(col + row);
-        } else {
-            v[u].x = row + 0 < n ? col[row + 0] : 0;
-            v[u].y = row + 1 < n ? col[row + 1] : 0;
-            v[u].z = row + 2 < n ? col[row + 2] : 0;
-            v[u].w = row + 3 < n ? col[row + 3] : 0;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t pass_bits(const int4 (&v)[kLbUnroll], uint64_t pass_base,
-                                              uint64_t n, uint32_t lo, uint32_t wm1, int tid) {
-    uint32_t pbits = 0;
-#pragma unroll
-    for (int u = 0; u < kLbUnroll; u++) {
-        const uint64_t row = pass_base + (uint64_t)u * kTileRows + (uint64_t)tid * 4;
-        const bool full = row + 3 < n;
-        const uint32_t b = (((uint32_t)v[u].x - lo) <= wm1 && (full || row + 0 < n) ? 1u : 0u) |
-                           (((uint32_t)v[u].y - lo) <= wm1 && (full || row + 1 < n) ? 2u : 0u) |
-                           (((uint32_t)v[u].z - lo) <= wm1 && (full || row + 2 < n) ? 4u : 0u) |
-                           (((uint32_t)v[u].w - lo) <= wm1 && (full || row + 3 < n) ? 8u : 0u);
-        pbits |= b << (4 * u);
-    }
-    return pbits;
-}
-
-__device__ __forceinline__ void count_pass(uint32_t pbits, int ps, int tid, int lane, int wave,
-                                           uint32_t (*s_bits)[kTPB], unsigned int* s_cnt) {
-    s_bits[ps][tid] = pbits;
-#pragma unroll
-    for (int u = 0; u < kLbUnroll; u++) {
-        const uint32_t b = pbits >> (4 * u);
-        const unsigned int c = (unsigned int)(__popcll(__ballot(b & 1u)) + __popcll(__ballot(b & 2u)) +
-                                              __popcll(__ballot(b & 4u)) + __popcll(__ballot(b & 8u)));
-        if (lane == 0) s_cnt[(ps * kLbUnroll + u) * kWaves + wave] = c;
-    }
-}
-
-template <bool PAYLOAD, bool VEC>
-__global__ __launch_bounds__(kTPB, 7) void k_select_lb(
-    const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, Pred pred,
-    unsigned long long* status, unsigned int* ticket, uint32_t ntiles, int* __restrict__ out,
-    unsigned long long* __restrict__ d_count, unsigned int* __restrict__ err) {
-    constexpr int kGroups = kLbPasses * kLbUnroll;  // (pass, u) sub-tiles of 1024 rows
-    __shared__ unsigned int s_tile;
-    __shared__ unsigned int s_cnt[kGroups * kWaves];
-    __shared__ uint32_t s_bits[kLbPasses][kTPB];
-    __shared__ unsigned long long s_excl;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t lo = pred.lo, wm1 = pred.wm1;
-    while (true) {
-        // Take the next tile only when this block can start it at once: a ticket
-        // held while its block is still busy would stall every later tile's look-back.
-        __syncthreads();  // the previous tile is done with s_tile / s_cnt / s_excl
-        if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-        __syncthreads();
-        const unsigned int tile = s_tile;
-        if (tile >= ntiles) break;
-        const uint64_t base = (uint64_t)tile * kLbTileRows;
-        // ---- predicate bits of all passes (kept in LDS); per-(pass, u, wave) counts.
-        // Software-pipelined: pass ps+1's loads are in flight while pass ps is counted.
-        int4 va[kLbUnroll], vb[kLbUnroll];
-        pass_load<VEC>(va, col, base, n, tid);
-#pragma unroll 1
-        for (int ps = 0; ps < kLbPasses; ps += 2) {
-            pass_load<VEC>(vb, col, base + (uint64_t)(ps + 1) * kLbPassRows, n, tid);
-            count_pass(pass_bits(va, base + (uint64_t)ps * kLbPassRows, n, lo, wm1, tid), ps, tid,
-                       lane, wave, s_bits, s_cnt);
-            if (ps + 2 < kLbPasses) pass_load<VEC>(va, col, base + (uint64_t)(ps + 2) * kLbPassRows, n, tid);
-            count_pass(pass_bits(vb, base + (uint64_t)(ps + 1) * kLbPassRows, n, lo, wm1, tid), ps + 1,
-                       tid, lane, wave, s_bits, s_cnt);
-        }
-        __syncthreads();
-        unsigned int tot = 0;
-#pragma unroll
-        for (int i = 0; i < kGroups * kWaves; i++) tot += s_cnt[i];
-        // ---- publish aggregate, look back, publish inclusive prefix
-        if (wave == 0) {
-            unsigned long long excl = 0;
-            if (tile == 0) {
-                if (lane == 0) st_status(&status[0], kStP | (unsigned long long)tot);
-            } else {
-                if (lane == 0) st_status(&status[tile], kStA | (unsigned long long)tot);
-                long long pos = (long long)tile - 1;
-                unsigned int spins = 0;
-                while (true) {
-                    const long long idx = pos - lane;
-                    const unsigned long long st = idx >= 0 ? ld_status(&status[idx]) : kStP;
-                    const unsigned long long flag = st & ~kStVal;
-                    const unsigned long long pmask = __ballot(flag == kStP);
-                    const unsigned long long zmask = __ballot(flag == 0ull);
-                    // lanes [0, nearest inclusive prefix] must all have published
-                    const unsigned long long upto = pmask ? ((pmask & (~pmask + 1)) << 1) - 1 : ~0ull;
-                    if (zmask & upto) {
-                        if (++spins > (1u << 24)) {  // never expected; fail loudly, never hang
-                            if (lane == 0) atomicOr(err, 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    const unsigned long long val = ((1ull << lane) & upto) ? (st & kStVal) : 0ull;
-                    excl += wave_sum_u64(val);
-                    if (pmask) break;
-                    pos -= 64;
-                }
-                if (lane == 0) st_status(&status[tile], kStP | (excl + tot));
-            }
-            if (lane == 0) {
-                s_excl = excl;
-                if (tile == ntiles - 1) *d_count = excl + tot;
-            }
-        }
-        __syncthreads();
-        // ---- write positions in row order: (pass, u, wave, lane, element)
-        unsigned long long off = s_excl;
-#pragma unroll 1
-        for (int ps = 0; ps < kLbPasses; ps++) {
-            const uint32_t pbits = s_bits[ps][tid];
-#pragma unroll
-            for (int u = 0; u < kLbUnroll; u++) {
-                const int g = ps * kLbUnroll + u;
-                unsigned long long o_uw = off;
-#pragma unroll
-                for (int w = 0; w < kWaves; w++) {
-                    const unsigned int c = s_cnt[g * kWaves + w];
-                    if (w < wave) o_uw += c;
-                    off += c;
-                }
-                if (s_cnt[g * kWaves + wave] != 0) {  // uniform in the wave
-                    const uint32_t b = (pbits >> (4 * u)) & 0xFu;
-                    const unsigned long long m0 = __ballot(b & 1u), m1 = __ballot(b & 2u),
-                                             m2 = __ballot(b & 4u), m3 = __ballot(b & 8u);
-                    const unsigned int pre =
-                        (unsigned int)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) +
-                                       __popcll(m2 & ltmask) + __popcll(m3 & ltmask));
-                    const uint64_t row = base + (uint64_t)ps * kLbPassRows +
-                                         (uint64_t)u * kTileRows + (uint64_t)tid * 4;
-                    int* o = out + o_uw + pre;
-                    unsigned int k = 0;
-                    if (b & 1u) o[k++] = PAYLOAD ? payload[row + 0] : (int)(row + 0);
-                    if (b & 2u) o[k++] = PAYLOAD ? payload[row + 1] : (int)(row + 1);
-                    if (b & 4u) o[k++] = PAYLOAD ? payload[row + 2] : (int)(row + 2);
-                    if (b & 8u) o[k++] = PAYLOAD ? payload[row + 3] : (int)(row + 3);
-                }
-            }
-        }
     }
 }
 
@@ -922,7 +509,7 @@ template <bool PAYLOAD, bool VEC, int BUF = kStBuf>
 __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     const int* __restrict__ col, const int* __restrict__ payload, uint64_t n, uint64_t rw, Pred pred,
     unsigned long long* status, unsigned long long* __restrict__ bm, int* __restrict__ out,
-    unsigned long long* __restrict__ d_count, unsigned int* err, int xmode) {
+    unsigned long long* __restrict__ d_count, unsigned int* err) {
     __shared__ __attribute__((aligned(16))) int s_buf[kWaves][BUF > 0 ? BUF : 1];
     __shared__ unsigned int s_cnt[kWaves];
     __shared__ unsigned long long s_red[kWaves];
@@ -1031,12 +618,12 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
     }
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i = flushed + (uint32_t)lane; i < fill; i += 64u) out[D + i] = buf[i % (uint32_t)BUF];
-    if (sw >= E || xmode == 2) return;  // (xmode 2, diagnostic: no bitmap expansion at all)
+    if (sw >= E) return;
     // ---- bitmap mode part: 64 tiles per step, one lane per tile (k_compact's scheme)
     unsigned long long o = D + fill;
     const uint64_t T1 = (E + 255) >> 8;
     const bool pal = PAYLOAD && ((reinterpret_cast<uintptr_t>(payload) & 15u) == 0);
-    // xmode 1: ring entries [bst, bst + bfill) go to out[ob ...]; bst = out + ob's
+    // ring entries [bst, bst + bfill) go to out[ob ...]; bst = out + ob's
     // dword offset within its 16 bytes
     unsigned long long ob = o;
     uint32_t bfill = 0, bst = (uint32_t)(((uintptr_t)(out + ob) >> 2) & 3u);
@@ -1070,142 +657,51 @@ __global__ __launch_bounds__(kTPB, 8) void k_select_stage(
             w3 = c2.y;
         }
         const unsigned int c = (unsigned int)(__popcll(w0) + __popcll(w1) + __popcll(w2) + __popcll(w3));
-        unsigned int incl = c;
+        unsigned int tot = c;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const unsigned int y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        const unsigned int tot = __shfl(incl, 63, 64);
-        const unsigned long long ol = o + (incl - c);
-        const uint64_t row0 = T * 256;
-        if (xmode == 3) {  // diagnostic: the bitmap words read and counted, nothing placed
-            o += tot;
-            if (PAYLOAD && __builtin_amdgcn_readfirstlane((int)tot) == -1) out[o] = payload[row0];
-            continue;
-        }
-        if (xmode == 4) {  // diagnostic: + the payload rows of every tile with a match loaded, nothing placed
+        for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+        // batched (round 4): tiles' outputs gathered in row order in the wave's LDS ring
+        // (free now: its entries went out above), placed so that ring index and output
+        // address agree mod 16 bytes, and flushed when the next tile would not fit as
+        // 16-byte stores, 64 lanes per instruction. Stored straight from the lanes' rows,
+        // every store instruction's addresses had gaps wherever a row does not match
+        // (round 4: 1.064 / 1.475 / 1.84 -> 1.022 / 1.355 / 1.56 ms at 10 / 50 / 100 %,
+        // profiles/r04_positions_batched_ab.log). select_result: the payload rows of 4
+        // tiles are loaded before any of them is placed.
+        constexpr int kPf = PAYLOAD ? 4 : 1;
+        for (int j0 = 0; j0 < 64; j0 += kPf) {
+            int pv[kPf][4];
             if constexpr (PAYLOAD) {
-                const bool pal4 = (reinterpret_cast<uintptr_t>(payload) & 15u) == 0;
-                int acc = 0;
-                for (int j0 = 0; j0 < 64; j0 += 4) {
-                    int pv[4][4];
-#pragma unroll
-                    for (int jj = 0; jj < 4; jj++) {
-                        const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
-                        pv[jj][0] = pv[jj][1] = pv[jj][2] = pv[jj][3] = 0;
-                        if (__builtin_amdgcn_readlane((int)c, j0 + jj) != 0) load_pay4(pv[jj], payload, r, n, pal4);
-                    }
-#pragma unroll
-                    for (int jj = 0; jj < 4; jj++) acc ^= pv[jj][0] ^ pv[jj][1] ^ pv[jj][2] ^ pv[jj][3];
-                }
-                if (acc == 0x7fffffff && tot == 0) out[o] = acc;
-            }
-            o += tot;
-            continue;
-        }
-        if (xmode == 1) {
-            // batched (round 4, the default): tiles' outputs gathered in row order in
-            // the wave's LDS ring (free now: its entries went out above), placed so that
-            // ring index and output address agree mod 16 bytes, and flushed when the next
-            // tile would not fit as 16-byte stores, 64 lanes per instruction. Straight
-            // from the lanes' rows (below), every store instruction's addresses have gaps
-            // wherever a row does not match. (A first form flushed every tile behind a
-            // wave barrier: slower at 10-50 %.) select_result: the payload rows of 4 tiles
-            // are loaded before any of them is placed.
-            constexpr int kPf = PAYLOAD ? 4 : 1;
-            for (int j0 = 0; j0 < 64; j0 += kPf) {
-                int pv[kPf][4];
-                if constexpr (PAYLOAD) {
-#pragma unroll
-                    for (int jj = 0; jj < kPf; jj++) {
-                        const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
-                        const bool any = __builtin_amdgcn_readlane((int)c, j0 + jj) != 0;
-                        if (any) load_pay4(pv[jj], payload, r, n, pal);
-                    }
-                }
 #pragma unroll
                 for (int jj = 0; jj < kPf; jj++) {
-                    const int j = j0 + jj;
-                    const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
-                    if (cj == 0) continue;
-                    if (bst + bfill + cj > (uint32_t)BUF) flush();
-                    auto rl64 = [&](unsigned long long x) {
-                        return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
-                               ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
-                    };
-                    const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
-                    const int rj = (int)((tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane) + rbase;
-                    uint32_t k = bst + bfill + rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
-                    if ((x0 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][0] : rj + 0;
-                    if ((x1 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][1] : rj + 1;
-                    if ((x2 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][2] : rj + 2;
-                    if ((x3 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][3] : rj + 3;
-                    bfill += cj;
+                    const uint64_t r = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
+                    const bool any = __builtin_amdgcn_readlane((int)c, j0 + jj) != 0;
+                    if (any) load_pay4(pv[jj], payload, r, n, pal);
                 }
             }
-            o += tot;
-            continue;
-        }
-        if (tot > 1024) {
-            // dense: the whole wave writes one tile at a time (lane l -> rows 4l+e).
-            // A tile's words, count and offset are read into scalars (v_readlane: the
-            // tile index is wave-uniform); round 4: as lane shuffles they were 12
-            // ds_bpermute round trips per tile, and 10-50 % selectivity paid ~0.5 ms
-            // for them after the scan.
-            // select_result: the payload rows of 4 tiles are loaded (indices clamped)
-            // before any of them is written; gathering at each write made every
-            // tile wait for its own round trip (10-50 % selectivity ran at twice the
-            // positions-only time)
-            constexpr int kPf = 4;  // tiles per payload batch (registers: launch bounds 8 waves)
-            const uint32_t olo = (uint32_t)ol, ohi = (uint32_t)(ol >> 32);
-            for (int j0 = 0; j0 < 64; j0 += kPf) {
-                int pv[kPf][4];
-                if constexpr (PAYLOAD) {
 #pragma unroll
-                    for (int jj = 0; jj < kPf; jj++) {
-                        const uint64_t rj = (tb + (uint64_t)(j0 + jj)) * 256 + 4 * (uint64_t)lane;
-                        load_pay4(pv[jj], payload, rj, n, pal);
-                    }
-                }
-#pragma unroll
-                for (int jj = 0; jj < kPf; jj++) {
-                    const int j = j0 + jj;
-                    if (__builtin_amdgcn_readlane((int)c, j) == 0) continue;
-                    auto rl64 = [&](unsigned long long x) {
-                        return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
-                               ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
-                    };
-                    const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
-                    const unsigned long long oj = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)olo, j) |
-                                                  ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)ohi, j) << 32);
-                    const uint64_t rj = (tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane;
-                    const unsigned int pre = rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
-                    int* q = out + oj + pre;
-                    unsigned int k = 0;
-                    if ((x0 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][0] : (int)(rj + 0) + rbase;
-                    if ((x1 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][1] : (int)(rj + 1) + rbase;
-                    if ((x2 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][2] : (int)(rj + 2) + rbase;
-                    if ((x3 >> lane) & 1ull) q[k++] = PAYLOAD ? pv[jj][3] : (int)(rj + 3) + rbase;
-                }
-            }
-        } else if (c) {
-            // sparse: each lane emits its own tile's rows in order
-            unsigned long long oo = ol;
-            unsigned long long m = w0 | w1 | w2 | w3;
-            while (m) {
-                const int l = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const uint64_t r = row0 + 4 * (uint64_t)l;
-                if ((w0 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 0] : (int)(r + 0) + rbase;
-                if ((w1 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 1] : (int)(r + 1) + rbase;
-                if ((w2 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 2] : (int)(r + 2) + rbase;
-                if ((w3 >> l) & 1ull) out[oo++] = PAYLOAD ? payload[r + 3] : (int)(r + 3) + rbase;
+            for (int jj = 0; jj < kPf; jj++) {
+                const int j = j0 + jj;
+                const uint32_t cj = (uint32_t)__builtin_amdgcn_readlane((int)c, j);
+                if (cj == 0) continue;
+                if (bst + bfill + cj > (uint32_t)BUF) flush();
+                auto rl64 = [&](unsigned long long x) {
+                    return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j) |
+                           ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j) << 32);
+                };
+                const unsigned long long x0 = rl64(w0), x1 = rl64(w1), x2 = rl64(w2), x3 = rl64(w3);
+                const int rj = (int)((tb + (uint64_t)j) * 256 + 4 * (uint64_t)lane) + rbase;
+                uint32_t k = bst + bfill + rank_lt(x3, rank_lt(x2, rank_lt(x1, rank_lt(x0, 0u))));
+                if ((x0 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][0] : rj + 0;
+                if ((x1 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][1] : rj + 1;
+                if ((x2 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][2] : rj + 2;
+                if ((x3 >> lane) & 1ull) buf[k++] = PAYLOAD ? pv[jj][3] : rj + 3;
+                bfill += cj;
             }
         }
         o += tot;
     }
-    if (xmode == 1 && bfill) flush();
+    if (bfill) flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -1386,14 +882,15 @@ __global__ __launch_bounds__(kTPB) void k_gen_uniform(int* __restrict__ out, uin
 
 // ---------------------------------------------------------------------------
 // k_scan_gather: config 3 fused (select col -> fetch aux -> agg; query.c:92-137,
-// 223-243, 306-354) with the gather deferred. k_scan<kAux> loads aux[row] inline at
-// each match, so every tile with a match waits a full random-read latency before
-// the next tile's loads go out. Here the scan streams like k_scan<kSum> (8 tiles of
+// 223-243, 306-354) with the gather deferred. Loading aux[row] inline at each match
+// made every tile with a match wait a full random-read latency before the next tile's
+// loads went out (0.975 vs 0.779 ms at 1e9, 1 %; that form was removed in round 6).
+// Here the scan streams like k_scan<kSum> (8 tiles of
 // nt dwordx4 in flight) and each wave appends its matching rows (as offsets from
 // the block's first row) to a 1024-entry LDS buffer, ranked with 4 ballots +
 // mbcnt. When a tile would overflow the buffer, and at the end, the wave drains it:
-// 8 independent aux loads per lane in flight, folded into count/sum/min/max. The
-// same aggregates as k_scan<kAux>, in the same partial slab and in-kernel combine.
+// 8 independent aux loads per lane in flight, folded into count/sum/min/max, in
+// k_scan's partial slab and in-kernel combine.
 // ---------------------------------------------------------------------------
 constexpr int kGBuf = 1024;
 
@@ -1533,13 +1030,6 @@ __global__ __launch_bounds__(kTPB) void k_copy1(unsigned char* __restrict__ dst,
                                                 uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * kTPB;
     for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) dst[i] = src[i];
-}
-
-// out[i] += base for the *count positions a non-staging select wrote (row shards)
-__global__ __launch_bounds__(kTPB) void k_add_base(int* __restrict__ out, const unsigned long long* __restrict__ count,
-                                                   int32_t base) {
-    const uint64_t n = *count, stride = (uint64_t)gridDim.x * kTPB;
-    for (uint64_t i = (uint64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += stride) out[i] += base;
 }
 
 __global__ __launch_bounds__(kTPB) void k_iota(int* __restrict__ out, uint64_t n) {
@@ -1846,7 +1336,7 @@ void arrive_forget(hipStream_t st) {
 // Launch k_scan<MODE> over n rows; returns the number of blocks (partials) via *g_out.
 // out != nullptr folds the partials inside the launch (block_arrive_last).
 template <int MODE>
-int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Partial* part,
+int launch_scan(const int32_t* col, uint64_t n, Pred p, Partial* part,
                 mq_agg* out, hipStream_t st, const DevState* s, uint32_t* g_out,
                 uint64_t* rpb_out = nullptr) {
     unsigned int* arrive = nullptr;
@@ -1857,10 +1347,10 @@ int launch_scan(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Part
     uint64_t rpb;
     geometry(s, n, scan_fn<MODE>(vec), &g, &rpb);
     if (vec)
-        hipLaunchKernelGGL((k_scan<MODE, true>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
+        hipLaunchKernelGGL((k_scan<MODE, true>), dim3(g), dim3(kTPB), 0, st, col, n, rpb, p,
                            part, out, arrive);
     else
-        hipLaunchKernelGGL((k_scan<MODE, false>), dim3(g), dim3(kTPB), 0, st, col, aux, n, rpb, p,
+        hipLaunchKernelGGL((k_scan<MODE, false>), dim3(g), dim3(kTPB), 0, st, col, n, rpb, p,
                            part, out, arrive);
     LAUNCHCHK("k_scan");
     *g_out = g;
@@ -1887,7 +1377,7 @@ int launch_gather(const int32_t* col, const int32_t* aux, uint64_t n, Pred p, Pa
     return MQ_OK;
 }
 
-size_t mask_bytes(uint64_t n) {  // 1 KiB (4 waves x 256 B) per 8192-row super-tile
+size_t mask_bytes(uint64_t n) {  // k_select_stage's bitmap / spill area: 32 B per 256-row wave tile
     return (size_t)((n + 8 * kTileRows - 1) / (8 * kTileRows)) * kWaves * 32 * sizeof(unsigned long long);
 }
 
@@ -1911,26 +1401,12 @@ int run_agg(const int32_t* col, const int32_t* aux, uint64_t n, Pred pred, mq_ag
         return set_err(MQ_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, partial_bytes());
     Partial* part = static_cast<Partial*>(d_ws);
     uint32_t g;
-    if (!aux) return launch_scan<kAgg>(col, nullptr, n, pred, part, d_out, st, s, &g);
-    // MQ_AUX_IMPL=inline keeps k_scan<kAux> (gather at each match) for A/B
-    const char* e = getenv("MQ_AUX_IMPL");
-    if (e && strcmp(e, "inline") == 0) return launch_scan<kAux>(col, aux, n, pred, part, d_out, st, s, &g);
+    if (!aux) return launch_scan<kAgg>(col, n, pred, part, d_out, st, s, &g);
     return launch_gather(col, aux, n, pred, part, d_out, st, s);
 }
 
-// Ordered compaction implementations (MQ_POSITIONS_IMPL, read per call):
-//   stage    (default) k_select_stage, one pass, 4N + 4K (+ staging) bytes;
-//   mask     k_mask + k_compact, 4N + N/8 + N/8 + 4K bytes;
-//   lookback k_select_lb, per-tile decoupled look-back.
-// Measured on 1e9 rows in DESIGN.md §3.2.
-enum PosImpl { kPosStage = 0, kPosMask = 1, kPosLookback = 2 };
-PosImpl positions_impl() {
-    const char* e = getenv("MQ_POSITIONS_IMPL");
-    if (e && strcmp(e, "mask") == 0) return kPosMask;
-    if (e && strcmp(e, "lookback") == 0) return kPosLookback;
-    return kPosStage;
-}
-
+// Ordered compaction: k_select_stage, one pass, 4N + 4K (+ staging) bytes (DESIGN.md §3.2;
+// round 6 removed the measured-slower k_mask + k_compact and look-back forms).
 // k_select_stage state: [err u32 | pad][status u64 x G] in the partial slab; the
 // bitmap (bitmap-mode tiles only) in the mask area after it.
 size_t stage_state_bytes(uint32_t g) { return 64 + (size_t)g * 8; }
@@ -1954,60 +1430,17 @@ int run_select_stage(const int32_t* col, const int32_t* payload, uint64_t n, Pre
     unsigned long long* bm = reinterpret_cast<unsigned long long*>(w + partial_bytes());
     HIPCHK(hipMemsetAsync(w, 0, stage_state_bytes(g), st));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
-    // The bitmap tiles expanded through the LDS ring into 16-byte stores, several tiles
-    // a flush (default), or (MQ_STAGE_EXPAND=0) by lane-scattered dword stores: 1.022 /
-    // 1.355 / 1.56 ms against 1.064 / 1.475 / 1.84 ms at 10 / 50 / 100 % alternating on
-    // one box (profiles/r04_positions_batched_ab.log; a first staged form that flushed
-    // every tile lost to the lanes, profiles/r04_positions_ab.log)
-    // (MQ_STAGE_EXPAND=2 / 3 / 4: diagnostics only, the output is incomplete: no bitmap
-    // expansion / the bitmap read and counted but nothing placed / + select_result's
-    // payload rows loaded for every tile with a match, nothing placed)
-    const char* xe = getenv("MQ_STAGE_EXPAND");
-    const int xmode = xe && xe[0] == '0' ? 0 : xe && xe[0] == '2' ? 2 : xe && xe[0] == '3' ? 3 : xe && xe[0] == '4' ? 4 : 1;
     if (payload) {
-        if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
-        else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
+        if (vec) hipLaunchKernelGGL((k_select_stage<true, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_stage<true, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
     } else {
-        if (vec) hipLaunchKernelGGL((k_select_stage<false, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
-        else hipLaunchKernelGGL((k_select_stage<false, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err, xmode);
+        if (vec) hipLaunchKernelGGL((k_select_stage<false, true>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
+        else hipLaunchKernelGGL((k_select_stage<false, false>), dim3(g), dim3(kTPB), 0, st, col, payload, n, rw, p, status, bm, out, cnt, err);
     }
     LAUNCHCHK("k_select_stage");
     return MQ_OK;
 }
 
-size_t lb_status_bytes(uint64_t n) {
-    return ((n + kLbTileRows - 1) / kLbTileRows) * sizeof(unsigned long long) + 16;
-}
-
-int run_select_lb(const int32_t* col, const int32_t* payload, uint64_t n, Pred p, int32_t* out,
-                  uint64_t* d_count, void* d_ws, size_t ws_bytes, hipStream_t st,
-                  const DevState* s) {
-    const uint32_t ntiles = (uint32_t)((n + kLbTileRows - 1) / kLbTileRows);
-    // workspace: [ticket u32 | err u32 | pad 8][status u64 x ntiles] after the partials
-    char* w = static_cast<char*>(d_ws) + partial_bytes();
-    if (ws_bytes < partial_bytes() + lb_status_bytes(n))
-        return set_err(MQ_EINVAL, "mq_select_positions: workspace too small");
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(w);
-    unsigned int* err = ticket + 1;
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(w + 16);
-    HIPCHK(hipMemsetAsync(w, 0, lb_status_bytes(n), st));
-    const bool vec = aligned16(col);
-    const void* fn = payload ? (vec ? (const void*)&k_select_lb<true, true> : (const void*)&k_select_lb<true, false>)
-                             : (vec ? (const void*)&k_select_lb<false, true> : (const void*)&k_select_lb<false, false>);
-    uint64_t g = (uint64_t)s->cus * (uint64_t)blocks_per_cu(fn);
-    if (g > ntiles) g = ntiles;
-    if (g == 0) g = 1;
-    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(d_count);
-    if (payload) {
-        if (vec) hipLaunchKernelGGL((k_select_lb<true, true>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
-        else hipLaunchKernelGGL((k_select_lb<true, false>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
-    } else {
-        if (vec) hipLaunchKernelGGL((k_select_lb<false, true>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
-        else hipLaunchKernelGGL((k_select_lb<false, false>), dim3((uint32_t)g), dim3(kTPB), 0, st, col, payload, n, p, status, ticket, ntiles, out, cnt, err);
-    }
-    LAUNCHCHK("k_select_lb");
-    return MQ_OK;
-}
 
 }  // namespace
 
@@ -2068,12 +1501,11 @@ static int h2d_staged(void* dst, const void* src, size_t bytes, hipStream_t st);
 
 // Large uploads (columns, CSV text) go through the pinned staging ring of the D2H
 // path below, host copies by the copy pool: a pageable hipMemcpy moved mmap'd
-// columns at 13-15 GB/s. MQ_H2D_STAGED=0 keeps the plain copy (A/B).
+// columns at 13-15 GB/s.
 int mq_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
     if (bytes == 0) return MQ_OK;
     hipStream_t st = (hipStream_t)stream;
-    static const bool staged = !(getenv("MQ_H2D_STAGED") && getenv("MQ_H2D_STAGED")[0] == '0');
-    if (staged && bytes >= ((size_t)64 << 20)) return h2d_staged(dst, src, bytes, st);
+    if (bytes >= ((size_t)64 << 20)) return h2d_staged(dst, src, bytes, st);
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     return MQ_OK;
@@ -2103,50 +1535,6 @@ struct Staging {
 };
 thread_local Staging g_staging[kMaxDev];
 
-// The CPUs next to the current device (its PCIe root's NUMA node, from sysfs): the staged
-// copies' helper threads run there, so their memcpy out of the pinned buffers and their
-// first touch of a fresh payload (which places its pages) stay on the GPU's socket. On a
-// two-socket host a helper the scheduler put on the far socket copied across the
-// interconnect: select_column's 40 MB D2H took 1.15-1.50 ms from one process to the next.
-// Measured (round 5, 15 reps over 3 processes each, one box, profiles/r05_api_numa_segs.log):
-// bound helpers were slower, select_column 1.86 vs 1.71 ms (4 segments) and 2.03 vs
-// 1.89 ms (one kernel), so binding is opt-in: MQ_NUMA_BIND=1. Empty set: no binding.
-bool device_cpuset(cpu_set_t* set) {
-    static const bool on = getenv("MQ_NUMA_BIND") && getenv("MQ_NUMA_BIND")[0] == '1';
-    CPU_ZERO(set);
-    if (!on) return false;
-    int dev = 0;
-    char bus[64] = {0};
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int)sizeof bus, dev) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    for (char* c = bus; *c; c++) *c = (char)((*c >= 'A' && *c <= 'F') ? *c - 'A' + 'a' : *c);
-    char path[160];
-    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/local_cpulist", bus);
-    FILE* f = fopen(path, "r");
-    if (!f) return false;
-    char list[1024] = {0};
-    const bool got = fgets(list, sizeof list, f) != nullptr;
-    fclose(f);
-    if (!got) return false;
-    int n = 0;
-    for (char* q = list; *q && *q != '\n';) {
-        char* end;
-        long a = strtol(q, &end, 10);
-        if (end == q) break;
-        long b = a;
-        if (*end == '-') b = strtol(end + 1, &end, 10);
-        for (long c = a; c <= b && c < CPU_SETSIZE; c++, n++) CPU_SET((int)c, set);
-        q = *end == ',' ? end + 1 : end;
-    }
-    return n > 0;
-}
-
-void bind_helper(const cpu_set_t& set, bool ok) {
-    if (ok) (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
-}
-
 // The host side of the staged D2H: each chunk copied out of the pinned buffer by
 // the calling thread and MQ_COPY_THREADS - 1 helpers (one memcpy thread moved ~10 GB/s,
 // a quarter of the DMA rate; 6 threads, round 4: see FaultPool). One pool per calling thread (row-shard workers copy
@@ -2167,12 +1555,7 @@ struct CopyPool {
         parts = e ? atoi(e) : 6;
         if (parts < 1) parts = 1;
         if (parts > 16) parts = 16;
-        cpu_set_t set;
-        const bool ok = device_cpuset(&set);
-        for (int i = 1; i < parts; i++) th.emplace_back([this, i, set, ok] {
-            bind_helper(set, ok);
-            loop(i);
-        });
+        for (int i = 1; i < parts; i++) th.emplace_back([this, i] { loop(i); });
     }
     void slice(int i) {
         const size_t a = len * (size_t)i / (size_t)parts, b = len * (size_t)(i + 1) / (size_t)parts;
@@ -2250,12 +1633,7 @@ struct FaultPool {
         F = e ? atoi(e) : 6;
         if (F < 0) F = 0;
         if (F > 16) F = 16;
-        cpu_set_t set;
-        const bool ok = device_cpuset(&set);
-        for (int i = 0; i < F; i++) th.emplace_back([this, set, ok] {
-            bind_helper(set, ok);
-            loop();
-        });
+        for (int i = 0; i < F; i++) th.emplace_back([this] { loop(); });
     }
     void work() {
         const size_t pg = 4096;
@@ -2572,8 +1950,7 @@ void mq_trim(void) {
 }
 
 size_t mq_scan_workspace_bytes(uint64_t n) {
-    const size_t a = mask_bytes(n), b = lb_status_bytes(n);
-    return partial_bytes() + (a > b ? a : b);
+    return partial_bytes() + mask_bytes(n);
 }
 
 void mq_scan_geometry(uint64_t n, uint32_t* blocks, uint64_t* rows_per_block) {
@@ -2652,7 +2029,7 @@ int mq_select_sum(const int32_t* d_col, uint64_t n, int has_low, int32_t low, in
     hipStream_t st = (hipStream_t)stream;
     if (n == 0 || !make_pred(has_low, low, has_high, high, &p)) return empty_agg(d_out, st);
     uint32_t g;
-    return launch_scan<kSum>(d_col, nullptr, n, p, static_cast<Partial*>(d_ws), d_out, st, s, &g);
+    return launch_scan<kSum>(d_col, n, p, static_cast<Partial*>(d_ws), d_out, st, s, &g);
 }
 
 int mq_select_fetch_agg(const int32_t* d_sel, const int32_t* d_val, uint64_t n, int has_low,
@@ -2691,8 +2068,8 @@ int mq_select_partials(const int32_t* d_col, uint64_t n, int has_low, int32_t lo
         return MQ_OK;
     }
     Partial* part = static_cast<Partial*>(d_ws);
-    return want_minmax ? launch_scan<kAgg>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks)
-                       : launch_scan<kSum>(d_col, nullptr, n, p, part, nullptr, st, s, nblocks);
+    return want_minmax ? launch_scan<kAgg>(d_col, n, p, part, nullptr, st, s, nblocks)
+                       : launch_scan<kSum>(d_col, n, p, part, nullptr, st, s, nblocks);
 }
 
 int mq_stream_read(const int32_t* d_col, uint64_t n, void* d_ws, size_t ws_bytes,
@@ -2794,15 +2171,8 @@ int mq_select_positions_at(const int32_t* d_col, const int32_t* d_payload, uint6
     if (row_base < 0 || (uint64_t)row_base + n > (uint64_t)INT32_MAX)
         return set_err(MQ_EINVAL, "mq_select_positions_at: rows [%d, %d + %llu) beyond int32 positions", row_base,
                        row_base, (unsigned long long)n);
-    int rc = select_positions_impl(d_col, d_payload, n, d_payload ? 0 : row_base, has_low, low, has_high, high,
-                                   d_pos_out, d_count, d_ws, ws_bytes, stream);
-    if (rc || d_payload || row_base == 0 || positions_impl() == kPosStage || n == 0) return rc;
-    DevState* s;
-    if ((rc = ensure_ready(&s))) return rc;
-    hipLaunchKernelGGL(k_add_base, dim3(stream_grid(s, n)), dim3(kTPB), 0, (hipStream_t)stream, d_pos_out,
-                       reinterpret_cast<const unsigned long long*>(d_count), row_base);
-    LAUNCHCHK("k_add_base");
-    return MQ_OK;
+    return select_positions_impl(d_col, d_payload, n, d_payload ? 0 : row_base, has_low, low, has_high, high,
+                                 d_pos_out, d_count, d_ws, ws_bytes, stream);
 }
 
 namespace {
@@ -2828,37 +2198,8 @@ int select_positions_impl(const int32_t* d_col, const int32_t* d_payload, uint64
     if (!d_ws || ws_bytes < mq_scan_workspace_bytes(n))
         return set_err(MQ_EINVAL, "mq_select_positions: workspace too small (%zu < %zu)", ws_bytes,
                        mq_scan_workspace_bytes(n));
-    p.base = row_base;  // k_select_stage adds it as it writes; the others via k_add_base
-    const PosImpl impl = positions_impl();
-    if (impl == kPosStage)
-        return run_select_stage(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, st, s);
-    if (impl == kPosLookback)
-        return run_select_lb(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, ws_bytes, st, s);
-    uint32_t g;
-    uint64_t rpb;
-    Partial* part = static_cast<Partial*>(d_ws);
-    unsigned long long* masks =
-        reinterpret_cast<unsigned long long*>(static_cast<char*>(d_ws) + partial_bytes());
-    {
-        const bool vec = aligned16(d_col);
-        const void* fn = vec ? (const void*)&k_mask<true> : (const void*)&k_mask<false>;
-        geometry(s, n, fn, &g, &rpb, 8 * kTileRows);
-        if (vec)
-            hipLaunchKernelGGL(k_mask<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, p, part, masks);
-        else
-            hipLaunchKernelGGL(k_mask<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, p, part, masks);
-        LAUNCHCHK("k_mask");
-    }
-    if (d_payload)
-        hipLaunchKernelGGL(k_compact<true>, dim3(g), dim3(kCompactTPB), 0, st, masks, part,
-                           d_payload, n, rpb, d_pos_out,
-                           reinterpret_cast<unsigned long long*>(d_count));
-    else
-        hipLaunchKernelGGL(k_compact<false>, dim3(g), dim3(kCompactTPB), 0, st, masks, part,
-                           nullptr, n, rpb, d_pos_out,
-                           reinterpret_cast<unsigned long long*>(d_count));
-    LAUNCHCHK("k_compact");
-    return MQ_OK;
+    p.base = row_base;  // k_select_stage adds it as it writes
+    return run_select_stage(d_col, d_payload, n, p, d_pos_out, d_count, d_ws, st, s);
 }
 }  // namespace
 

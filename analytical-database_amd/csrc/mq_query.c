@@ -383,15 +383,6 @@ static void* arm_thread(void* a) {
     return NULL;
 }
 
-static int arm_async_on(void) {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("MQ_GUARD_ASYNC");
-        v = !(e && e[0] == '0');
-    }
-    return v;
-}
-
 static int column_device(Column* c, const int32_t** d, Status* st) {
     const double t0 = now_s();
     ColEntry* e = col_find(c);
@@ -408,7 +399,7 @@ static int column_device(Column* c, const int32_t** d, Status* st) {
     if (rc) return fail(st, "column allocation", rc);
     ArmArg arm = {c->data, bytes, ~(uint64_t)0};
     pthread_t th;
-    const int async = bytes >= ((size_t)64 << 20) && mq_guard_enabled() && arm_async_on() &&
+    const int async = bytes >= ((size_t)64 << 20) && mq_guard_enabled() &&
                       pthread_create(&th, NULL, arm_thread, &arm) == 0;
     if (c->row_count && (rc = h2d(dev, c->data, bytes))) {
         if (async) {

@@ -718,10 +718,24 @@ typedef struct {
     double ms[4]; /* host wall time of the phases (partition, join, place, total) */
 } PJ;
 
-static void* pj_alloc(int* rc, size_t bytes) {
+/* Test hook (mq_shard_join_inject_failure): the phase whose allocations fail (1 = the
+ * partition, 2 = the local joins, 3 = the placement, 4 = the one-shard join; 0 = none). */
+static volatile int g_pj_fail;
+
+void mq_shard_join_inject_failure(int phase) { g_pj_fail = phase; }
+
+static void* pj_alloc(int* rc, size_t bytes, int phase) {
     void* p = NULL;
+    if (!*rc && g_pj_fail == phase) *rc = MQ_ENOMEM;
     if (!*rc) *rc = mq_pool_malloc(&p, bytes ? bytes : 4);
     return p;
+}
+
+/* The end of a worker's phase: its stream drained whatever rc is, so that on an error
+ * path no queued peer copy or kernel still uses a buffer the caller's thread frees. */
+static int pj_end(Shard* s, int rc) {
+    const int r2 = mq_stream_sync(s->stream);
+    return rc ? rc : r2;
 }
 
 /* Entry fence of mq_shard_join: its inputs are device pointers the caller may still be
@@ -740,10 +754,10 @@ static void t_pj_single(Shard* s, void* a) {
     uint64_t m = 0;
     int rc = mq_join_build(x->c1[0], x->p1[0], x->n1[0], &j, s->stream);
     if (!rc) rc = mq_join_probe(j, x->c2[0], x->n2[0], &m, s->stream);
-    x->out1[0] = (int32_t*)pj_alloc(&rc, m * 4);
-    x->out2[0] = (int32_t*)pj_alloc(&rc, m * 4);
+    x->out1[0] = (int32_t*)pj_alloc(&rc, m * 4, 4);
+    x->out2[0] = (int32_t*)pj_alloc(&rc, m * 4, 4);
     if (!rc && m) rc = mq_join_write(j, x->p2[0], x->out1[0], x->out2[0], s->stream);
-    if (!rc) rc = mq_stream_sync(s->stream);
+    rc = pj_end(s, rc);
     if (j) mq_join_free(j);
     x->m[0] = m;
     x->mg[0][0] = m;
@@ -755,16 +769,15 @@ static void t_pj_part(Shard* s, void* a) {
     PJ* x = (PJ*)a;
     const int i = s->idx;
     int rc = 0;
-    x->bk[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4);
-    x->bp[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4);
-    x->pk[i] = (int32_t*)pj_alloc(&rc, x->n2[i] * 4);
-    x->inv[i] = (uint32_t*)pj_alloc(&rc, x->n2[i] * 4);
+    x->bk[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4, 1);
+    x->bp[i] = (int32_t*)pj_alloc(&rc, x->n1[i] * 4, 1);
+    x->pk[i] = (int32_t*)pj_alloc(&rc, x->n2[i] * 4, 1);
+    x->inv[i] = (uint32_t*)pj_alloc(&rc, x->n2[i] * 4, 1);
     if (!rc)
         rc = mq_pjoin_partition(x->c1[i], x->p1[i], x->n1[i], g_G, x->bk[i], x->bp[i], NULL, x->cb[i], s->stream);
     if (!rc)
         rc = mq_pjoin_partition(x->c2[i], NULL, x->n2[i], g_G, x->pk[i], NULL, x->inv[i], x->cp[i], s->stream);
-    if (rc) (void)mq_stream_sync(s->stream); /* pj_free_temps frees the outputs from the caller's thread */
-    s->rc = rc;
+    s->rc = pj_end(s, rc); /* pj_free_temps frees the outputs from the caller's thread */
 }
 
 /* first index of bucket b in shard s's partitioned side (cnt = cb or cp) */
@@ -783,10 +796,10 @@ static void t_pj_join(Shard* s, void* a) {
         np += x->cp[k][g];
     }
     int rc = 0;
-    int32_t* jk = (int32_t*)pj_alloc(&rc, nb * 4);
-    int32_t* jp = (int32_t*)pj_alloc(&rc, nb * 4);
-    int32_t* jq = (int32_t*)pj_alloc(&rc, np * 4);
-    x->cnt[g] = (uint32_t*)pj_alloc(&rc, np * 4);
+    int32_t* jk = (int32_t*)pj_alloc(&rc, nb * 4, 2);
+    int32_t* jp = (int32_t*)pj_alloc(&rc, nb * 4, 2);
+    int32_t* jq = (int32_t*)pj_alloc(&rc, np * 4, 2);
+    x->cnt[g] = (uint32_t*)pj_alloc(&rc, np * 4, 2);
     /* bucket g of every shard, in shard order */
     uint64_t ab = 0, ap = 0;
     for (int k = 0; k < g_G && !rc; k++) {
@@ -817,9 +830,9 @@ static void t_pj_join(Shard* s, void* a) {
         }
         sp += x->cp[k][g];
     }
-    x->o1[g] = (int32_t*)pj_alloc(&rc, m * 4);
+    x->o1[g] = (int32_t*)pj_alloc(&rc, m * 4, 2);
     if (!rc && m) rc = mq_join_write(j, NULL, x->o1[g], NULL, s->stream);
-    if (!rc) rc = mq_stream_sync(s->stream);
+    rc = pj_end(s, rc);
     if (j) mq_join_free(j);
     /* stream-ordered: on an error path peer copies or the build may still be queued */
     mq_pool_free_on(jk, s->stream);
@@ -836,10 +849,10 @@ static void t_pj_place(Shard* s, void* a) {
     for (int g = 0; g < g_G; g++) M += x->mg[g][i];
     x->m[i] = M;
     int rc = 0;
-    uint32_t* cntp = (uint32_t*)pj_alloc(&rc, n * 4);
-    int32_t* o1p = (int32_t*)pj_alloc(&rc, M * 4);
-    x->out1[i] = (int32_t*)pj_alloc(&rc, M * 4);
-    x->out2[i] = (int32_t*)pj_alloc(&rc, M * 4);
+    uint32_t* cntp = (uint32_t*)pj_alloc(&rc, n * 4, 3);
+    int32_t* o1p = (int32_t*)pj_alloc(&rc, M * 4, 3);
+    x->out1[i] = (int32_t*)pj_alloc(&rc, M * 4, 3);
+    x->out2[i] = (int32_t*)pj_alloc(&rc, M * 4, 3);
     /* from every device g, in g order: this shard's bucket-g rows' counts and pairs */
     uint64_t ac = 0, am = 0;
     for (int g = 0; g < g_G && !rc; g++) {
@@ -855,7 +868,7 @@ static void t_pj_place(Shard* s, void* a) {
         am += x->mg[g][i];
     }
     if (!rc) rc = mq_pjoin_place(cntp, o1p, x->inv[i], x->p2[i], n, M, x->out1[i], x->out2[i], s->stream);
-    if (!rc) rc = mq_stream_sync(s->stream);
+    rc = pj_end(s, rc);
     mq_pool_free_on(cntp, s->stream);
     mq_pool_free_on(o1p, s->stream);
     s->rc = rc;
@@ -874,10 +887,9 @@ static void pj_free_temps(PJ* x) {
     }
 }
 
-/* The three phases; every worker synchronises its stream before a phase ends, so the
- * next phase's peer copies read finished data. On error nothing of x's stays allocated
- * (each worker has synchronised or ordered its frees on its stream; t_pj_part's buffers
- * are freed after its partitions, which synchronise). */
+/* The three phases; every worker synchronises its stream before a phase ends, error or
+ * not (pj_end), so the next phase's peer copies read finished data and, on error, the
+ * caller's thread frees x's buffers only after every queued use of them has run. */
 static int pj_run(PJ* x) {
     double t0 = shim_now();
     if (g_G == 1) { /* one shard: the local join alone (timed as the join phase) */
@@ -927,10 +939,7 @@ int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const 
     if (start(&st)) return MQ_ENODEV;
     PJ* x = (PJ*)calloc(1, sizeof(PJ));
     if (!x) return MQ_ENOMEM;
-    /* MQ_SHARD_JOIN_FENCE=0 skips the fence: only to show that the regression test
-     * (tests/test_gpu_pjoin.py, null-stream writers) fails without it */
-    const char* fe = getenv("MQ_SHARD_JOIN_FENCE");
-    int rc = fe && fe[0] == '0' ? 0 : run_all(t_pj_fence, NULL);
+    int rc = run_all(t_pj_fence, NULL);
     if (rc) {
         free(x);
         return rc;

@@ -1,19 +1,18 @@
 // mq_shared.hip — shared_select (src/query.c:439-583): Q range selects over one
-// column with the column read twice, whatever Q is (the reference reads it once
-// per thread with Q predicates per value, query.c:472-479; a per-query loop of
-// mq_select_positions would read it Q times).
+// column with the column read once (the reference reads it once per thread with Q
+// predicates per value, query.c:472-479; a per-query loop of mq_select_positions
+// would read it Q times).
 //
 // Decomposition: the scan grid of mq_scan_common.h, but inside a block each WAVE
-// owns a contiguous quarter of the block's chunk (a "wave-chunk"). Row order is
-// then (block, wave, wave-tile, lane, element), so:
-//   pass 1 (k_ss_count): per (query, wave-chunk) match counts;
-//   scan: one flat exclusive scan over the query-major count array gives every
-//         (query, wave-chunk) its output offset (minus the query's own base);
-//   pass 2 (k_ss_write): each wave re-reads its wave-chunk, evaluates the Q
-//         predicates per 256-row wave-tile and writes each query's positions at
-//         running offsets it keeps in LDS (no barriers, no atomics).
-// HBM traffic: 8N (two nt reads) + 4 * sum(K_q), plus Q x 4 x blocks counters.
-// VALU: ~2 compares + 1 ballot per row per query, so Q >> 1 is VALU-bound.
+// owns a contiguous quarter of the block's chunk (a "wave-chunk"). The Q bounds cut
+// the int32 line into elementary intervals (EIs); the count pass (k_ssk_count) finds
+// each covered row's EI through an LDS cell table, counts per (query, wave-chunk) and
+// lists every (query, row) pair of its wave-chunk into the wave's slice of the
+// workspace; one kernel scans the counts into offsets and totals (k_ss_offsets); the
+// scatter (k_ssp_scatter) sorts each slice by query in LDS and writes every query's
+// run of rows. A slice that overflows (dense queries: more than a pair a row) sends
+// the write to the column pass (k_ssi_write) on the same counts. DESIGN.md §3.4.
+// HBM traffic: 4N + 4 sum(K_q) (pairs) + 4 sum(K_q) read + 4 sum(K_q) written.
 
 #include <hip/hip_runtime.h>
 
@@ -72,94 +71,6 @@ __device__ __forceinline__ uint32_t match4(int4 v, Pred p, uint64_t row, uint64_
     return b;
 }
 
-// Ballot of "row matches" straight off the compare (v_sub + v_cmp -> SGPR pair).
-__device__ __forceinline__ unsigned long long bal(int x, uint32_t lo, uint32_t wm1) {
-    return __ballot(((uint32_t)x - lo) <= wm1);
-}
-
-// counts[q * nwc + wc], wc = block * 4 + wave. PAIRS: also list every (query, row)
-// match into the wave's pair slice (tile by tile; inside a tile query by query, rows
-// ascending: per query, row order), the single pass of k_ssp_count / k_ssp_scatter
-// below.
-__device__ __forceinline__ void list_pairs(uint32_t* __restrict__ list, uint32_t at, uint32_t j, uint32_t r0,
-                                           unsigned long long m0, unsigned long long m1, unsigned long long m2,
-                                           unsigned long long m3, int lane, unsigned long long ltmask) {
-    const unsigned long long bit = 1ull << lane;
-    at += (uint32_t)(__popcll(m0 & ltmask) + __popcll(m1 & ltmask) + __popcll(m2 & ltmask) + __popcll(m3 & ltmask));
-    const uint32_t tag = j << 24;
-    if (m0 & bit) list[at++] = tag | (r0 + 0);
-    if (m1 & bit) list[at++] = tag | (r0 + 1);
-    if (m2 & bit) list[at++] = tag | (r0 + 2);
-    if (m3 & bit) list[at++] = tag | (r0 + 3);
-}
-
-template <bool VEC, bool PAIRS>
-__global__ __launch_bounds__(kTPB) void k_ss_count(const int* __restrict__ col, uint64_t n,
-                                                   uint64_t rpb, const Pred* __restrict__ preds,
-                                                   int q, uint32_t* __restrict__ counts,
-                                                   uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
-                                                   uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
-    __shared__ uint32_t wcnt[kWaves][kMaxQ];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int i = tid; i < q; i += kTPB) {
-#pragma unroll
-        for (int w = 0; w < kWaves; w++) wcnt[w][i] = 0;
-    }
-    __syncthreads();
-    uint64_t s, e;
-    wave_chunk(n, rpb, wave, &s, &e);
-    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
-    uint32_t* list = PAIRS ? pairs + wc * cap : nullptr;
-    uint32_t run = 0;
-    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
-        int4 v[kSsUnroll];
-#pragma unroll
-        for (int u = 0; u < kSsUnroll; u++)
-            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
-        const bool full = t + kWaveTile * kSsUnroll <= e;
-        for (int j = 0; j < q; j++) {
-            const Pred p = preds[j];  // uniform index: scalar-cache load
-            uint32_t c = 0;
-#pragma unroll
-            for (int u = 0; u < kSsUnroll; u++) {
-                const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
-                unsigned long long m0, m1, m2, m3;
-                if (full) {  // ballots straight off the compares
-                    m0 = bal(v[u].x, p.lo, p.wm1);
-                    m1 = bal(v[u].y, p.lo, p.wm1);
-                    m2 = bal(v[u].z, p.lo, p.wm1);
-                    m3 = bal(v[u].w, p.lo, p.wm1);
-                } else {
-                    const uint32_t b = match4(v[u], p, row, e);
-                    m0 = __ballot(b & 1u);
-                    m1 = __ballot(b & 2u);
-                    m2 = __ballot(b & 4u);
-                    m3 = __ballot(b & 8u);
-                }
-                const uint32_t tc = (uint32_t)(__popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3));
-                if (PAIRS && tc) {
-                    if ((uint64_t)run + tc <= cap)
-                        list_pairs(list, run, (uint32_t)j, (uint32_t)(row - s), m0, m1, m2, m3, lane, ltmask);
-                    run += tc;
-                }
-                c += tc;
-            }
-            if (lane == 0) wcnt[wave][j] += c;  // this wave only: no atomics
-        }
-    }
-    if (PAIRS && lane == 0) {
-        npairs[wc] = run;
-        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
-    }
-    __syncthreads();
-    for (int i = tid; i < q; i += kTPB) {
-#pragma unroll
-        for (int w = 0; w < kWaves; w++)
-            counts[(uint64_t)i * nwc + (uint64_t)blockIdx.x * kWaves + w] = wcnt[w][i];
-    }
-}
-
 // Output pointers come from a device array, so the compiler sees generic (flat)
 // pointers; flat stores count in lgkmcnt and every later LDS wait would also wait
 // for them to reach memory. The outputs are global memory: store through that.
@@ -185,54 +96,8 @@ __device__ __forceinline__ void ss_emit(gint* __restrict__ out, unsigned long lo
     o += tot;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, uint64_t n,
-                                                   uint64_t rpb, const Pred* __restrict__ preds,
-                                                   int q, const unsigned long long* __restrict__ offs,
-                                                   uint64_t nwc, int* const* __restrict__ outs, int32_t base,
-                                                   const unsigned int* __restrict__ only_if) {
-    if (only_if && !*only_if) return;  // single pass without overflow: k_ssp_scatter wrote
-    __shared__ unsigned long long run[kWaves][kMaxQ];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int i = tid; i < q; i += kTPB) {
-        const unsigned long long base = offs[(uint64_t)i * nwc];  // query i's first offset
-#pragma unroll
-        for (int w = 0; w < kWaves; w++)
-            run[w][i] = offs[(uint64_t)i * nwc + (uint64_t)blockIdx.x * kWaves + w] - base;
-    }
-    __syncthreads();
-    uint64_t s, e;
-    wave_chunk(n, rpb, wave, &s, &e);
-    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
-        int4 v[kSsUnroll];
-#pragma unroll
-        for (int u = 0; u < kSsUnroll; u++)
-            v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
-        const bool full = t + kWaveTile * kSsUnroll <= e;
-        for (int j = 0; j < q; j++) {
-            const Pred p = preds[j];  // uniform index: scalar-cache load
-            unsigned long long o = run[wave][j];
-            gint* const out = global_ptr(outs[j]);
-#pragma unroll
-            for (int u = 0; u < kSsUnroll; u++) {
-                const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
-                if (full) {
-                    ss_emit(out, o, row, bal(v[u].x, p.lo, p.wm1), bal(v[u].y, p.lo, p.wm1),
-                            bal(v[u].z, p.lo, p.wm1), bal(v[u].w, p.lo, p.wm1), lane, ltmask, base);
-                } else {
-                    const uint32_t b = match4(v[u], p, row, e);
-                    ss_emit(out, o, row, __ballot(b & 1u), __ballot(b & 2u), __ballot(b & 4u),
-                            __ballot(b & 8u), lane, ltmask, base);
-                }
-            }
-            if (lane == 0) run[wave][j] = o;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
-// Many queries (q >= kEiMinQ): elementary intervals. The 2q query bounds cut the
+// Elementary intervals. The 2q query bounds cut the
 // int32 line into m+1 <= 2q+1 "elementary intervals" (EIs); every value lies in
 // exactly one, e(v) = #{bounds <= v}, and query i covers the EIs [ea_i, eb_i).
 // e(v) comes from a 4096-bucket table over [bmin, bmax] (each entry: the EI range
@@ -247,14 +112,12 @@ __global__ __launch_bounds__(kTPB) void k_ss_write(const int* __restrict__ col, 
 //          the tile) gives its slot after the query's running offset. Tiles with
 //          many pairs (dense queries) take the per-query ballot loop instead.
 // ---------------------------------------------------------------------------
-// Round 2's crossover was Q = 12 (two-pass kernels: Q=8 ballots 2.65 vs 3.25 ms). Against
-// the single-pass k-major count (round 5, 1e9 rows, count + write, one box,
-// profiles/r05_ss_small_q.log) the ballots lose from Q = 2: 0.1 % ranges Q = 2 / 4 / 8
-// 0.96 / 1.38 / 2.38 vs 0.79 / 0.83 / 0.89 ms, 10 % ranges 1.90 / 3.17 / 6.0 vs
-// 1.72 / 2.52 / 4.22 ms; only very dense sets (50 % ranges, a pair per row, the pair
-// slices overflow) keep the ballots ahead (Q = 2 4.77 vs 5.17 ms). The ballot kernels
-// stay as MQ_SS_EI_MIN=N (N > Q) / MQ_SS_IMPL=ballot.
-constexpr int kEiMinQ = 1;
+// Per-query ballot kernels (every predicate on every row) ran up to round 5 for small Q.
+// Against the single-pass k-major count (1e9 rows, count + write, one box,
+// profiles/r05_ss_small_q.log) they lost from Q = 2: 0.1 % ranges Q = 2 / 4 / 8 0.96 /
+// 1.38 / 2.38 vs 0.79 / 0.83 / 0.89 ms, 10 % ranges 1.90 / 3.17 / 6.0 vs 1.72 / 2.52 /
+// 4.22 ms; only very dense sets (50 % ranges, a pair per row, the pair slices overflow)
+// were faster with them (Q = 2 4.77 vs 5.17 ms). Removed in round 6.
 constexpr int kEiMax = 2 * kMaxQ + 2;   // EIs (m + 1 <= 2 q + 1) + prefix slot
 constexpr int kBuckets = 4096;
 constexpr int kPairCap = 512;
@@ -263,17 +126,14 @@ constexpr int kPairCap = 512;
 // 1.13 against 0.90 / 0.97 / 1.18 ms), on at Q = 150 (1.567 against 1.612), three
 // alternating rounds on one box, profiles/r05_ss_pf_ab.log; was 64)
 constexpr int kSsPfMinQ = 100;
-constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssp_count
-constexpr int kBucketsP = kBuckets / 2;  // k_ssp_count's bucket table (LDS)
-constexpr int kCoarse = 16384;           // k_ssp_count's coverage bitmap cells
+constexpr int kQlCap = 1024;  // per-EI query-list entries staged in LDS by k_ssk_count
 constexpr int kCells = 4096;             // k_ssk_count's cell table (u16 per cell, 8 KB of LDS)
 constexpr uint32_t kRingK = 320;         // k_ssk_count's queued rows per wave (< 64 + a 256-row tile)
-constexpr uint32_t kRing = 320;          // k_ssp_count's queued rows per wave (< 64 + a 256-row tile)
 // Pairs of one 1024-row wave-group held in LDS until the next group's loads are
 // issued, then written with at most 4 straight-line coalesced stores: vmcnt retires
 // loads and stores in order, so stores issued before a group's loads (or a
 // data-dependent number of them, which makes the compiler wait for all) would put
-// their round trip on every group (k_ssp_count with direct per-pair stores ran at
+// their round trip on every group (a count pass with direct per-pair stores ran at
 // 2.3 ms, 1.2 without the stores, at Q = 150).
 constexpr uint32_t kPb = 256;
 
@@ -281,7 +141,6 @@ struct EiMeta {
     int m;          // number of bounds
     int shift;      // bucket width 2^shift
     int bmin, bmax; // first / last bound
-    int cshift;     // coverage cell width 2^cshift
     int xshift;     // k_ssk_count's cell width 2^xshift
 };
 
@@ -291,7 +150,6 @@ struct EiTables {  // device copies, filled by the host (ss_count)
     const uint32_t* qoff;       // m + 2: CSR offsets of the per-EI query lists
     const uint16_t* qlist;      // queries covering each EI, ascending
     const uint32_t* qab;        // per query: ea (low 16) | eb (high 16)
-    const uint32_t* cov;        // kCoarse bits over [bmin, bmax]: a covered EI meets the cell
     const uint16_t* cell;       // kCells entries over [bmin, bmax] (k_ssk_count): 0 = no covered
                                 // EI meets the cell; e + 1 (< 0x8000) = the cell lies in covered
                                 // EI e; 0x8000 | e0 = bounds inside, e(v) >= e0: search
@@ -497,7 +355,7 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
 }
 
 // ---------------------------------------------------------------------------
-// One read of the column (q >= kEiMinQ, the usual case): the count pass also lists
+// One read of the column (the usual case): the count pass also lists
 // every (query, row) pair of its wave-chunk, in row order, into the wave's slice of
 // the workspace (one u32 per pair: query << 24 | row offset in the wave-chunk);
 // after the scan, k_ssp_scatter sorts each slice by query in LDS, 2048 pairs at a
@@ -507,271 +365,26 @@ __global__ __launch_bounds__(kTPB) void k_ssi_write(const int* __restrict__ col,
 // of its wave-chunk; a wave-chunk with more pairs (dense queries) flags an overflow
 // and the write falls back to the column pass (k_ssi_write) on the same counts.
 // ---------------------------------------------------------------------------
-// Rows no query covers (most of them at the usual selectivities) are dropped before
-// the interval lookup by a coarse bitmap over [bmin, bmax] (kCoarse cells, a cell
-// set when any covered EI meets it); the rows that pass are queued per wave in LDS
-// in row order and looked up 64 at a time, so the lookup and the pair listing run
-// on full waves instead of on every row slot of every tile.
-template <bool VEC>
-__global__ __launch_bounds__(kTPB) void k_ssp_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
-                                                    EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
-                                                    uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
-                                                    uint32_t* __restrict__ npairs, unsigned int* __restrict__ overflow) {
-    __shared__ uint32_t s_bkt[kBucketsP];
-    __shared__ int32_t s_b[kEiMax];
-    __shared__ uint32_t s_qoff[kEiMax];
-    __shared__ uint32_t hist[kWaves][kEiMax];
-    __shared__ uint16_t s_ql[kQlCap];
-    __shared__ uint32_t s_pb[kWaves][kPb];
-    __shared__ uint32_t s_cov[kCoarse / 32];
-    __shared__ int32_t s_qv[kWaves][kRing];
-    __shared__ uint32_t s_qr[kWaves][kRing];
-    // (the wave index through readfirstlane: the chunk bounds and the per-group
-    // branches below are then scalar)
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    {  // the 2048-bucket table: bucket k covers the 4096-bucket table's 2k and 2k+1
-        constexpr int kPer = kBucketsP / kTPB;
-        uint32_t u[kPer], w[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) u[k] = T.bucket[2 * (tid + k * kTPB)], w[k] = T.bucket[2 * (tid + k * kTPB) + 1];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) s_bkt[tid + k * kTPB] = (u[k] & 0xFFFFu) | (w[k] & 0xFFFF0000u);
-    }
-    for (int i = tid; i < kCoarse / 32; i += kTPB) s_cov[i] = T.cov[i];
-    for (int i = tid; i < M.m; i += kTPB) s_b[i] = T.bounds[i];
-    for (int i = tid; i <= M.m + 1; i += kTPB) s_qoff[i] = T.qoff[i];
-    for (int i = tid; i < kWaves * kEiMax; i += kTPB) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    EiMeta MP = M;
-    MP.shift = M.shift + 1;
-    // the per-EI query lists: in LDS when they fit (the usual case), else read from HBM
-    const uint32_t nql = s_qoff[M.m + 1];
-    const bool ql_lds = nql <= (uint32_t)kQlCap;
-    if (ql_lds)
-        for (uint32_t i = tid; i < nql; i += kTPB) s_ql[i] = T.qlist[i];
-    __syncthreads();
-    // the cell of v - bmin, clamped to the last cell: the host sets every cell past
-    // bmax's (and the last, which values below bmin also reach) to "EI m is covered";
-    // a value below bmin that lands on a set cell only costs a lookup (EI 0 has no query)
-    auto covered = [&](int32_t v) -> bool {
-        const uint32_t c = min(((uint32_t)v - (uint32_t)M.bmin) >> M.cshift, (uint32_t)kCoarse - 1u);
-        return (s_cov[c >> 5] >> (c & 31)) & 1u;
-    };
-    uint64_t s, e;
-    wave_chunk(n, rpb, wave, &s, &e);
-    const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
-    uint32_t* list = pairs + wc * cap;
-    uint32_t* pb = s_pb[wave];
-    int32_t* qv = s_qv[wave];
-    uint32_t* qr = s_qr[wave];
-    uint32_t run = 0;  // pairs of this wave-chunk so far (wave-uniform)
-    uint32_t pend = 0, pend_at = 0;  // the previous group's pairs, still in pb
-    uint32_t head = 0, tail = 0;  // queued rows [head, tail) of qv / qr
-    uint32_t fill = 0;    // this group's pairs in pb
-    bool direct = false;  // the group outgrew pb: its later pairs are stored directly
-    // one round: up to 64 queued rows (lanes < nr), their EI, counts and pairs
-    auto round = [&](uint32_t nr) {
-        const bool has = (uint32_t)lane < nr;
-        uint32_t qa = 0, qn = 0, r = 0;
-        if (has) {
-            const uint32_t slot = head + (uint32_t)lane;
-            const int32_t x = qv[slot];
-            r = qr[slot];
-            const int ei = ei_of(x, MP, s_bkt, s_b);
-            qa = s_qoff[ei];
-            qn = s_qoff[ei + 1] - qa;
-            if (qn) atomicAdd(&hist[wave][ei], 1u);
-        }
-        head += nr;
-        // exclusive prefix of qn over the lanes (a row is covered by a few queries)
-        uint32_t pre = 0, tot = 0;
-        if (!__ballot(qn >= 8u)) {
-#pragma unroll
-            for (int bit = 0; bit < 3; bit++) {
-                const unsigned long long bm = __ballot((qn >> bit) & 1u);
-                pre += (uint32_t)__popcll(bm & ltmask) << bit;
-                tot += (uint32_t)__popcll(bm) << bit;
-            }
-        } else {
-            for (uint32_t t = 1;; t++) {
-                const unsigned long long bm = __ballot(qn >= t);
-                if (!bm) break;
-                pre += (uint32_t)__popcll(bm & ltmask);
-                tot += (uint32_t)__popcll(bm);
-            }
-        }
-        if (tot == 0) return;
-        if ((uint64_t)run + tot <= cap) {
-            direct = direct || fill + tot > kPb;
-            if (!direct) {
-                uint32_t at = fill + pre;
-                if (!__ballot(qn > 1u)) {
-                    if (qn) pb[at] = ((uint32_t)(ql_lds ? s_ql[qa] : T.qlist[qa]) << 24) | r;
-                } else {
-                    for (uint32_t i = 0; i < qn; i++)
-                        pb[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
-                }
-                fill += tot;
-            } else {
-                uint32_t at = run + pre;
-                for (uint32_t i = 0; i < qn; i++)
-                    list[at++] = ((uint32_t)(ql_lds ? s_ql[qa + i] : T.qlist[qa + i]) << 24) | r;
-            }
-        }
-        run += tot;  // past cap: still counted, the slice is incomplete
-    };
-    // the slice as a buffer resource: a store at an offset past it is dropped, so the
-    // deferred stores below are always the same kPb / 64 instructions (a conditional
-    // store makes the count of stores behind a group's loads unknown to the compiler,
-    // which then waits for all of them, store acks included, before using the loads)
-    const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(list, 0, (int)(cap * 4), 0x00020000);
-    for (uint64_t t = s; t < e; t += kWaveTile * kSsUnroll) {
-        int4 v[kSsUnroll];
-        const bool whole = t + kWaveTile * kSsUnroll <= e;  // no row past the chunk's end
-        if (whole) {  // (wave-uniform) straight-line loads
-#pragma unroll
-            for (int u = 0; u < kSsUnroll; u++)
-                v[u] = load4_nt<VEC>(col + t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4);
-        } else {
-#pragma unroll
-            for (int u = 0; u < kSsUnroll; u++)
-                v[u] = load_row4<VEC>(col, t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4, e);
-        }
-        {  // the previous group's pairs, behind this group's loads
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int k = 0; k < (int)(kPb / 64); k++) {
-                const uint32_t i = (uint32_t)(k * 64 + lane);
-                __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, i < pend ? (int)((pend_at + i) * 4u) : (int)0x80000000u,
-                                                      0, 0);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        const uint32_t grp_at = run;
-        fill = 0;
-        direct = false;
-#pragma unroll
-        for (int u = 0; u < kSsUnroll; u++) {
-            const uint64_t row = t + (uint64_t)u * kWaveTile + (uint64_t)lane * 4;
-            const int x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            bool c[4];
-            uint32_t nc = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                c[k] = covered(x[k]) && (whole || row + k < e);
-                nc += c[k] ? 1u : 0u;
-            }
-            // queue the covered rows in row order: exclusive prefix of nc (< 8)
-            uint32_t pre = 0, tot = 0;
-#pragma unroll
-            for (int bit = 0; bit < 3; bit++) {
-                const unsigned long long bm = __ballot((nc >> bit) & 1u);
-                pre += (uint32_t)__popcll(bm & ltmask) << bit;
-                tot += (uint32_t)__popcll(bm) << bit;
-            }
-            if (tot == 0) continue;
-            uint32_t at = tail + pre;
-            const uint32_t r0 = (uint32_t)(row - s);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (c[k]) {
-                    qv[at] = x[k];
-                    qr[at] = r0 + (uint32_t)k;
-                    at++;
-                }
-            }
-            tail += tot;
-            __builtin_amdgcn_wave_barrier();
-            if (tail >= 64u) {
-                do {
-                    round(64u);
-                    __builtin_amdgcn_wave_barrier();
-                } while (tail - head >= 64u);
-                // the rest (< 64) to the front: the queue stays linear, no modulo
-                const uint32_t rest = tail - head;
-                int32_t mv = 0;
-                uint32_t mr = 0;
-                if ((uint32_t)lane < rest) mv = qv[head + lane], mr = qr[head + lane];
-                __builtin_amdgcn_wave_barrier();
-                if ((uint32_t)lane < rest) qv[lane] = mv, qr[lane] = mr;
-                __builtin_amdgcn_wave_barrier();
-                head = 0;
-                tail = rest;
-            }
-        }
-        pend = fill;
-        pend_at = grp_at;
-    }
-    // the rows still queued: their pairs go straight to the slice, after pb's
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
-    __builtin_amdgcn_wave_barrier();
-    fill = 0;
-    direct = true;
-    while (tail != head) {
-        round(tail - head < 64u ? tail - head : 64u);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) {
-        npairs[wc] = run;
-        if ((uint64_t)run > cap) atomicOr(overflow, 1u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    // per-query counts from the EI histogram's prefix (as k_ssi_count)
-    uint32_t* h = hist[wave];
-    const int ne = M.m + 2;
-    const int per = (ne + 63) / 64;
-    uint32_t loc = 0;
-    for (int i = 0; i < per; i++) {
-        const int j = lane * per + i;
-        if (j < ne) loc += h[j];
-    }
-    uint32_t incl = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    uint32_t acc = incl - loc;
-    __builtin_amdgcn_wave_barrier();
-    for (int i = 0; i < per; i++) {
-        const int j = lane * per + i;
-        if (j < ne) {
-            const uint32_t c = h[j];
-            h[j] = acc;
-            acc += c;
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (int i = lane; i < q; i += 64) {
-        const uint32_t ab = T.qab[i];
-        counts[(uint64_t)i * nwc + wc] = h[ab >> 16] - h[ab & 0xFFFFu];
-    }
-}
-
-// The same single pass, k-major (round 3): lane l of a wave-tile holds rows l, l + 64,
+// The single pass, k-major (round 3): lane l of a wave-tile holds rows l, l + 64,
 // l + 128, l + 192 (four coalesced dword loads instead of one dwordx4), so the rows of
 // one load are 64 consecutive rows and a row's place in the wave's queue is one
 // mbcnt of the ballot of "covered" (rows in row order, no per-lane prefix over four
 // rows). A covered row is found with one LDS read of the cell table (kCells u16 over
 // [bmin, bmax], ei_build), which also gives its EI unless a bound lies inside the
 // cell; such rows are queued with a flag and their EI found from the cell's first EI
-// by a short search. k_ssp_count spent 670 M VALU per pass at Q = 150 on its
-// per-row coverage test, per-lane prefix and queue writes (PMC); this pass does the
-// per-row work in fewer instructions (625 vs 720 M VALU before the cell table shrank
-// to 4096 cells, which let 4 blocks share a CU). Outputs identical.
+// by a short search. The round-2 form of this pass (a coverage bitmap test per row, a
+// per-lane prefix over a lane's 4 consecutive rows, removed in round 6) spent 670 M
+// VALU per pass at Q = 150 on that per-row work (PMC); this pass does it in fewer
+// instructions (625 vs 720 M VALU before the cell table shrank to 4096 cells, which let
+// 4 blocks share a CU).
 __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// P16 (round 5): the list as 16-bit entries, half the bytes of the u32 pairs (the pair
-// stores inside the column read cost the pass far more than their share of its bytes,
-// tools/mix_probe): a pair is query << 7 | the row within its 128-row tile; a token
-// 0x8000 | d, written ahead of a queued row whose tile is d tiles past the previous
-// queued row's (from tile 0 at the wave-chunk's start), gives the tile. cap counts
-// entries. Wave-chunks of at most 2^22 rows (d < 2^15; the host checks).
-template <bool PF, bool P16>
+// (Round 5 measured a 16-bit list, query << 7 | the row in its 128-row tile plus tile
+// tokens: half the bytes, yet the count pass 1.20 -> 1.28 ms and the scatter 0.51 -> 0.57
+// at Q = 150, profiles/r05_ss_host_ab.log; removed in round 6.)
+template <bool PF>
 __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col, uint64_t n, uint64_t rpb,
                                                     EiMeta M, EiTables T, int q, uint32_t* __restrict__ counts,
                                                     uint64_t nwc, uint32_t* __restrict__ pairs, uint64_t cap,
@@ -815,17 +428,15 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
     uint64_t s, e;
     wave_chunk(n, rpb, wave, &s, &e);
     const uint64_t wc = (uint64_t)blockIdx.x * kWaves + wave;
-    constexpr uint32_t kEb = P16 ? 2u : 4u;  // bytes per list entry
     uint32_t* list = pairs + wc * cap;
-    uint16_t* list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
     uint32_t* pb = s_pb[wave];
     int32_t* qv = s_qv[wave];
     uint32_t* qr = s_qr[wave];
-    uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0, last_tile = 0;
+    uint32_t run = 0, pend = 0, pend_at = 0, head = 0, tail = 0, fill = 0;
     bool direct = false;
     const __amdgpu_buffer_rsrc_t lrs =
-        __builtin_amdgcn_make_buffer_rsrc(P16 ? (void*)list16 : (void*)list, 0, (int)(cap * kEb), 0x00020000);
-    auto enc = [&](uint32_t qid, uint32_t r) { return P16 ? (qid << 7) | (r & 127u) : (qid << 24) | r; };
+        __builtin_amdgcn_make_buffer_rsrc((void*)list, 0, (int)(cap * 4u), 0x00020000);
+    auto enc = [&](uint32_t qid, uint32_t r) { return (qid << 24) | r; };
     auto round = [&](uint32_t nr) {
         const bool has = (uint32_t)lane < nr;
         uint32_t qa = 0, qn = 0, r = 0;
@@ -859,17 +470,7 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             if (qn) atomicAdd(&hist[wave * hs + ei], 1u);
         }
         head += nr;
-        // P16: a token ahead of a row in another tile than the queued row before it
-        uint32_t tok = 0, delta = 0;
-        if (P16) {
-            const uint32_t tr = r >> 7;
-            uint32_t prev = (uint32_t)__shfl_up((int)tr, 1, 64);
-            if (lane == 0) prev = last_tile;
-            tok = has && tr != prev ? 1u : 0u;
-            delta = tr - prev;
-            last_tile = (uint32_t)__builtin_amdgcn_readlane((int)tr, (int)nr - 1);
-        }
-        const uint32_t ne = qn + tok;  // entries this row writes
+        const uint32_t ne = qn;  // entries this row writes
         uint32_t pre = 0, tot = 0;
         const bool single = !__ballot(ne > 1u);
         if (single) {  // the usual case: at most one entry per row
@@ -902,16 +503,14 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
             // pointers and stores through flat)
             auto put = [&](uint32_t i, uint32_t y) {
                 if (!direct) pb[fill + pre + i] = y;
-                else if (P16) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)y, lrs, (int)((run + pre + i) * 2u), 0, 0);
                 else __builtin_amdgcn_raw_buffer_store_b32(y, lrs, (int)((run + pre + i) * 4u), 0, 0);
             };
-            if (P16 && tok) put(0, 0x8000u | delta);
             if (single && ql_lds) {
                 if (qn) put(0, enc(s_ql[qa], r));
             } else if (ql_lds) {
-                for (uint32_t i = 0; i < qn; i++) put(tok + i, enc(s_ql[qa + i], r));
+                for (uint32_t i = 0; i < qn; i++) put(i, enc(s_ql[qa + i], r));
             } else {
-                for (uint32_t i = 0; i < qn; i++) put(tok + i, enc(T.qlist[qa + i], r));
+                for (uint32_t i = 0; i < qn; i++) put(i, enc(T.qlist[qa + i], r));
             }
             if (!direct) fill += tot;
         }
@@ -971,9 +570,8 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
 #pragma unroll
             for (int k = 0; k < (int)(kPb / 64); k++) {
                 const uint32_t i = (uint32_t)(k * 64 + lane);
-                const int off = i < pend ? (int)((pend_at + i) * kEb) : (int)0x80000000u;
-                if (P16) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pb[i], lrs, off, 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, off, 0, 0);
+                const int off = i < pend ? (int)((pend_at + i) * 4u) : (int)0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b32(pb[i], lrs, off, 0, 0);
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -1019,10 +617,7 @@ __global__ __launch_bounds__(kTPB) void k_ssk_count(const int* __restrict__ col,
         }
     }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) {
-        if (P16) list16[pend_at + i] = (uint16_t)pb[i];
-        else list[pend_at + i] = pb[i];
-    }
+    for (uint32_t i = (uint32_t)lane; i < pend; i += 64) list[pend_at + i] = pb[i];
     __builtin_amdgcn_wave_barrier();
     fill = 0;
     direct = true;
@@ -1080,11 +675,6 @@ constexpr int kSpBatch = 4;                     // rounds whose pairs are loaded
 // at Q = 150 on 1e9 rows; 8192-pair chunks (2 waves per SIMD) took 0.77 ms.
 // `pairs` is clobbered: the padding stores of a chunk land on pairs of that chunk
 // already read (hence not const, not __restrict__).
-// P16: the 16-bit list of k_ssk_count<*, true> (cap in entries). A round's tokens give
-// each lane's tile by a wave scan of their deltas from the wave's running tile; the pair
-// goes to LDS as the u32 form with its row relative to the wave's part of the chunk,
-// and the part's first tile (the chunk's, plus the deltas of the waves before it) is
-// added when the pairs are placed. Tokens take a list slot but no output slot.
 // Up to kArgQ output pointers by value (the kernel's argument block): a write that runs
 // only the scatter then needs no upload before it.
 constexpr int kArgQ = kMaxQ;  // 2 KB of arguments (the limit is 4 KB)
@@ -1092,7 +682,7 @@ struct SsArgOuts {
     int* p[kArgQ];
 };
 
-template <bool P16, int SW>
+template <int SW>
 __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uint64_t cap,
                                                       const uint32_t* __restrict__ npairs,
                                                       const unsigned long long* __restrict__ offs, uint64_t nwc,
@@ -1113,14 +703,11 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
     __shared__ unsigned long long s_run[kMaxQ];
     __shared__ gint* s_out[kMaxQ];
     __shared__ uint32_t s_wsum[SW];
-    __shared__ uint32_t s_wt[SW];  // P16: tiles a wave's part of the chunk advances
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long ltmask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint64_t wc = blockIdx.x;
     const uint32_t np = npairs[wc];
-    uint32_t* const list = pairs + wc * cap;  // (the u32 form only)
-    uint16_t* const list16 = reinterpret_cast<uint16_t*>(pairs) + wc * cap;
-    uint32_t ctile = 0;  // P16: the tile at the chunk's first entry
+    uint32_t* const list = pairs + wc * cap;
     const uint64_t row0 = (wc / kWaves) * rpb + (wc % kWaves) * (rpb / kWaves);
     for (int i = tid; i < q; i += TPB) {
         s_run[i] = offs[(uint64_t)i * nwc + wc] - offs[(uint64_t)i * nwc];
@@ -1134,7 +721,7 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
 #pragma unroll
         for (int r = 0; r < kSpRounds; r++) {
             const uint32_t idx = c0 + (uint32_t)(wave * kSpPerWave + r * 64 + lane);
-            nx[r] = idx < np ? (P16 ? (uint32_t)list16[idx] : list[idx]) : 0u;
+            nx[r] = idx < np ? list[idx] : 0u;
         }
     };
     load_chunk(0);
@@ -1146,7 +733,6 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
         for (int i = tid; i < SW * kMaxQ; i += TPB) (&s_cnt[0][0])[i] = 0;
         __syncthreads();
         // this wave's 1024 pairs of the chunk
-        uint32_t wt = 0;  // P16: tiles advanced so far in this wave's part
 #pragma unroll
         for (int r0 = 0; r0 < kSpRounds; r0 += kSpBatch) {
             uint32_t x[kSpBatch];
@@ -1155,22 +741,8 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
 #pragma unroll
             for (int b = 0; b < kSpBatch; b++) {
                 const uint32_t li = (uint32_t)(wave * kSpPerWave + (r0 + b) * 64 + lane);
-                bool valid = c0 + li < np;
-                uint32_t qid = x[b] >> 24, y = x[b];
-                if (P16) {
-                    const bool tk = valid && (x[b] & 0x8000u);
-                    uint32_t inc = tk ? (x[b] & 0x7FFFu) : 0u;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
-                        if (lane >= o) inc += t;
-                    }
-                    const uint32_t tile = wt + inc;
-                    wt += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-                    valid = valid && !tk;
-                    qid = (x[b] >> 7) & 0xFFu;
-                    y = valid ? (qid << 24) | (tile * 128u + (x[b] & 127u)) : 0xFFFFFFFFu;
-                }
+                const bool valid = c0 + li < np;
+                const uint32_t qid = x[b] >> 24, y = x[b];
                 const unsigned long long peers = match_any8(qid, __ballot(valid));
                 const uint32_t before = valid ? s_cnt[wave][qid] : 0u;
                 s_buf[li] = y;
@@ -1181,7 +753,6 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
                 __builtin_amdgcn_wave_barrier();
             }
         }
-        if (P16 && lane == 0) s_wt[wave] = wt;
         __syncthreads();
         // bucket starts: queries in order, waves in order inside a query
         uint32_t tq = 0;
@@ -1212,28 +783,12 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
         }
         __syncthreads();
         const uint32_t cn = np - c0 < (uint32_t)CH ? np - c0 : (uint32_t)CH;
-        // the chunk's pairs (P16: its entries less the tokens)
-        uint32_t cnv = 0;
-#pragma unroll
-        for (int w = 0; w < SW; w++) cnv += s_wsum[w];
-        uint32_t wrow[SW];  // P16: the first row of each wave's part
-        {
-            uint32_t a = ctile;
-#pragma unroll
-            for (int w = 0; w < SW; w++) {
-                wrow[w] = a * 128u;
-                if (P16) a += s_wt[w];
-            }
-            ctile = a;
-        }
         uint32_t px[(CH / TPB)], pd[(CH / TPB)];
 #pragma unroll
         for (int k = 0; k < (CH / TPB); k++) {
             const uint32_t i = (uint32_t)(k * TPB + tid);
             px[k] = s_buf[i];
-            const bool pair = i < cn && (!P16 || px[k] != 0xFFFFFFFFu);
-            pd[k] = pair ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
-            if (P16 && pair) px[k] += wrow[i / kSpPerWave];
+            pd[k] = i < cn ? s_cnt[i / kSpPerWave][px[k] >> 24] + s_loc[i] : 0xFFFFFFFFu;
         }
         __syncthreads();
 #pragma unroll
@@ -1244,12 +799,11 @@ __global__ __launch_bounds__(64 * SW, 4) void k_ssp_scatter(uint32_t* pairs, uin
         // pair of this chunk already read (the slice is not read again): with a
         // data-dependent count the wait for the next chunk's loads at the loop's top was
         // vmcnt(0), i.e. also for every store of this chunk
-        // (P16: `list` is not this slice's start, cap counting 16-bit entries)
-        gint* const dummy = P16 ? (gint*)(list16 + c0) : (gint*)(list + c0);
+        gint* const dummy = (gint*)(list + c0);
 #pragma unroll
         for (int k = 0; k < (CH / TPB); k++) {
             const uint32_t i = (uint32_t)(k * TPB + tid);
-            const bool in = i < cnv;
+            const bool in = i < cn;
             const uint32_t y = s_buf[i], qid = in ? y >> 24 : 0u;
             gint* const dst = in ? s_dst[qid] + i : dummy;
             *dst = (int)(row0 + (y & 0xFFFFFFu)) + base;
@@ -1337,9 +891,8 @@ struct SsLayout {
 // EI tables in the workspace: bounds, bucket table, qoff, qab, then qlist
 constexpr size_t kEiBoundsB = (size_t)kEiMax * 4, kEiBucketB = (size_t)kBuckets * 4,
                  kEiQoffB = (size_t)kEiMax * 4, kEiQabB = (size_t)kMaxQ * 4,
-                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2, kEiCovB = (size_t)kCoarse / 8,
-                 kEiCellB = (size_t)kCells * 2;
-constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB + kEiCellB + kEiQlistB;
+                 kEiQlistB = (size_t)kEiMax * kMaxQ * 2, kEiCellB = (size_t)kCells * 2;
+constexpr size_t kEiBytes = kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCellB + kEiQlistB;
 
 SsLayout ss_layout(uint64_t nwc, int q) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1453,11 +1006,9 @@ struct SsState {
     int q, qk;
     uint64_t n;
     const int32_t* col;
-    bool ei;    // elementary-interval kernels (qk >= kEiMinQ)
     EiMeta meta;
     int32_t base;  // first row number of this (row-shard) column
     bool pairs;    // the count pass listed the pairs (single pass)
-    bool p16;      // ... as 16-bit entries (k_ssk_count<*, true>)
     bool flag_known;  // the host read the overflow word after the count (flag) ...
     unsigned int flag;
     uint64_t pairs_total;  // ... and the totals (their sum)
@@ -1493,7 +1044,6 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used, u
     static thread_local int32_t hb[kEiMax];
     static thread_local uint32_t hbkt[kBuckets], hqoff[kEiMax], hqab[kMaxQ];
     static thread_local uint16_t hql[(size_t)kEiMax * kMaxQ];
-    static thread_local uint32_t hcov[kCoarse / 32];
     for (int j = 0; j < m; j++) hb[j] = (int32_t)b[j];
     std::vector<int> ea(qk), eb(qk);
     for (int i = 0; i < qk; i++) {
@@ -1532,28 +1082,6 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used, u
             hbkt[k] = (uint32_t)el | ((uint32_t)eh << 16);
         }
     }
-    // coverage bitmap: cell c (values bmin + [c, c+1) << cshift) is set when a covered
-    // EI meets it; EI e (1 <= e < m) holds [b[e-1], b[e]), EI m holds [b[m-1], ...)
-    int cshift = 0;
-    while (((bmax - bmin) >> cshift) >= kCoarse - 1) cshift++;  // the last cell: outside
-    {
-        static thread_local int diff[kCoarse + 1];
-        std::fill(diff, diff + kCoarse + 1, 0);
-        for (int e = 1; e <= m; e++) {
-            if (hqoff[e + 1] == hqoff[e]) continue;
-            const long long lo = b[e - 1], hi = e < m ? b[e] - 1 : bmax;
-            diff[(lo - bmin) >> cshift]++;
-            diff[((hi - bmin) >> cshift) + 1]--;
-        }
-        std::fill(hcov, hcov + kCoarse / 32, 0u);
-        int acc = 0;
-        const int cmax = (int)((bmax - bmin) >> cshift);  // bmax's cell
-        const bool tail = hqoff[m + 1] > hqoff[m];       // EI m = [bmax, ...) is covered
-        for (int c = 0; c < kCoarse; c++) {
-            acc += diff[c];
-            if (acc > 0 || (c > cmax && tail)) hcov[c >> 5] |= 1u << (c & 31);
-        }
-    }
     // k_ssk_count's cell table: one u16 per cell of 2^xshift values from bmin (the last
     // cell also takes every value below bmin and past the table, by the clamp)
     int xshift = 0;
@@ -1577,9 +1105,9 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used, u
         }
         // past bmax's cell every value is in EI m; below bmin (wrapped) in EI 0
         hcell[kCells - 1] = hqoff[m + 1] > hqoff[m] ? (uint16_t)0x8000 : (uint16_t)0;
-        std::memcpy(region + kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB + kEiCovB, hcell, kEiCellB);
+        std::memcpy(region + kEiBoundsB + kEiBucketB + kEiQoffB + kEiQabB, hcell, kEiCellB);
     }
-    *meta = EiMeta{m, shift, (int)bmin, (int)bmax, cshift, xshift};
+    *meta = EiMeta{m, shift, (int)bmin, (int)bmax, xshift};
     size_t o = 0;
     std::memcpy(region + o, hb, (size_t)m * 4);
     o += kEiBoundsB;
@@ -1589,8 +1117,6 @@ int ei_build(const Pred* hp, int qk, char* region, EiMeta* meta, size_t* used, u
     o += kEiQoffB;
     std::memcpy(region + o, hqab, (size_t)qk * 4);
     o += kEiQabB;
-    std::memcpy(region + o, hcov, kEiCovB);
-    o += kEiCovB;
     o += kEiCellB;  // the cell table, written above
     if (at) std::memcpy(region + o, hql, (size_t)at * 2);
     *used = o + (size_t)at * 2;
@@ -1609,8 +1135,6 @@ EiTables ei_tables(char* region) {
     o += kEiQoffB;
     T.qab = reinterpret_cast<const uint32_t*>(region + o);
     o += kEiQabB;
-    T.cov = reinterpret_cast<const uint32_t*>(region + o);
-    o += kEiCovB;
     T.cell = reinterpret_cast<const uint16_t*>(region + o);
     o += kEiCellB;
     T.qlist = reinterpret_cast<const uint16_t*>(region + o);
@@ -1646,27 +1170,18 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     }
     char* w = static_cast<char*>(d_ws);
     const bool vec = aligned16(d_col);
-    const char* emin = getenv("MQ_SS_EI_MIN");  // A/B of the threshold
-    const bool ei = qk >= (emin ? atoi(emin) : kEiMinQ) && getenv("MQ_SS_IMPL") == nullptr;  // MQ_SS_IMPL=ballot: A/B
-    // the grid is sized for the kernel that reads the column: the k-major count pass of
-    // the single-pass EI path (its LDS allows 3 blocks a CU), else the write pass
-    static const bool filt = getenv("MQ_SS_COUNT") && strcmp(getenv("MQ_SS_COUNT"), "filter") == 0;
-    const bool kmajor = ei && !filt && getenv("MQ_SS_TWOPASS") == nullptr;
+    // the grid is sized for the kernel that reads the column: the single-pass count,
+    // or (MQ_SS_TWOPASS=1: the column pass forced, as a pair-slice overflow takes it)
+    // the write pass
+    const bool kmajor = getenv("MQ_SS_TWOPASS") == nullptr;
     // k_ssk_count with the next group's loads issued ahead from kSsPfMinQ queries (1e9
     // rows, 0.1 % each, alternating on one box: Q = 150 1.85 -> 1.81 ms, Q = 16 0.93 ->
     // 0.96 ms, where the rounds are few and the stream alone sets the time);
-    // MQ_SS_PF=0 / 1 forces it off / on (A/B)
+    // MQ_SS_PF=0 / 1 forces it off / on (tuning)
     static const char* pfe = getenv("MQ_SS_PF");
     const bool pf = pfe ? pfe[0] != '0' : qk >= kSsPfMinQ;
-    // MQ_SS_P16=1: the k-major pass lists 16-bit entries (k_ssk_count<*, true>). Measured
-    // and not the default: half the list bytes, yet Q = 150 1.76 -> 1.86 ms and Q = 16
-    // 0.87 -> 0.92 (count + write, alternating on one box, profiles/r05_ss_host_ab.log)
-    const char* p16e = getenv("MQ_SS_P16");  // read per call (tests toggle it)
-    const bool p16w = kmajor && p16e && p16e[0] == '1';
-    const void* fn = kmajor ? (pf ? (p16w ? (const void*)&k_ssk_count<true, true> : (const void*)&k_ssk_count<true, false>)
-                                  : (p16w ? (const void*)&k_ssk_count<false, true> : (const void*)&k_ssk_count<false, false>))
-                   : ei     ? (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>)
-                            : (vec ? (const void*)&k_ss_write<true> : (const void*)&k_ss_write<false>);
+    const void* fn = kmajor ? (pf ? (const void*)&k_ssk_count<true> : (const void*)&k_ssk_count<false>)
+                            : (vec ? (const void*)&k_ssi_write<true> : (const void*)&k_ssi_write<false>);
     // preds, slot, EI tables and the zeroed flag: one upload from pinned staging (their
     // offsets do not depend on the grid, the EI tables size k_ssk_count's LDS)
     const SsLayout L0 = ss_layout(1, 1);
@@ -1675,10 +1190,10 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     std::memcpy(up + L0.preds, hp, sizeof(Pred) * (qk > 0 ? qk : 1));
     std::memcpy(up + L0.slot, hslot, sizeof(int) * q);
     std::memset(up + L0.flag, 0, 4);
-    EiMeta meta{0, 0, 0, 0, 0, 0};
+    EiMeta meta{0, 0, 0, 0, 0};
     size_t ei_used = 0;
     uint32_t nql = 0;
-    if (ei && (rc = ei_build(hp, qk, up + L0.ei, &meta, &ei_used, &nql))) return rc;
+    if (qk > 0 && (rc = ei_build(hp, qk, up + L0.ei, &meta, &ei_used, &nql))) return rc;
     const uint32_t qlcap = nql <= (uint32_t)kQlCap ? nql : 0u;
     const size_t dyn = kmajor ? ssk_dyn_bytes(meta.m, qlcap) : 0;
     // blocks a CU for the k-major pass: with the tables in dynamic LDS 5-6 fit, but fewer,
@@ -1697,63 +1212,29 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     const uint64_t cap = pair_cap(rpb);
     const bool single = n && getenv("MQ_SS_TWOPASS") == nullptr &&
                         ws_bytes >= L.pairs + (size_t)nwc * cap * sizeof(uint32_t) && cap < (1ull << 24);
-    // 16-bit entries: twice as many in the same slice bytes; tile deltas < 2^15
-    const bool p16 = p16w && single && cap <= (1ull << 22);
     if ((rc = staging_put(0, w, L.ei + ei_used, st))) return rc;
-    const Pred* dp = reinterpret_cast<const Pred*>(w + L.preds);
     uint32_t* counts = reinterpret_cast<uint32_t*>(w + L.counts);
     unsigned long long* offs = reinterpret_cast<unsigned long long*>(w + L.offs);
     if (qk > 0) {
-        if (single && ei) {
-            const EiTables T = ei_tables(w + L.ei);
+        const EiTables T = ei_tables(w + L.ei);
+        if (single) {
             uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
             uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
             unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
-            // MQ_SS_COUNT=filter keeps the coverage-bitmap pass (A/B)
-            if (filt) {
-                if (vec)
-                    hipLaunchKernelGGL(k_ssp_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                       nwc, pr, cap, npr, of);
-                else
-                    hipLaunchKernelGGL(k_ssp_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts,
-                                       nwc, pr, cap, npr, of);
-                LAUNCHCHK("k_ssp_count");
-            } else {
-                const uint64_t ce = p16 ? 2 * cap : cap;  // slice capacity in entries
-                if (pf && p16)
-                    hipLaunchKernelGGL((k_ssk_count<true, true>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of, qlcap);
-                else if (pf)
-                    hipLaunchKernelGGL((k_ssk_count<true, false>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of, qlcap);
-                else if (p16)
-                    hipLaunchKernelGGL((k_ssk_count<false, true>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of, qlcap);
-                else
-                    hipLaunchKernelGGL((k_ssk_count<false, false>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk,
-                                       counts, nwc, pr, ce, npr, of, qlcap);
-                LAUNCHCHK("k_ssk_count");
-            }
-        } else if (ei) {
-            const EiTables T = ei_tables(w + L.ei);
+            if (pf)
+                hipLaunchKernelGGL((k_ssk_count<true>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of, qlcap);
+            else
+                hipLaunchKernelGGL((k_ssk_count<false>), dim3(g), dim3(kTPB), dyn, st, d_col, n, rpb, meta, T, qk, counts,
+                                   nwc, pr, cap, npr, of, qlcap);
+            LAUNCHCHK("k_ssk_count");
+        } else {
             if (vec)
                 hipLaunchKernelGGL(k_ssi_count<true>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
             else
                 hipLaunchKernelGGL(k_ssi_count<false>, dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, meta, T, qk, counts, nwc);
             LAUNCHCHK("k_ssi_count");
-        } else {
-            uint32_t* pr = reinterpret_cast<uint32_t*>(w + L.pairs);
-            uint32_t* npr = reinterpret_cast<uint32_t*>(w + L.npairs);
-            unsigned int* of = reinterpret_cast<unsigned int*>(w + L.flag);
-            if (single) {
-                if (vec) hipLaunchKernelGGL((k_ss_count<true, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
-                else hipLaunchKernelGGL((k_ss_count<false, true>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
-            } else {
-                if (vec) hipLaunchKernelGGL((k_ss_count<true, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
-                else hipLaunchKernelGGL((k_ss_count<false, false>), dim3(g), dim3(kTPB), 0, st, d_col, n, rpb, dp, qk, counts, nwc, pr, cap, npr, of);
-            }
         }
-        LAUNCHCHK("k_ss_count");
         hipLaunchKernelGGL(k_ss_offsets, dim3((uint32_t)qk), dim3(kOffTPB), 0, st, counts, offs, nwc,
                            reinterpret_cast<const int*>(w + L.slot), d_totals, q,
                            reinterpret_cast<const unsigned int*>(w + L.flag), flag_out ? d_totals + q : nullptr);
@@ -1770,11 +1251,9 @@ int ss_count(const int32_t* d_col, uint64_t n, int32_t row_base, const int32_t* 
     state->qk = qk;
     state->n = n;
     state->col = d_col;
-    state->ei = ei;
     state->meta = meta;
     state->base = row_base;
     state->pairs = single && qk > 0;
-    state->p16 = p16 && ei && !filt;
     state->flag_known = false;
     state->flag = 0;
     state->pairs_total = 0;
@@ -1826,38 +1305,25 @@ int ss_write(const SsState& S, int32_t* const* d_pos_out, void* d_ws, hipStream_
     int* const* outs = reinterpret_cast<int* const*>(w + L.outs);
     const unsigned int* of = reinterpret_cast<const unsigned int*>(w + L.flag);
     if (scatter) {
-        if (S.p16)
-            hipLaunchKernelGGL((k_ssp_scatter<true, 4>), dim3((uint32_t)nwc), dim3(kTPB), 0, st,
-                               reinterpret_cast<uint32_t*>(w + L.pairs), 2 * pair_cap(S.rpb),
-                               reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
-                               S.rpb, S.base, of);
-        else if (ss_scatter_waves(S, nwc) == 8)
-            hipLaunchKernelGGL((k_ssp_scatter<false, 8>), dim3((uint32_t)nwc), dim3(512), 0, st,
+        if (ss_scatter_waves(S, nwc) == 8)
+            hipLaunchKernelGGL((k_ssp_scatter<8>), dim3((uint32_t)nwc), dim3(512), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
                                reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
                                S.rpb, S.base, of);
         else
-            hipLaunchKernelGGL((k_ssp_scatter<false, 4>), dim3((uint32_t)nwc), dim3(kTPB), 0, st,
+            hipLaunchKernelGGL((k_ssp_scatter<4>), dim3((uint32_t)nwc), dim3(kTPB), 0, st,
                                reinterpret_cast<uint32_t*>(w + L.pairs), pair_cap(S.rpb),
                                reinterpret_cast<const uint32_t*>(w + L.npairs), offs, nwc, S.qk, outs, ao, by_arg,
                                S.rpb, S.base, of);
         LAUNCHCHK("k_ssp_scatter");
     }
     if (!column) return MQ_OK;
-    if (S.ei) {
-        const EiTables T = ei_tables(w + L.ei);
-        if (aligned16(S.col))
-            hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
-        else
-            hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
-        LAUNCHCHK("k_ssi_write");
-        return MQ_OK;
-    }
+    const EiTables T = ei_tables(w + L.ei);
     if (aligned16(S.col))
-        hipLaunchKernelGGL(k_ss_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
+        hipLaunchKernelGGL(k_ssi_write<true>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
     else
-        hipLaunchKernelGGL(k_ss_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
-    LAUNCHCHK("k_ss_write");
+        hipLaunchKernelGGL(k_ssi_write<false>, dim3(S.g), dim3(kTPB), 0, st, S.col, S.n, S.rpb, S.meta, T, dp, S.qk, offs, nwc, outs, S.base, S.pairs ? of : nullptr);
+    LAUNCHCHK("k_ssi_write");
     return MQ_OK;
 }
 

@@ -183,6 +183,7 @@ _SIGS = {
                              C.POINTER(_u64), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_u64)]),
     "mq_shard_devices": (_int, [C.POINTER(_int), _int]),
     "mq_shard_join_times": (None, [C.POINTER(C.c_double)]),
+    "mq_shard_join_inject_failure": (None, [C.c_int]),
     # reference API (query.h:20-50)
     "select_result": (_PR, [_PR, _PR, C.POINTER(_int), C.POINTER(_int), _PS]),
     "select_column": (_PR, [C.POINTER(Column), C.POINTER(_int), C.POINTER(_int), _PS]),

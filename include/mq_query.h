@@ -239,6 +239,11 @@ int mq_shard_join(const int32_t* const* d_c1, const int32_t* const* d_p1, const 
 /* Host wall ms of the last partitioned join's phases: partition, exchange + local join,
  * return exchange + place, total. */
 void mq_shard_join_times(double* ms);
+/* Test hook (no reference counterpart): every device allocation of the next
+ * mq_shard_join calls' phase `phase` fails with MQ_ENOMEM (1 partition, 2 exchange + local
+ * join, 3 return + place, 4 the one-shard join; 0 turns it off). The error paths drain
+ * every worker's stream before buffers go back to the pool. */
+void mq_shard_join_inject_failure(int phase);
 /* Drop every cached device copy. */
 void mq_release_all(void);
 /* Residency counters since load (tests and the bench read them). */

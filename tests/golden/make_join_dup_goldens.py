@@ -5,7 +5,7 @@ oracle/_ref/libref.so is the reference's src/query.c + multimap.c (+ index.c, ut
 compiled unchanged (oracle/Makefile). Keys: the config-5 many-to-many variant of
 oracle/refcpu.c (rc_gen_join_build_dup: every build key twice, rows i and i + n/2;
 rc_gen_join_probe_dup: about half the probes hit, two matches each); positions are
-identity. Records M and the FNV-1a-64 of the interleaved (out1, out2) pairs into
+identity (2^16 .. 2^24). Records M and the FNV-1a-64 of the interleaved (out1, out2) pairs into
 tests/golden/goldens.json under "join_dup".
 Run here, where /root/reference exists:  python tests/golden/make_join_dup_goldens.py
 """
@@ -28,7 +28,7 @@ def main() -> None:
         raise SystemExit("oracle/_ref/libref.so missing: run make -C oracle here first")
     api = Api(refcpu.reference())
     rows = []
-    for logn in (16, 20, 22):
+    for logn in (16, 20, 22, 24):
         n = 1 << logn
         a, b = refcpu.gen_join(n, "build_dup"), refcpu.gen_join(n, "probe_dup")
         p = refcpu.gen_join(n, "iota")

@@ -1,13 +1,13 @@
-"""shared_select at BASELINE's full size (-m gpu, big): VERDICT r02 next-1.
+"""shared_select at BASELINE's full size (-m gpu, big): VERDICT r02 next-1, r05 next-6.
 
 S11 shared_select (src/query.c:439-583) changes behaviour with size: the count pass
 lists (query, row) pairs with 24-bit row offsets into per-wave slices of one pair per
 row, a slice that overflows sends the write to the column pass, and the coverage
-filter's 16384-cell bitmap spans [bmin, bmax] of the queries. On
-the seed-42 1e9-row column (generated on the device) every query's
-output must equal mq_select_positions on the same range, which the 1e9 goldens pin
-(test_gpu_parity.py): K equal, and the two position lists equal element by element
-(their difference, mq_sub, reduces to min = max = 0 on the device).
+filter's cell table spans [bmin, bmax] of the queries. On the seed-42
+1e9-row column (generated on the device) every query's K and the FNV-1a-64
+of its position list must equal the REFERENCE's own shared_select on the same column
+and queries (tests/golden/shared_goldens.json, made by tests/golden/make_shared_goldens.py
+through oracle/_ref/libref.so, the reference's query.c compiled unchanged).
 
 Cases: Q = 16 and Q = 150 ranges of 0.1 % (the bench's sets), through the pair path,
 the forced column pass (MQ_SS_TWOPASS=1), and the drop-in API with two row shards on
@@ -15,6 +15,8 @@ device 0 (host Column, host Result payloads); plus a dense Q = 16 set of 10 % ra
 1.6 pairs per row, which overflows every pair slice.
 """
 import ctypes as C
+import json
+import os
 
 import numpy as np
 import pytest
@@ -25,6 +27,25 @@ from refapi import _libc, make_column, mq, take
 pytestmark = [pytest.mark.gpu, pytest.mark.big]
 
 N = 1_000_000_000
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shared_goldens.json")
+
+
+@pytest.fixture(scope="module")
+def sgold():
+    g = json.load(open(GOLDEN))
+    assert g["n"] == N
+    return g["sets"]
+
+
+def check_set(refcpu, sgold, name, lows, highs, ks, get):
+    """K and the position list's FNV-1a-64 of every query equal the reference's; get(j)
+    returns query j's positions as a host int32 array."""
+    gs = sgold[name]["queries"]
+    assert len(gs) == len(lows)
+    for j, g in enumerate(gs):
+        assert (g["low"], g["high"]) == (int(lows[j]), int(highs[j])), (name, j)
+        assert ks[j] == g["k"], (name, j)
+        assert f"{refcpu.fnv1a64(get(j)):016x}" == g["pos_fnv1a64"], (name, j)
 
 
 @pytest.fixture(scope="module")
@@ -51,34 +72,6 @@ def query_set(q, width, seed=5):
     return lows, (lows + width).astype(np.int32)
 
 
-class Checker:
-    """mq_select_positions of each range (the pinned single-query path) and an exact
-    device comparison of another position list against it."""
-
-    def __init__(self, lib, col):
-        self.lib, self.col = lib, col
-        self.ws = Dev(lib.mq_scan_workspace_bytes(N))
-        self.cnt = Dev(8)
-        self.ref = Dev(N // 5 * 4)  # room for a 20 % range
-        self.diff = Dev(N // 5 * 4)
-        self.agg = Dev(32)
-
-    def positions(self, lo, hi):
-        L = self.lib
-        mq.check(L.mq_select_positions(self.col.ptr, None, N, 1, int(lo), 1, int(hi), self.ref.ptr,
-                                       self.cnt.ptr, self.ws.ptr, self.ws.nbytes, None))
-        return int(self.cnt.get(np.uint64, 1)[0])
-
-    def equal_on_device(self, other_ptr, k):
-        L = self.lib
-        if k == 0:
-            return True
-        mq.check(L.mq_sub(other_ptr, self.ref.ptr, k, self.diff.ptr, None))
-        mq.check(L.mq_reduce(self.diff.ptr, k, self.agg.ptr, self.ws.ptr, self.ws.nbytes, None))
-        a = mq.MqAgg.from_buffer_copy(self.agg.get(np.uint8, 32).tobytes())
-        return (a.count, a.min, a.max) == (k, 0, 0)
-
-
 def run_device(lib, col, lows, highs):
     q = len(lows)
     ws = Dev(lib.mq_shared_select_workspace_bytes(N, q))
@@ -96,20 +89,17 @@ def run_device(lib, col, lows, highs):
 
 @pytest.mark.parametrize("twopass", [False, True], ids=["pairs", "twopass"])
 @pytest.mark.parametrize("q", [16, 150])
-def test_shared_select_1e9_vs_select_positions(lib, col, monkeypatch, q, twopass):
+def test_shared_select_1e9_vs_reference(lib, col, refcpu, sgold, monkeypatch, q, twopass):
     if twopass:
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
     lows, highs = query_set(q, N // 1000)
     ks, outs = run_device(lib, col, lows, highs)
-    chk = Checker(lib, col)
-    for j in range(q):
-        kw = chk.positions(lows[j], highs[j])
-        assert ks[j] == kw, (q, j)
-        assert chk.equal_on_device(outs[j].ptr, kw), (q, j)
-        outs[j].free()
+    check_set(refcpu, sgold, f"q{q}", lows, highs, ks, lambda j: outs[j].get(np.int32, ks[j]))
+    for o in outs:
+        o.free()
 
 
-def test_shared_select_1e9_pair_slice_overflow(lib, col):
+def test_shared_select_1e9_pair_slice_overflow(lib, col, refcpu, sgold):
     """16 ranges of 10 % each: 1.6 (query, row) pairs per row, more than a wave's
     slice holds (one pair per row), so the write runs the column pass on the count
     pass's offsets. Two of the ranges are nested and one is a single value."""
@@ -118,18 +108,15 @@ def test_shared_select_1e9_pair_slice_overflow(lib, col):
     lows[4], highs[4] = 777_777_777, 777_777_778
     ks, outs = run_device(lib, col, lows, highs)
     assert sum(ks) > 1.5 * N
-    chk = Checker(lib, col)
-    for j in range(16):
-        kw = chk.positions(lows[j], highs[j])
-        assert ks[j] == kw, j
-        assert chk.equal_on_device(outs[j].ptr, kw), j
-        outs[j].free()
+    check_set(refcpu, sgold, "q16_dense", lows, highs, ks, lambda j: outs[j].get(np.int32, ks[j]))
+    for o in outs:
+        o.free()
 
 
-def test_shared_select_1e9_api_two_shards(lib, col):
+def test_shared_select_1e9_api_two_shards(lib, col, refcpu, sgold):
     """The drop-in shared_select (query.h) over a host Column, split into two row
     shards on device 0 (mq_shard_config): Q = 150 host payloads, each equal to the
-    single-query device path's positions."""
+    reference's shared_select output (K and FNV)."""
     host = col.get(np.int32, N)
     c = make_column(host)
     arr = (C.c_int * 2)(0, 0)
@@ -144,13 +131,9 @@ def test_shared_select_1e9_api_two_shards(lib, col):
         out = lib.shared_select(ops, q, C.byref(c), C.byref(s))
         assert s.code == mq.OK and out
         assert mq.residency(lib)["shards"] == 2
-        chk = Checker(lib, col)
-        for j in range(q):
-            kw = chk.positions(lows[j], highs[j])
-            got = take(out[j])
-            assert len(got) == kw, j
-            assert np.array_equal(got, chk.ref.get(np.int32, kw)), j
+        got = [take(out[j]) for j in range(q)]
         _libc.free(C.cast(out, C.c_void_p))
+        check_set(refcpu, sgold, "q150", lows, highs, [len(g) for g in got], lambda j: got[j])
     finally:
         lib.mq_release_all()
         assert lib.mq_shard_config(0, None, 0, 0) == 0

@@ -71,22 +71,8 @@ def _data(n, seed):
     return d
 
 
-# MQ_POSITIONS_IMPL (read by libmq per call); "stage_lanes": k_select_stage with its
-# bitmap tiles expanded by lane-scattered stores (MQ_STAGE_EXPAND=0) instead of through
-# the LDS ring
-POS_IMPLS = ["stage", "stage_lanes", "mask", "lookback"]
-
-
-@pytest.fixture(params=POS_IMPLS)
-def pos_impl(request, monkeypatch):
-    monkeypatch.setenv("MQ_POSITIONS_IMPL", "stage" if request.param.startswith("stage") else request.param)
-    if request.param == "stage_lanes":
-        monkeypatch.setenv("MQ_STAGE_EXPAND", "0")
-    return request.param
-
-
 @pytest.mark.parametrize("n", SIZES)
-def test_select_agg_and_positions_vs_oracle(lib, refcpu, n, pos_impl):
+def test_select_agg_and_positions_vs_oracle(lib, refcpu, n):
     d = _data(n, n)
     for off in (0, 1):  # 16-B aligned column and an unaligned (+4 B) one
         dd = Dev.of(d, offset_elems=off)
@@ -107,7 +93,7 @@ def test_select_agg_and_positions_vs_oracle(lib, refcpu, n, pos_impl):
 
 
 @pytest.mark.parametrize("out_off", [1, 2, 3])
-def test_positions_into_unaligned_output(lib, refcpu, out_off, pos_impl):
+def test_positions_into_unaligned_output(lib, refcpu, out_off):
     """The output pointer 4 / 8 / 12 B past a 16-byte boundary: the batched bitmap
     expansion (round 4) flushes its LDS ring as 16-byte stores placed by the output
     address, so a base that is not 16-byte aligned shifts every flush. Dense ranges
@@ -222,7 +208,7 @@ def test_select_sum_in_kernel_combine_32_streams(lib, refcpu):
 
 
 @pytest.mark.parametrize("n", [0, 7, 4097, 200_003, 3_000_017])
-def test_select_result_payload_vs_oracle(lib, refcpu, n, pos_impl):
+def test_select_result_payload_vs_oracle(lib, refcpu, n):
     rng = np.random.default_rng(n + 1)
     vals = rng.integers(-100, 100, n, dtype=np.int32)
     prev = np.sort(rng.choice(10 ** 7, n, replace=False)).astype(np.int32)
@@ -236,7 +222,7 @@ def test_positions_stage_repeated_queued(lib, refcpu):
     """k_select_stage: waves switch from the LDS buffer to bitmap mode at different
     points (selectivities from 0.1 % to 100 %); blocks combine counts across the
     grid at the end. Every launch (three queued back to back, one sync) must
-    equal the oracle's list word for word, with the mask path as a second opinion."""
+    equal the oracle's list word for word."""
     n = 20_000_003
     rng = np.random.default_rng(77)
     d = rng.integers(0, 1000, n, dtype=np.int32)
@@ -246,20 +232,16 @@ def test_positions_stage_repeated_queued(lib, refcpu):
     ws = Dev(lib.mq_scan_workspace_bytes(n))
     outs = [Dev(n * 4) for _ in range(3)]
     cnts = [Dev(8) for _ in range(3)]
-    os.environ["MQ_POSITIONS_IMPL"] = "stage"
-    try:
-        for rep in range(3):
-            for lo, hi in cases:
-                hl, l, hh, h = mq.bounds(lo, hi)
-                for i in range(3):  # three launches queued, one sync
-                    mq.check(lib.mq_select_positions(dd.ptr, None, n, hl, l, hh, h, outs[i].ptr,
-                                                     cnts[i].ptr, ws.ptr, ws.nbytes, None))
-                for i in range(3):
-                    k = int(cnts[i].get(np.uint64, 1)[0])
-                    assert k == len(want[(lo, hi)]), (rep, lo, hi, i)
-                    assert np.array_equal(outs[i].get(np.int32, k), want[(lo, hi)]), (rep, lo, hi, i)
-    finally:
-        os.environ.pop("MQ_POSITIONS_IMPL", None)
+    for rep in range(3):
+        for lo, hi in cases:
+            hl, l, hh, h = mq.bounds(lo, hi)
+            for i in range(3):  # three launches queued, one sync
+                mq.check(lib.mq_select_positions(dd.ptr, None, n, hl, l, hh, h, outs[i].ptr,
+                                                 cnts[i].ptr, ws.ptr, ws.nbytes, None))
+            for i in range(3):
+                k = int(cnts[i].get(np.uint64, 1)[0])
+                assert k == len(want[(lo, hi)]), (rep, lo, hi, i)
+                assert np.array_equal(outs[i].get(np.int32, k), want[(lo, hi)]), (rep, lo, hi, i)
 
 
 @pytest.mark.parametrize("k", [0, 1, 5, 4096, 100_003])
@@ -290,12 +272,9 @@ def test_add_sub_vs_oracle(lib, refcpu, n):
     assert np.array_equal(out.get(np.int32, n), refcpu.sub(a, b))
 
 
-@pytest.mark.parametrize("aux_impl", ["gather", "inline"])
-def test_fused_select_fetch_agg_vs_oracle(lib, refcpu, monkeypatch, aux_impl):
-    """config 3 fused: k_scan_gather (default) and k_scan<kAux> (MQ_AUX_IMPL=inline);
-    dense selections overflow the per-wave LDS buffer many times."""
-    if aux_impl == "inline":
-        monkeypatch.setenv("MQ_AUX_IMPL", "inline")
+def test_fused_select_fetch_agg_vs_oracle(lib, refcpu):
+    """config 3 fused (k_scan_gather); dense selections overflow the per-wave LDS buffer
+    many times."""
     for n in (1, 1023, 4099, 2_000_003):
         d0, d1 = refcpu.gen_uniform(n, 42), refcpu.gen_uniform(n, 43)
         d1[: min(n, 3)] = [I32MIN, I32MAX, -1][: min(n, 3)]
@@ -446,7 +425,7 @@ def _check_positions_exact(lib, col, n, lo, hi, pos):
 
 
 @pytest.mark.big
-def test_positions_spill_boundary_1e9(lib, pos_impl):
+def test_positions_spill_boundary_1e9(lib):
     """k_select_stage's three regimes at full size: LDS ring only, ring + spill to
     the workspace (density below 1/32 with more than 1024 matches per wave), and
     the switch to bitmap mode (past 1/32), on a uniform column and on a bursty one
@@ -659,7 +638,7 @@ def _dev_join(lib, c1, p1, c2, p2):
     return o1.get(np.int32, m), o2.get(np.int32, m)
 
 
-JOIN_PATHS = {"winruns": {}, "winruns16": {"MQ_JOIN_SLOT16": "1"}, "sorted": {"MQ_JOIN_WINRUNS": "0"},
+JOIN_PATHS = {"winruns": {}, "sorted": {"MQ_JOIN_WINRUNS": "0"},
               "cas": {"MQ_JOIN_RUNS": "0"},
               # the windowed runs table probed by random bucket reads / window by window in LDS
               # (round 5: the default from 2^20 build rows, forced here from 2^16)
@@ -673,13 +652,12 @@ JOIN_PATHS = {"winruns": {}, "winruns16": {"MQ_JOIN_SLOT16": "1"}, "sorted": {"M
 
 @pytest.mark.parametrize("path", list(JOIN_PATHS))
 @pytest.mark.parametrize("case", ["unique", "dups", "skew", "neg", "tiny", "empty", "marker",
-                                  "unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned",
+                                  "unique_partitioned", "dups_partitioned",
                                   "ragged_hits", "dups_short_runs", "dups_run_of_15"])
 def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
     """Duplicate keys: winruns (default) partitions the build rows by window and finds
-    each window's runs in LDS (k_win_build_runs); winruns16 the same into 16-byte slots
-    that carry runs of one or two rows (k_win_build_runs16, MQ_JOIN_SLOT16=1);
-    a window over 6144 rows or 3072 keys, or a key on 15+ rows, falls back to: sorted,
+    each window's runs in LDS (k_win_build_runs); a window over 6144 rows or 3072 keys,
+    or a key on 15+ rows, falls back to: sorted,
     the sorted runs behind the windowed table of distinct keys (MQ_JOIN_WINRUNS=0);
     cas: the global-CAS table of run heads (MQ_JOIN_RUNS=0, the last fallback)."""
     for k, v in JOIN_PATHS[path].items():
@@ -719,9 +697,7 @@ def test_hash_join_vs_oracle(lib, refcpu, monkeypatch, case, path):
         c1[1 + rng.choice(len(c1) - 1, 14, replace=False)] = c1[0]
         c2 = rng.choice(keys, 100_000)
         c2[:5] = c1[0]
-    elif case in ("unique_partitioned", "unique_partitioned_nomarks", "dups_partitioned"):
-        if case.endswith("nomarks"):  # the windowed table without overflow marks
-            monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
+    elif case in ("unique_partitioned", "dups_partitioned"):
         # > 2^22 build rows: the window-partitioned insert. Keys from the spread
         # config-5 generator: the oracle restates the reference's `key % size`
         # multimap, which goes quadratic on dense or arithmetic key runs.
@@ -839,20 +815,17 @@ def _inv_fmix32(h):
 
 @pytest.mark.parametrize("probe", ["table", "part"])
 @pytest.mark.parametrize("dup", [False, True])
-@pytest.mark.parametrize("marks", [True, False])
-def test_hash_join_clustered_window(lib, refcpu, monkeypatch, dup, marks, probe):
+def test_hash_join_clustered_window(lib, refcpu, monkeypatch, dup, probe):
     """One 8192-slot window of the unique table holds a 5000-slot cluster: 5000 keys
     homed in 16 buckets at its start, so probes of those keys (hits) and of other keys
     homed there (misses) follow chains of up to ~5000 slots through the per-wave
     continuation queue (requeued every step, then drained at the end; the in-step
-    drain runs when more than 128 rows wait), with and without the overflow marks.
+    drain runs when more than 128 rows wait), past the full buckets' overflow marks.
     dup: every cluster key twice (the runs table behind the same windowed build).
     probe "part": the partitioned probe (unique builds), whose LDS lookups follow the
     same chains inside the window."""
     for k, v in JOIN_PROBE_MODES["part" if probe == "part" else "table"].items():
         monkeypatch.setenv(k, v)
-    if not marks:
-        monkeypatch.setenv("MQ_JOIN_NOMARKS", "1")
     rng = np.random.default_rng(4242)
     n_rand, n_cl = 295_000, 5000
     slots = 1 << 20  # the table of ~300K build rows: 2^20 slots, 128 windows of 8192
@@ -968,23 +941,18 @@ def test_hash_join_golden_2e28(lib, refcpu, goldens):
 # ---------------------------------------------------------------------------
 # S11 shared_select (device API): Q predicates, two passes, exact-size outputs
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("form", ["ei", "ballot", "ei_p16"])
 @pytest.mark.parametrize("twopass", [False, True])
 @pytest.mark.parametrize("n,q", [(0, 3), (1, 2), (5, 1), (4099, 7), (100_003, 150), (1 << 20, 256),
                                  (3_000_017, 20), (2_000_003, 2), (2_000_003, 5),
                                  # round-5 boundaries: 3 -> 4 count blocks a CU (Q 8 / 9),
                                  # output pointers as scatter arguments (Q 32 / 33)
                                  (1_000_003, 8), (1_000_003, 9), (1_000_003, 32), (1_000_003, 33)])
-def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass, form):
-    """Every Q takes the elementary-interval kernels by default (round 5: from Q = 1);
-    "ballot" forces the per-query ballot kernels (MQ_SS_IMPL=ballot), "ei_p16" the
-    count pass's 16-bit pair lists (MQ_SS_P16=1, measured, not the default)."""
+def test_shared_select_vs_oracle(lib, refcpu, monkeypatch, n, q, twopass):
+    """Every Q takes the elementary-interval kernels: the single pass (pairs listed by the
+    count pass, k_ssp_scatter), or the column pass (MQ_SS_TWOPASS=1 forces it; a pair-slice
+    overflow takes it)."""
     if twopass:
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
-    if form == "ballot":
-        monkeypatch.setenv("MQ_SS_IMPL", "ballot")
-    if form == "ei_p16":
-        monkeypatch.setenv("MQ_SS_P16", "1")
     rng = np.random.default_rng(n + q)
     d = rng.integers(-1000, 1000, n, dtype=np.int32)
     if n > 8:
@@ -1033,23 +1001,18 @@ def _shared_run(lib, d, lows, highs):
     return [outs[j].get(np.int32, int(k[j])) for j in range(q)]
 
 
-@pytest.mark.parametrize("impl", ["ei", "ballot", "ei_twopass", "ballot_twopass", "ei_p16", "ei_sw8"])
+@pytest.mark.parametrize("impl", ["ei", "ei_twopass", "ei_sw8"])
 @pytest.mark.parametrize("case", ["sparse150", "nested", "identical", "dense", "extremes",
                                   "mixed256", "narrow_domain"])
 def test_shared_select_many_queries(lib, refcpu, monkeypatch, impl, case):
-    """q >= 12 runs the elementary-interval kernels (MQ_SS_IMPL=ballot forces the
-    per-query ballot kernels); by default the count pass lists (query, row) pairs and
-    k_ssp_scatter writes them (one column read), MQ_SS_TWOPASS=1 forces the column
-    pass (k_ssi_write / k_ss_write), which is also what a pair-slice overflow (the
-    dense case) falls back to. Sparse and dense queries (dense tiles fall back to
+    """The elementary-interval kernels: by default the count pass lists (query, row) pairs
+    and k_ssp_scatter writes them (one column read), MQ_SS_TWOPASS=1 forces the column
+    pass (k_ssi_write), which is also what a pair-slice overflow (the dense case) falls
+    back to. Sparse and dense queries (dense tiles fall back to
     ballots inside k_ssi_write), nested and identical ranges, INT32 extremes, all 256
     queries, a 7-value domain."""
-    if impl.startswith("ballot"):
-        monkeypatch.setenv("MQ_SS_IMPL", "ballot")
     if impl.endswith("twopass"):
         monkeypatch.setenv("MQ_SS_TWOPASS", "1")
-    if impl == "ei_p16":  # the count pass's 16-bit pair lists (not the default)
-        monkeypatch.setenv("MQ_SS_P16", "1")
     if impl == "ei_sw8":  # the scatter's 8-wave blocks, which the default takes for long slices only
         monkeypatch.setenv("MQ_SS_SCATTER_WAVES", "8")
     rng = np.random.default_rng(hash(case) % 2 ** 32)

@@ -165,6 +165,34 @@ def test_shard_join_waits_for_null_stream_writers(lib, refcpu, goldens):
     assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"])
 
 
+@pytest.mark.parametrize("g,phase", [(2, 1), (2, 2), (3, 3), (1, 4)])
+def test_shard_join_injected_failure_then_goldens(lib, refcpu, goldens, g, phase):
+    """an allocation that fails inside a phase (mq_shard_join_inject_failure)
+    must return MQ_ENOMEM with no output and only then hand the phase's buffers back to
+    the pool (every worker drains its stream first, pj_end), so the next join on the
+    same pool is still exact: the 2^20 golden, then the many-to-many 2^20 golden."""
+    rows = [r for r in goldens["join"] if r.get("n") == 1 << 20 and "dup" not in r] + \
+           [r for r in goldens["join_dup"] if r["n"] == 1 << 20]
+    config(lib, g)
+    n = 1 << 20
+    D = _golden_inputs(lib, n, False)
+    b = bounds_of(n, g, 3)
+    V, U = C.c_void_p * g, C.c_uint64 * g
+    ptrs = [V(*[D[k].ptr + 4 * b[s] for s in range(g)]) for k in range(4)]
+    ns = U(*[b[s + 1] - b[s] for s in range(g)])
+    o1, o2, m = V(), V(), U()
+    lib.mq_shard_join_inject_failure(phase)
+    try:
+        rc = lib.mq_shard_join(ptrs[0], ptrs[1], ns, ptrs[2], ptrs[3], ns, o1, o2, m)
+    finally:
+        lib.mq_shard_join_inject_failure(0)
+    assert rc == mq.MQ_ENOMEM
+    for r, dup in ((rows[0], False), (rows[1], True)):
+        D = _golden_inputs(lib, n, dup)
+        a1, a2, _ = shard_join(lib, g, D, n, n, seed=5)
+        assert (len(a1), f"{refcpu.fnv1a64_pairs(a1, a2):016x}") == (r["m"], r["pairs_fnv1a64"]), dup
+
+
 CASES = ["unique", "dups", "skew", "neg", "tiny", "empty_build", "empty_probe", "dups_long", "unique_big"]
 
 
