@@ -65,8 +65,9 @@ int lomuto_sort(const int32_t* col, uint64_t n, int32_t* vout, uint64_t* pout, h
 // idle blocks are released by mq_trim(). A freed block may be handed out again at
 // once, so callers free only what no queued kernel still uses (sync first);
 // pool_free_on(p, st) is the stream-ordered free: an event recorded on st marks
-// when the block may be reused, and pool_alloc waits for it (or picks another
-// block) before handing the block out again. Call it with the block's device current.
+// when the block may be reused: pool_alloc hands it out only once that has passed,
+// takes a fresh block while it is pending, and waits for it only when no fresh block
+// fits in HBM. Call it with the block's device current.
 void* pool_alloc(size_t bytes);
 void pool_free(void* p);
 void pool_free_on(void* p, hipStream_t st);

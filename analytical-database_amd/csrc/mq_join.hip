@@ -803,8 +803,9 @@ __device__ __forceinline__ void win_load(const u64* __restrict__ in, uint32_t b,
 
 // The window's c words (c <= kCsrCap, threads' words vs[k] = word threadIdx + k * kWinTPB)
 // grouped by bucket into csr; boff[b] .. boff[b + 1] = bucket b's words. Ends synced.
+// cidx (when not null): each grouped word's index in the window's stretch (input order).
 __device__ __forceinline__ void csr_build(const u64 (&vs)[kWinPer], uint32_t c, const Win& t, u64* csr,
-                                          uint32_t* boff, uint32_t* wsum) {
+                                          uint32_t* boff, uint32_t* wsum, uint16_t* cidx = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t x = tid; x <= kCsrBuckets; x += kWinTPB) boff[x] = 0;
     __syncthreads();
@@ -843,23 +844,28 @@ __device__ __forceinline__ void csr_build(const u64 (&vs)[kWinPer], uint32_t c, 
 #pragma unroll
     for (int k = 0; k < kWinPer; k++) {
         const uint32_t i = (uint32_t)tid + (uint32_t)k * kWinTPB;
-        if (i < c) csr[boff[csr_bucket((uint32_t)vs[k], t)] + rk[k]] = vs[k];
+        if (i < c) {
+            const uint32_t x = boff[csr_bucket((uint32_t)vs[k], t)] + rk[k];
+            csr[x] = vs[k];
+            if (cidx) cidx[x] = (uint16_t)i;
+        }
     }
     __syncthreads();
 }
 
 // One window at a time per block: the window's build words grouped in LDS, then each of
 // the window's probe keys (partitioned order) looks itself up in its bucket. r[i] =
-// payload << 32 | 1 on a hit, 0 on a miss. The build was not checked: a window over
-// kCsrCap words, or a probe key that finds two build words, sets *flag, and the caller
-// rebuilds without the partition (the table's empty word is an ordinary word here).
+// payload << 32 | 1 on a hit, 0 on a miss. The build was not checked: a probe key that
+// finds two build words sets bit 0 of *flag (the caller probes again with the duplicate-
+// capable k_win_join_runs), a window over kCsrCap words bit 1 (the caller rebuilds
+// without the partition; the table's empty word is an ordinary word here).
 template <typename RT>
 __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bwords,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ pkeys,
                                                       const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
                                                       RT* __restrict__ r, uint32_t* __restrict__ flag,
-                                                      uint32_t sentinel) {
+                                                      uint32_t sentinel, unsigned long long* __restrict__ mtot) {
     __shared__ u64 csr[kCsrCap];
     __shared__ uint32_t boff[kCsrBuckets + 1];
     __shared__ uint32_t wsum[kWinTPB / 64];
@@ -873,7 +879,8 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
             key[k] = i < pe ? __builtin_nontemporal_load(pkeys + i) : 0u;
         }
     };
-    bool dup = false;
+    bool dup = false, overfull = false;
+    unsigned long long nhit = 0;  // the window joins' pairs (M, for the fused write)
     // a key on two build words shows up only where a probe key matches it (duplicates no
     // probe row meets do not change the unique output): then the flag
     auto lookup = [&](uint32_t key) -> RT {
@@ -886,6 +893,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
             if ((uint32_t)v == key) out = (v & 0xFFFFFFFF00000000ull) | 1ull, hits++;
         }
         dup |= hits > 1;
+        nhit += hits ? 1u : 0u;
         if constexpr (sizeof(RT) == 4) return hits ? (uint32_t)(out >> 32) : sentinel;
         else return out;
     };
@@ -918,7 +926,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
             vs[k] = vn[k];
         }
         if (over) {
-            dup = true;
+            overfull = true;
         } else {
 #pragma unroll
             for (int k = 0; k < kJoinPer; k++) {
@@ -933,7 +941,10 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
         b = bn, e = en, pb = pbn, pe = pen;
         bn = bnn, en = enn, pbn = pbnn, pen = penn;
     }
-    if (dup) *flag = 1;
+    if (dup || overfull) atomicOr(flag, (dup ? 1u : 0u) | (overfull ? 2u : 0u));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nhit += __shfl_xor(nhit, o, 64);
+    if ((threadIdx.x & 63) == 0 && nhit) atomicAdd(mtot, nhit);
 }
 
 // The partitioned probe of a windowed RUNS table (duplicate keys, k_win_build_runs: the
@@ -941,18 +952,14 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
 // global table is loaded into LDS whole (coalesced) and each of the window's probe keys
 // follows the table's own probe sequence there (home bucket, linear inside the window,
 // an empty slot ends it). r[i] = the slot's packed run, 0 = no match (a run is never
-// empty, so a hit's payload is never 0).
-// RT = u64 (run2): a run of one or two rows carries its build positions (read from the
-// run array, whose window slice stays in the XCD's L2 while the block works on it), so
-// the write streams instead of fetching a random run line per row: {p0, p1} with p1 =
-// S (the sentinel, outside the payloads) for one row, {S, packed} for a longer run,
-// {S, 0} for a miss.
+// empty, so a hit's payload is never 0). (Round 5's u64 form carried short runs' build
+// positions from the run array; round 6's k_win_join_runs does that without the table.)
 template <typename RT>
 __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict__ words,
                                                            const uint32_t* __restrict__ pkeys,
                                                            const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
-                                                           RT* __restrict__ r, const int* __restrict__ bpos,
-                                                           uint32_t S) {
+                                                           RT* __restrict__ r) {
+    static_assert(sizeof(RT) == 4, "packed runs");
     __shared__ u64 tab[1 << kWinLog];
     const uint32_t W = (uint32_t)t.wmask + 1, G = gridDim.x;
     uint32_t w = blockIdx.x;
@@ -976,14 +983,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict
             }
             h = (h + 1) & (W - 1);
         }
-        if constexpr (sizeof(RT) == 4) {
-            return pk;
-        } else {
-            const uint32_t L = pk & 15u, a = pk >> 4;
-            if (L == 0u || L > 2u) return (u64)S | ((u64)pk << 32);
-            const uint32_t p0 = (uint32_t)bpos[a], p1 = L == 2u ? (uint32_t)bpos[a + 1] : S;
-            return (u64)p0 | ((u64)p1 << 32);
-        }
+        return pk;
     };
     uint32_t pb = pstartw[w], pe = pstartw[w + 1];
     u64 vs[kWinPer];
@@ -1017,6 +1017,141 @@ __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict
         key_load(pbn, pen, key);
         pb = pbn, pe = pen, pbn = pbnn, pen = penn;
     }
+}
+
+// The partitioned probe for DUPLICATE build keys (round 6): no runs table. The build
+// words stay partitioned by window as for unique keys (the stable LSD passes keep a
+// window's words in input order, their stretch index i); per window the block groups
+// them by bucket in LDS (csr_build, with each word's i) and answers each probe key of
+// the window from its bucket: the words of equal key are the key's build rows, ordered
+// by i (build-insertion order, query.c:669-681). r[k] is the run2 record the gathers
+// and the write read: {p0, S} for one row, {p0, p1} for two (in order), {S, (b + s) << 4
+// | L} for L = 3..14 rows, whose build positions are in bpos[b + s ...] in insertion
+// order (s = the run's place when the bucket is ordered by (key, i), so every run has its
+// own stretch inside the window's; written by the probe keys that meet the run, each the
+// same values), and {S, 0} for a miss. S: a value outside the build payloads (the host
+// checks one exists). A window over kCsrCap words or a probed key on 15+ rows sets *flag
+// (the caller rebuilds on the sorted runs); *mtot += the pairs (sum of L over the probe
+// keys).
+// Replaces k_win_build_runs (the 4 GB runs table written by the build, 1.9 ms at 2^28)
+// and k_win_probe_tab (reading it back, 1.76 ms).
+__global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict__ bwords,
+                                                           const uint32_t* __restrict__ bstart,
+                                                           const uint32_t* __restrict__ pkeys,
+                                                           const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
+                                                           u64* __restrict__ r, int* __restrict__ bpos,
+                                                           uint32_t* __restrict__ flag, unsigned long long* mtot,
+                                                           uint32_t S) {
+    __shared__ u64 csr[kCsrCap];
+    __shared__ uint32_t boff[kCsrBuckets + 1];
+    __shared__ uint16_t cidx[kCsrCap];
+    __shared__ uint32_t wsum[kWinTPB / 64];
+    const uint32_t G = gridDim.x;
+    uint32_t w = blockIdx.x;
+    if (w >= nwin) return;
+    auto key_load = [&](uint32_t pb, uint32_t pe, uint32_t (&key)[kJoinPer]) {
+#pragma unroll
+        for (int k = 0; k < kJoinPer; k++) {
+            const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+            key[k] = i < pe ? __builtin_nontemporal_load(pkeys + i) : 0u;
+        }
+    };
+    bool bad = false;
+    unsigned long long pairs = 0;
+    // key k's words in bucket [x0, x1): count L, those below k (its run's place in the
+    // bucket ordered by (key, i)), and the first two by i
+    auto scan_bucket = [&](uint32_t key, uint32_t b, uint32_t x0, uint32_t x1, uint32_t& L, uint32_t& lt,
+                           uint32_t& p0, uint32_t& p1) {
+        // the first two matches in bucket order, then put in input order (selects, no
+        // array: an insertion by index compiled to a scratch array)
+        uint32_t n = 0, ia = 0, ib = 0, pa = S, pb = S;
+        for (uint32_t x = x0; x < x1; x++) {
+            const u64 v = csr[x];
+            if ((uint32_t)v == key) {
+                const uint32_t i = cidx[x], p = (uint32_t)(v >> 32);
+                ia = n == 0 ? i : ia;
+                pa = n == 0 ? p : pa;
+                ib = n == 1 ? i : ib;
+                pb = n == 1 ? p : pb;
+                n++;
+            }
+        }
+        const bool sw = n == 2 && ib < ia;
+        p0 = sw ? pb : pa;
+        p1 = sw ? pa : pb;
+        L = n;
+        lt = 0;
+        if (n >= 3u) {
+            // a long run: its place in the bucket ordered by (key, i), and its rows' payloads
+            // written there in insertion order by every probe key that meets it (the same
+            // values to the same places: no race); no key of the window pays otherwise
+            for (uint32_t x = x0; x < x1; x++) lt += (uint32_t)csr[x] < key ? 1u : 0u;
+            if (n < 15u)
+                for (uint32_t x = x0; x < x1; x++) {
+                    const u64 v = csr[x];
+                    if ((uint32_t)v != key) continue;
+                    const uint32_t me = cidx[x];
+                    uint32_t rk = 0;
+                    for (uint32_t y = x0; y < x1; y++)
+                        rk += ((uint32_t)csr[y] == key && cidx[y] < me) ? 1u : 0u;
+                    bpos[b + x0 + lt + rk] = (int)(uint32_t)(v >> 32);
+                }
+            else
+                bad = true;  // not packable: the caller takes the sorted runs
+        }
+    };
+    auto lookup = [&](uint32_t key, uint32_t b) -> u64 {
+        const uint32_t bk = csr_bucket(key, t);
+        const uint32_t x0 = boff[bk], x1 = boff[bk + 1];
+        uint32_t L, lt, p0, p1;
+        scan_bucket(key, b, x0, x1, L, lt, p0, p1);
+        pairs += L;
+        if (L == 0) return (u64)S;
+        if (L <= 2) return (u64)p0 | ((u64)p1 << 32);
+        return (u64)S | ((u64)(((b + x0 + lt) << 4) | (L < 15u ? L : 15u)) << 32);
+    };
+    uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
+    u64 vs[kWinPer];
+    uint32_t key[kJoinPer];
+    win_load(bwords, b, e, vs);
+    key_load(pb, pe, key);
+    uint32_t bn = 0, en = 0, pbn = 0, pen = 0;
+    if (w + G < nwin) bn = bstart[w + G], en = bstart[w + G + 1], pbn = pstartw[w + G], pen = pstartw[w + G + 1];
+    __builtin_amdgcn_s_waitcnt(0);  // (see k_win_join)
+    for (; w < nwin; w += G) {
+        u64 vn[kWinPer];
+        win_load(bwords, bn, en, vn);
+        uint32_t bnn = 0, enn = 0, pbnn = 0, penn = 0;
+        if (w + 2 * G < nwin)
+            bnn = bstart[w + 2 * G], enn = bstart[w + 2 * G + 1], pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
+        const uint32_t c = e - b;
+        const bool over = c > kCsrCap;  // uniform
+        if (!over) csr_build(vs, c, t, csr, boff, wsum, cidx);
+#pragma unroll
+        for (int k = 0; k < kWinPer; k++) {
+            asm volatile("" : "+v"(vn[k]));  // (see k_win_join)
+            vs[k] = vn[k];
+        }
+        if (over) {
+            bad = true;
+        } else {
+#pragma unroll
+            for (int k = 0; k < kJoinPer; k++) {
+                const uint32_t i = pb + threadIdx.x + (uint32_t)k * kWinTPB;
+                if (i < pe) __builtin_nontemporal_store(lookup(key[k], b), r + i);
+            }
+            for (uint32_t i = pb + threadIdx.x + (uint32_t)kJoinPer * kWinTPB; i < pe; i += kWinTPB)
+                __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i), b), r + i);
+            __syncthreads();
+        }
+        key_load(pbn, pen, key);
+        b = bn, e = en, pb = pbn, pe = pen;
+        bn = bnn, en = enn, pbn = pbnn, pen = penn;
+    }
+    if (bad) *flag = 1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pairs += __shfl_xor(pairs, o, 64);
+    if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(mtot, pairs);
 }
 
 // The inverse of one k_pwin_scatter pass: keys = that pass's input (tile order), rin =
@@ -1153,6 +1288,233 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
         } else {
             if (i < n) __builtin_nontemporal_store(v, rout + i);
         }
+    }
+}
+
+// The last inverse pass fused with the pair write (round 6): k_pwin_gather<true>'s tile
+// (4096 probe rows in row order; each row's result taken back from the window join's
+// order) counts its pairs, learns the pairs of every earlier tile by decoupled look-back
+// and writes its rows' pairs straight to out1 / out2, so neither the per-row results
+// (pstart, p01: 4-12 B a row written and read back) nor the hit words, their scan and a
+// separate write pass exist. MODE 0: unique, u32 results (sentinel = miss); 1: unique,
+// u64 {payload << 32 | 1} (0 = miss); 2: run2 records (k_win_join_runs), runs of 3-14
+// rows read from bpos. Tiles are numbered by a ticket taken at the block's start, so
+// every tile a block waits for belongs to a block that is already running.
+// status[t] = kLbAgg | the tile's pairs, then kLbPre | the pairs of tiles 0..t.
+constexpr u64 kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ u64 lb_load(const u64* p) {
+    return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename RT, int MODE>
+__global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __restrict__ keys, uint64_t n, Win t,
+                                                            const u64* __restrict__ goff, uint32_t ntiles,
+                                                            const RT* __restrict__ rin, const int* __restrict__ p2,
+                                                            const int* __restrict__ bpos, uint32_t sentinel,
+                                                            int* __restrict__ out1, int* __restrict__ out2,
+                                                            u64* status, uint32_t* ticket, uint32_t* err) {
+    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    __shared__ uint32_t loff[kRadix];
+    __shared__ u64 gofs[kRadix];
+    __shared__ RT stage[kSortTile];
+    __shared__ uint8_t sdig[kSortTile];
+    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ uint32_t s_tile;
+    __shared__ u64 s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    __syncthreads();
+    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    uint32_t el[kSortItems], dr[kSortItems];
+    int pv[kSortItems];  // the rows' probe positions, loaded with the keys (a load at each
+                         // store serialised 16 round trips a wave)
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        el[k] = __builtin_nontemporal_load(keys + (i < n ? i : n - 1));
+        pv[k] = out2 ? __builtin_nontemporal_load(p2 + (i < n ? i : n - 1)) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = win_id(el[k], t) & 0xFF;
+        const u64 peers = match_any8(d, __ballot(valid));
+        const uint32_t lt = lanes_below(peers);
+        const uint32_t cur = wcnt[wave][d];
+        __builtin_amdgcn_wave_barrier();
+        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) {
+        const uint32_t c = wcnt[w][tid];
+        wcnt[w][tid] = tot;
+        tot += c;
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t excl = incl - tot;
+    for (int w = 0; w < wave; w++) excl += wsum[w];
+    loff[tid] = excl;
+    __syncthreads();
+    uint32_t sp[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        sp[k] = 0;
+        if (dr[k] != 0xFFFFFFFFu) {
+            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
+            sp[k] = loff[d] + wcnt[wave][d] + r;
+            sdig[sp[k]] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    {
+        RT v[kSortItems];
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) {
+            const uint32_t e = (uint32_t)(k * kTPB + tid);
+            const uint32_t d = e < tn ? sdig[e] : 0u;
+            v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : (RT)0;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortItems; k++) stage[k * kTPB + tid] = v[k];
+    }
+    __syncthreads();
+    // each row's pair count (from its result, read from stage twice: once for the wave's
+    // total, once for the write, instead of holding results, counts and prefixes in
+    // registers: 229 VGPRs, 2 waves a SIMD). Counts are below 16, so a wave's prefix and
+    // total are 4 bit-ballots (1 for unique keys). Row order: wave, item, lane.
+    auto count_of = [&](RT v) -> uint32_t {
+        if constexpr (MODE == 0) {
+            return (uint32_t)v != sentinel ? 1u : 0u;
+        } else if constexpr (MODE == 1) {
+            return (uint32_t)((u64)v & 1ull);
+        } else {
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)((u64)v >> 32);
+            return lo != sentinel ? (hi == sentinel ? 1u : 2u) : (hi & 15u);
+        }
+    };
+    constexpr int kBits = MODE == 2 ? 4 : 1;
+    auto wave_prefix = [&](uint32_t c, uint32_t& tot) -> uint32_t {
+        uint32_t pre = 0;
+        tot = 0;
+#pragma unroll
+        for (int b = 0; b < kBits; b++) {
+            const u64 m = __ballot((c >> b) & 1u);
+            pre += lanes_below(m) << b;
+            tot += (uint32_t)__popcll(m) << b;
+        }
+        return pre;
+    };
+    uint32_t wrun = 0;
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const uint32_t c = i < n ? count_of(stage[sp[k]]) : 0u;
+        uint32_t tot;
+        (void)wave_prefix(c, tot);
+        wrun += tot;
+    }
+    __syncthreads();  // (wsum reused)
+    if (lane == 0) wsum[wave] = wrun;
+    __syncthreads();
+    uint32_t wbase = 0, ttot = 0;
+#pragma unroll
+    for (int w = 0; w < kTPB / 64; w++) {
+        wbase += w < wave ? wsum[w] : 0u;
+        ttot += wsum[w];
+    }
+    // decoupled look-back over the earlier tiles (wave 0)
+    if (wave == 0) {
+        if (lane == 0) lb_store(&status[tile], (tile ? kLbAgg : kLbPre) | (u64)ttot);
+        u64 acc = 0;
+        int64_t j = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        while (j >= 0) {
+            const int64_t idx = j - lane;
+            u64 x = idx >= 0 ? lb_load(&status[idx]) : kLbPre;
+            // every lane's status published (bounded: never expected to run long)
+            while (__ballot((x & ~kLbVal) == 0)) {
+                if (++spins > (1u << 24)) {
+                    if (lane == 0) atomicOr(err, 1u);
+                    x = kLbPre;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                if ((x & ~kLbVal) == 0) x = lb_load(&status[idx]);
+            }
+            const u64 pm = __ballot((x & kLbPre) != 0);
+            const int stop = pm ? __ffsll((long long)pm) - 1 : 64;  // the nearest inclusive prefix
+            u64 val = lane <= stop ? (x & kLbVal) : 0ull;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
+            acc += val;
+            if (pm) break;
+            j -= 64;
+        }
+        if (lane == 0) {
+            if (tile) lb_store(&status[tile], kLbPre | (acc + ttot));
+            s_excl = acc;
+        }
+    }
+    __syncthreads();
+    u64 o = s_excl + wbase;  // (wave-uniform) the first pair of this wave's next item
+#pragma unroll
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const RT v = i < n ? stage[sp[k]] : (RT)0;
+        const uint32_t c = i < n ? count_of(v) : 0u;
+        uint32_t tot;
+        const uint32_t pre = wave_prefix(c, tot);
+        if (c) {
+            const u64 q = o + pre;
+            const int pp = pv[k];
+            if constexpr (MODE == 0) {
+                out1[q] = (int)(uint32_t)v;
+                if (out2) out2[q] = pp;
+            } else if constexpr (MODE == 1) {
+                out1[q] = (int)(uint32_t)((u64)v >> 32);
+                if (out2) out2[q] = pp;
+            } else {
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)((u64)v >> 32);
+                if (lo != sentinel) {
+                    out1[q] = (int)lo;
+                    if (out2) out2[q] = pp;
+                    if (c == 2u) {
+                        out1[q + 1] = (int)hi;
+                        if (out2) out2[q + 1] = pp;
+                    }
+                } else {
+                    const uint32_t a = hi >> 4;
+                    for (uint32_t e = 0; e < c; e++) {
+                        out1[q + e] = bpos[a + e];
+                        if (out2) out2[q + e] = pp;
+                    }
+                }
+            }
+        }
+        o += tot;
     }
 }
 
@@ -2046,6 +2408,18 @@ struct mq_join {
     uint32_t* pflag;       // the window join's flag (a duplicate met, a window overfull)
     bool narrow;           // the window join's results as u32 payloads, `sentinel` = a miss
     bool run2;             // the last probe left short runs' positions in p01 (k_join_write_runs16)
+    // deferred (round 6): the partitioned probe stopped before its last inverse pass, which
+    // mq_join_write runs fused with the pair write (dmode: 0 unique u32 results, 1 unique
+    // u64, 2 run2 records); dkeys = the probe keys (the caller's, valid until the write),
+    // dhs0 = pass 0's tile offsets, dres = the results in pass-0 order (pool, owned)
+    bool deferred;
+    int dmode;
+    const uint32_t* dkeys;
+    u64* dhs0;
+    void* dres;
+    bool dupw;             // a partitioned build whose probe answers duplicate keys window by
+                           // window (k_win_join_runs: run2 records, long runs into bpos)
+    unsigned long long* mtot;  // the window joins' pair count (device)
     bool rsent_ok;         // windowed runs: `sentinel` is outside the payloads (the partitioned
                            // runs probe then carries short runs' positions, run2)
     uint32_t sentinel;     // (a value outside the build payloads' range)
@@ -2060,7 +2434,7 @@ namespace {
 
 int jown(mq_join* j, void* p) {
     if (j->nowned >= (int)(sizeof(j->owned) / sizeof(j->owned[0]))) {
-        pool_free(p);
+        pool_free_on(p, j->stream);  // (stream-ordered: queued work may still write it)
         return set_err(MQ_EINVAL, "join: handle owns too many allocations");
     }
     j->owned[j->nowned++] = p;
@@ -2205,6 +2579,9 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     u64* dst = a;
     for (int pass = 0; pass < passes; pass++) {
         const int shift = 8 * pass;
+        // (round 6 measured digit bytes for the next pass's histogram, as the index sort
+        // writes them: the byte stores cost the scatter 0.2-0.4 ms at 2^28 against the
+        // histogram's 0.32 ms saved; not kept)
         if (pass == 0) {
             hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1,
                                (const u64*)nullptr, n, t, shift, hist, (uint32_t)ntiles);
@@ -2229,7 +2606,10 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     hipLaunchKernelGGL(k_win_bounds<u64>, dim3(nw / kTPB + 1), dim3(kTPB), 0, st, src, n, t, nw, wstart);
     if (keep) {  // the partitioned build: the words and window bounds kept (checked by the probe)
         int rc = jown(j, src);
-        if (rc) return done(rc);  // (jown freed src)
+        if (rc) {  // (jown freed src, stream-ordered: not again here)
+            if (src == a) a = nullptr; else b = nullptr;
+            return done(rc);
+        }
         if ((rc = jown(j, wstart))) {
             if (src == a) a = nullptr; else b = nullptr;
             wstart = nullptr;
@@ -2529,8 +2909,12 @@ int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, i
 
 namespace {
 
+// defer (round 6): the last inverse pass is left to mq_join_write, fused with the pair
+// write (k_pwin_gather_write); the handle keeps what it reads: the probe keys (the
+// caller's d_c2), pass 0's tile offsets and the results in pass-0 order.
 template <typename RT, bool RUNS = false>
-int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
+int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st,
+                        bool defer = false) {
     const Win t = j->win;
     const int passes = j->passes;
     const uint64_t ntiles = ceil_div(n2, kSortTile), nh = ntiles * kRadix;
@@ -2570,15 +2954,28 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     DevState* s;
     if (int rc0 = ensure_ready(&s)) return done(rc0);
     const uint32_t gj = j->nwin < (uint32_t)s->cus * 2 ? j->nwin : (uint32_t)s->cus * 2;
-    if constexpr (RUNS)
+    if constexpr (RUNS && sizeof(RT) == 8)  // duplicate keys on the partitioned words (run2 records)
+        hipLaunchKernelGGL(k_win_join_runs, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws,
+                           j->nwin, t, reinterpret_cast<u64*>(R[0]), const_cast<int*>(j->bpos), j->pflag, j->mtot,
+                           j->sentinel);
+    else if constexpr (RUNS)  // a windowed runs table (k_win_build_runs), a slice per window in LDS
         hipLaunchKernelGGL(k_win_probe_tab<RT>, dim3(gj), dim3(kWinTPB), 0, st, (const u64*)j->words, K[passes], pws,
-                           j->nwin, t, R[0], j->bpos, j->sentinel);
+                           j->nwin, t, R[0]);
     else
         hipLaunchKernelGGL(k_win_join<RT>, dim3(gj), dim3(kWinTPB), 0, st, j->pwords, j->pwstart, K[passes], pws,
-                           j->nwin, t, R[0], j->pflag, j->sentinel);
+                           j->nwin, t, R[0], j->pflag, j->sentinel, j->mtot);
     if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: window join"));
     int cur = 0;
     for (int p = passes - 1; p >= 0; p--) {
+        if (p == 0 && defer) {
+            j->dkeys = K[0];
+            j->dhs0 = hs[0];
+            j->dres = R[cur];
+            hs[0] = nullptr;
+            R[cur] = nullptr;
+            j->deferred = true;
+            break;
+        }
         if (p == 0)
             hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t,
                                0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)(RUNS ? (void*)j->p01 : nullptr),
@@ -2593,16 +2990,6 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     return done(MQ_OK);
 }
 
-// The partitioned unique probe (k_pwin_scatter / k_win_join / k_pwin_gather above):
-// per probe row its payload (pstart) and per 64 rows the hit word, as k_ht_probe_unique
-// leaves them. Results move as u32 payloads with a sentinel outside the build payloads'
-// range for a miss, or (every int32 is a payload) as u64 {payload, hit}. Temporaries are
-// freed stream-ordered.
-int probe_partitioned(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st) {
-    return j->narrow ? probe_partitioned_t<uint32_t>(j, d_c2, n2, pstart, hits, st)
-                     : probe_partitioned_t<u64>(j, d_c2, n2, pstart, hits, st);
-}
-
 // The same over a windowed runs table (j->words, built by k_win_build_runs): per row the
 // packed run (pstart) and per 64 rows the run lengths' sum (wcnt).
 int probe_partitioned_runs(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, uint32_t* wcnt,
@@ -2611,9 +2998,51 @@ int probe_partitioned_runs(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_
     while ((1ull << lg) < j->mask + 1) lg++;
     j->nwin = (uint32_t)((j->mask + 1) >> j->win.wlog);
     j->passes = (lg - j->win.wlog + 7) / 8;
-    if (j->p01)  // run2: the short runs' positions ride along (j->p01, n2 u64)
+    if (j->dupw)  // run2 records from the partitioned build words (j->p01: n2 u64)
         return probe_partitioned_t<u64, true>(j, d_c2, n2, pstart, reinterpret_cast<u64*>(wcnt), st);
     return probe_partitioned_t<uint32_t, true>(j, d_c2, n2, pstart, reinterpret_cast<u64*>(wcnt), st);
+}
+
+// A deferred probe's last inverse pass in the classic form (per-row results, hit words or
+// per-word run lengths, their scan): for mq_join_counts, whose caller (the key-partitioned
+// shard join) needs every row's pair count; mq_join_write then takes the classic kernels.
+int finish_classic(mq_join* j, hipStream_t st) {
+    DevState* s;
+    if (int rc = ensure_ready(&s)) return rc;
+    const uint64_t n2 = j->n2, nw = (n2 + 63) / 64, ntiles = ceil_div(n2, kSortTile);
+    const bool runs = j->dmode == 2;
+    j->pstart = (uint32_t*)pool_alloc(n2 * 4);
+    j->plen = (uint32_t*)pool_alloc(runs ? nw * 4 : nw * 12);
+    j->offs = (u64*)pool_alloc(nw * 8);
+    j->scan_scratch = (u64*)pool_alloc(scan_scratch_elems(nw) * 8);
+    if (runs) j->p01 = (u64*)pool_alloc(n2 * 8);
+    if (!j->pstart || !j->plen || !j->offs || !j->scan_scratch || (runs && !j->p01))
+        return set_err(MQ_ENOMEM, "mq_join_counts: buffers for %llu rows", (unsigned long long)n2);
+    uint32_t* const cnt = runs ? j->plen : j->plen + 2 * nw;
+    u64* const hits = reinterpret_cast<u64*>(j->plen);
+    const dim3 g((uint32_t)ntiles), b(kTPB);
+    if (runs)
+        hipLaunchKernelGGL((k_pwin_gather<true, u64, true>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
+                           (uint32_t)ntiles, (const u64*)j->dres, j->p01, j->pstart, hits, j->sentinel);
+    else if (j->dmode == 1)
+        hipLaunchKernelGGL((k_pwin_gather<true, u64>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0, (uint32_t)ntiles,
+                           (const u64*)j->dres, (u64*)nullptr, j->pstart, hits, j->sentinel);
+    else
+        hipLaunchKernelGGL((k_pwin_gather<true, uint32_t>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
+                           (uint32_t)ntiles, (const uint32_t*)j->dres, (uint32_t*)nullptr, j->pstart, hits,
+                           j->sentinel);
+    LAUNCHCHK("k_pwin_gather");
+    if (!runs) {
+        hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
+        LAUNCHCHK("k_hits_count");
+    }
+    if (int rc = scan_exclusive<uint32_t>(cnt, j->offs, nw, j->scan_scratch, st)) return rc;
+    pool_free_on(j->dhs0, st);
+    pool_free_on(j->dres, st);
+    j->dhs0 = nullptr;
+    j->dres = nullptr;
+    j->deferred = false;
+    return MQ_OK;
 }
 
 // The global table of a partitioned build, for a probe too small to pay for its own
@@ -2640,6 +3069,29 @@ int materialize_table(mq_join* j, hipStream_t st, bool* flagged) {
     return MQ_OK;
 }
 
+// The duplicate-key window join on the partitioned words (k_win_join_runs) unless a
+// test forces one of the runs tables (MQ_JOIN_WINRUNS=0, MQ_JOIN_RUNS=0, MQ_JOIN_RUN2=0)
+bool dupw_allowed() {
+    const char* a = getenv("MQ_JOIN_WINRUNS");
+    const char* b = getenv("MQ_JOIN_RUNS");
+    const char* c = getenv("MQ_JOIN_RUN2");
+    return !(a && a[0] == '0') && !(b && b[0] == '0') && !(c && c[0] == '0');
+}
+
+// A partitioned build (pwords, pwstart kept) turned into the duplicate-key form: packed
+// run2 records, long runs' positions into bpos (n1 ints, written by the probe's windows).
+int make_dupw(mq_join* j) {
+    int* bp = nullptr;
+    if (int rc = jalloc(j, (void**)&bp, (j->n1 ? j->n1 : 1) * 4)) return rc;
+    j->bpos = bp;
+    j->dupw = true;
+    j->unique = 2;
+    j->packed = true;
+    j->rs = nullptr;
+    j->marks = true;
+    return MQ_OK;
+}
+
 // The build proper into a fresh handle (device and stream set). allow_part: a unique
 // build of part_min_rows() rows and more keeps its window partition for the
 // partitioned probe instead of building the table (a duplicate key or an overfull
@@ -2661,9 +3113,10 @@ int build_into(mq_join* j, const int32_t* d_c1, const int32_t* d_p1, uint64_t n1
     // the partitioned build keeps no global table: allocated only if a path needs it
     const bool part = allow_part && n1 >= kWindowBuildRows && n1 >= part_min_rows() && j->win.wlog == kWinLog;
     uint32_t* dflag = nullptr;
-    if ((!part && (rc = jalloc(j, (void**)&j->words, slots * 8))) || (rc = jalloc(j, (void**)&dflag, 16 + 512)))
+    if ((!part && (rc = jalloc(j, (void**)&j->words, slots * 8))) || (rc = jalloc(j, (void**)&dflag, 16 + 512 + 16)))
         return rc;
     j->pflag = dflag + 2;  // (dflag[1] is the sampled duplicate check's)
+    j->mtot = reinterpret_cast<unsigned long long*>(dflag + 132);  // (after the 128 range slots)
     j->bpos = nullptr;  // unique table carries the build positions itself
     j->unique = 1;
     if (n1) {
@@ -2676,23 +3129,37 @@ int build_into(mq_join* j, const int32_t* d_c1, const int32_t* d_p1, uint64_t n1
         bool sampled = false;
         if ((rc = sample_has_dups(d_c1, n1, dflag, st, s, &sampled))) return rc;
         uint32_t dup = sampled ? 1u : 0u;
-        if (!sampled) {
-            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, part, pmm))) return rc;
-            if (part) {  // the probe checks the windows; the payloads' range picks the result width
-                int sl[128];
-                HIPCHK(hipMemcpyAsync(sl, pmm, sizeof sl, hipMemcpyDeviceToHost, st));
-                HIPCHK(hipStreamSynchronize(st));
-                int mm[2] = {INT32_MAX, INT32_MIN};
-                for (int q = 0; q < 64; q++) {
-                    mm[0] = sl[q] < mm[0] ? sl[q] : mm[0];
-                    mm[1] = sl[64 + q] > mm[1] ? sl[64 + q] : mm[1];
-                }
-                const char* nw = getenv("MQ_JOIN_NARROW");
-                j->narrow = !(nw && nw[0] == '0') && (mm[1] < INT32_MAX || mm[0] > INT32_MIN);
-                j->sentinel = (uint32_t)(mm[1] < INT32_MAX ? INT32_MAX : INT32_MIN);
-                j->part = true;
-                return MQ_OK;
+        // the partition alone when the probe will join window by window: unique keys, or
+        // (round 6) sampled duplicates answered by k_win_join_runs
+        const bool keep = part && (!sampled || dupw_allowed());
+        if (keep) {
+            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, true, pmm))) return rc;
+            // the payloads' range: a value outside it marks a miss (u32 results; the run2
+            // records of duplicate keys need one)
+            int sl[128];
+            HIPCHK(hipMemcpyAsync(sl, pmm, sizeof sl, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            int mm[2] = {INT32_MAX, INT32_MIN};
+            for (int q = 0; q < 64; q++) {
+                mm[0] = sl[q] < mm[0] ? sl[q] : mm[0];
+                mm[1] = sl[64 + q] > mm[1] ? sl[64 + q] : mm[1];
             }
+            const char* nw = getenv("MQ_JOIN_NARROW");
+            j->rsent_ok = mm[1] < INT32_MAX || mm[0] > INT32_MIN;
+            j->narrow = !(nw && nw[0] == '0') && j->rsent_ok;
+            j->sentinel = (uint32_t)(mm[1] < INT32_MAX ? INT32_MAX : INT32_MIN);
+            j->part = true;
+            if (!sampled) return MQ_OK;
+            if (j->rsent_ok) return make_dupw(j);
+            // duplicates but no free payload value: the runs tables below, from the inputs
+            jdrop(j, j->pwords);
+            jdrop(j, j->pwstart);
+            j->pwords = nullptr;
+            j->pwstart = nullptr;
+            j->part = false;
+        }
+        if (!sampled) {
+            if ((rc = insert_unique(j, d_c1, d_p1, n1, slots, dflag, st, s, false, pmm))) return rc;
             HIPCHK(hipMemcpyAsync(&dup, dflag, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
         }
@@ -2749,6 +3216,8 @@ int rebuild_unpartitioned(mq_join* j, hipStream_t st) {
     j->plen = keep.plen;
     j->offs = keep.offs;
     j->scan_scratch = keep.scan_scratch;
+    j->dhs0 = keep.dhs0;  // (freed by the probe that follows)
+    j->dres = keep.dres;
     j->longq = keep.longq;
     return build_into(j, c1, p1, n1, st, s, false);
 }
@@ -2793,8 +3262,14 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     pool_free_on(j->plen, st);
     pool_free_on(j->offs, st);
     pool_free_on(j->scan_scratch, st);
+    pool_free_on(j->dhs0, st);
+    pool_free_on(j->dres, st);
     j->pstart = j->plen = nullptr;
     j->offs = j->scan_scratch = nullptr;
+    j->dhs0 = nullptr;
+    j->dres = nullptr;
+    j->dkeys = nullptr;
+    j->deferred = false;
     j->n2 = n2;
     j->m = 0;
     *h_m = 0;
@@ -2802,6 +3277,10 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     // a partitioned build and a probe side too small to pay for its own partition (its
     // passes and the window join read all n1 build words): the global table, once
     const uint64_t pdiv = getenv("MQ_JOIN_PART_DIV") ? strtoull(getenv("MQ_JOIN_PART_DIV"), nullptr, 10) : 16;
+    if (j->dupw && n2 < j->n1 / (pdiv ? pdiv : 1)) {  // duplicate keys, a small probe: a runs table
+        if ((rc = rebuild_unpartitioned(j, st))) return rc;
+        return mq_join_probe(j, d_c2, n2, h_m, stream);
+    }
     if (j->part && n2 < j->n1 / (pdiv ? pdiv : 1)) {
         bool flagged = false;
         if ((rc = materialize_table(j, st, &flagged))) return rc;
@@ -2809,6 +3288,44 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
             if ((rc = rebuild_unpartitioned(j, st))) return rc;
             return mq_join_probe(j, d_c2, n2, h_m, stream);
         }
+    }
+    // the partitioned probes of a unique build and of duplicate keys on the partitioned
+    // words: up to the window join and all but the last inverse pass; M from the window
+    // joins' pair count, the rest in mq_join_write (k_pwin_gather_write)
+    if (j->dupw || (j->unique == 1 && j->part)) {
+        j->pruns = j->run2 = j->dupw;
+        HIPCHK(hipMemsetAsync(j->pflag, 0, 4, st));
+        HIPCHK(hipMemsetAsync(j->mtot, 0, 8, st));
+        if (j->dupw) {
+            j->dmode = 2;
+            rc = probe_partitioned_t<u64, true>(j, d_c2, n2, nullptr, nullptr, st, true);
+        } else if (j->narrow) {
+            j->dmode = 0;
+            rc = probe_partitioned_t<uint32_t>(j, d_c2, n2, nullptr, nullptr, st, true);
+        } else {
+            j->dmode = 1;
+            rc = probe_partitioned_t<u64>(j, d_c2, n2, nullptr, nullptr, st, true);
+        }
+        if (rc) return rc;
+        uint32_t pf = 0;
+        unsigned long long mm = 0;
+        HIPCHK(hipMemcpyAsync(&pf, j->pflag, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&mm, j->mtot, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (pf) {
+            // a probe key met a duplicate build key: the same partitioned words answer
+            // duplicate keys (k_win_join_runs) when a payload value is free; otherwise, an
+            // overfull window or a key on 15+ rows: rebuild from the inputs on the runs tables
+            if (pf == 1u && !j->dupw && j->rsent_ok && dupw_allowed()) {
+                if ((rc = make_dupw(j))) return rc;
+            } else if ((rc = rebuild_unpartitioned(j, st))) {
+                return rc;
+            }
+            return mq_join_probe(j, d_c2, n2, h_m, stream);
+        }
+        j->m = mm;
+        *h_m = mm;
+        return MQ_OK;
     }
     const uint64_t nwords = (n2 + 63) / 64;
     // packed runs: per-word lengths. Only for the windowed runs build (rs == nullptr:
@@ -2832,10 +3349,8 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     const uint64_t nscan = words_scan ? nw : n2;
     uint32_t* const cnt = j->unique == 1 ? j->plen + 2 * nw : j->plen;
     if (pruns && j->win.wlog == kWinLog && j->n1 >= part_min_rows() && n2 >= j->n1 / (pdiv ? pdiv : 1)) {
-        // packed runs, partitioned: the probe keys by window, each window's table slice in LDS;
-        // with a marker outside the payloads the short runs' positions ride along (run2)
-        j->run2 = j->rsent_ok && !(getenv("MQ_JOIN_RUN2") && getenv("MQ_JOIN_RUN2")[0] == '0');
-        if (j->run2 && !(j->p01 = (u64*)pool_alloc(n2 * 8))) return set_err(MQ_ENOMEM, "mq_join_probe: positions");
+        // packed runs, partitioned: the probe keys by window, each window's slice of the runs
+        // table in LDS (no free payload value for run2 records, or forced by a test)
         if ((rc = probe_partitioned_runs(j, d_c2, n2, j->pstart, cnt, st))) return rc;
     } else if (pruns) {  // packed runs: each row's payload, then the per-word run lengths
         auto kern = k_ht_probe_unique<true>;
@@ -2848,12 +3363,6 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
                            j->words, j->win, j->pstart, (u64*)nullptr, j->rs, cnt, j->packed, j->marks,
                            (uint32_t*)nullptr);
         LAUNCHCHK("k_ht_probe_unique");
-    } else if (j->unique && j->part) {
-        u64* const hits = reinterpret_cast<u64*>(j->plen);
-        HIPCHK(hipMemsetAsync(j->pflag, 0, 4, st));
-        if ((rc = probe_partitioned(j, d_c2, n2, j->pstart, hits, st))) return rc;
-        hipLaunchKernelGGL(k_hits_count, dim3(stream_grid(s, nw)), dim3(kTPB), 0, st, hits, nw, cnt);
-        LAUNCHCHK("k_hits_count");
     } else if (j->unique) {
         u64* const hits = reinterpret_cast<u64*>(j->plen);
         auto kern = k_ht_probe_unique<false>;
@@ -2873,13 +3382,7 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     uint32_t last_len = 0;
     HIPCHK(hipMemcpyAsync(&last_off, j->offs + (nscan - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&last_len, cnt + (nscan - 1), 4, hipMemcpyDeviceToHost, st));
-    uint32_t pf = 0;
-    if (j->part) HIPCHK(hipMemcpyAsync(&pf, j->pflag, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (pf) {  // a probe key met a duplicate build key (or a window overflowed): rebuild
-        if ((rc = rebuild_unpartitioned(j, st))) return rc;
-        return mq_join_probe(j, d_c2, n2, h_m, stream);
-    }
     j->m = last_off + last_len;
     *h_m = j->m;
     return MQ_OK;
@@ -2893,6 +3396,32 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if (j->m == 0) return MQ_OK;
     if (!d_out1 || (d_out2 && !d_p2)) return set_err(MQ_EINVAL, "mq_join_write: NULL pointer");
     if ((rc = juse(j, (hipStream_t)stream))) return rc;
+    if (j->deferred) {  // the last inverse pass fused with the pair write (look-back over tiles)
+        hipStream_t st = (hipStream_t)stream;
+        const uint64_t ntiles = ceil_div(j->n2, kSortTile);
+        u64* stat = (u64*)pool_alloc(ntiles * 8 + 16);
+        if (!stat) return set_err(MQ_ENOMEM, "mq_join_write: tile status");
+        HIPCHK(hipMemsetAsync(stat, 0, ntiles * 8 + 16, st));
+        HIPCHK(hipMemsetAsync(j->pflag + 1, 0, 4, st));
+        uint32_t* ticket = reinterpret_cast<uint32_t*>(stat + ntiles);
+        const dim3 g((uint32_t)ntiles), b(kTPB);
+        if (j->dmode == 2)
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 2>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+                               (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
+                               ticket, j->pflag + 1);
+        else if (j->dmode == 1)
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 1>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+                               (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
+                               ticket, j->pflag + 1);
+        else
+            hipLaunchKernelGGL((k_pwin_gather_write<uint32_t, 0>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+                               (uint32_t)ntiles, (const uint32_t*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2,
+                               stat, ticket, j->pflag + 1);
+        const hipError_t e = hipGetLastError();
+        pool_free_on(stat, st);
+        if (e != hipSuccess) return set_err(MQ_EHIP, "launch of k_pwin_gather_write failed: %s", hipGetErrorString(e));
+        return MQ_OK;
+    }
     if (j->unique == 1) {
         const bool v4 = ((reinterpret_cast<uintptr_t>(j->pstart) | reinterpret_cast<uintptr_t>(d_p2)) & 15u) == 0;
         if (v4)
@@ -2946,6 +3475,7 @@ int mq_join_counts(mq_join* j, uint32_t* d_cnt, void* stream) {
         HIPCHK(hipMemsetAsync(d_cnt, 0, j->n2 * 4, st));
         return MQ_OK;
     }
+    if (j->deferred && (rc = finish_classic(j, st))) return rc;
     const u64* hits = j->unique == 1 ? reinterpret_cast<const u64*>(j->plen) : nullptr;
     const uint32_t* pk = (!hits && j->pruns) ? j->pstart : nullptr;
     const uint32_t* plen = (!hits && !j->pruns) ? j->plen : nullptr;
@@ -2977,6 +3507,8 @@ int mq_join_free(mq_join* j) {
     pool_free_on(j->offs, j->stream);
     pool_free_on(j->scan_scratch, j->stream);
     pool_free_on(j->longq, j->stream);
+    pool_free_on(j->dhs0, j->stream);
+    pool_free_on(j->dres, j->stream);
     jfree_all(j);
     delete j;
     return MQ_OK;
@@ -2997,8 +3529,14 @@ int mq_hash_join(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, const in
         mq_join_free(j);
         return *h_m == 0 ? MQ_OK : MQ_ECAP;
     }
+    const bool fused = j->deferred;
     rc = mq_join_write(j, d_p2, d_out1, d_out2, stream);
     if (!rc) rc = mq_stream_sync(stream);
+    if (!rc && fused) {  // the fused write's look-back gave up (never expected): fail loudly
+        uint32_t e = 0;
+        if (hipMemcpy(&e, j->pflag + 1, 4, hipMemcpyDeviceToHost) != hipSuccess || e)
+            rc = set_err(MQ_EHIP, "mq_hash_join: the fused write's look-back failed");
+    }
     mq_join_free(j);
     return rc;
 }

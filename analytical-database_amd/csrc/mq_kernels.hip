@@ -1127,15 +1127,6 @@ void* pool_alloc(size_t bytes) {
             PoolBlock*& slot = pool_in_flight(b) ? wait : best;
             if (!slot || b.bytes < slot->bytes) slot = &b;
         }
-    if (!best && wait) {  // the only fit is still used by queued work: wait for it outside the lock
-        wait->busy = true;
-        void* p = wait->p;
-        hipEvent_t ev = wait->ev;
-        wait->pending = false;
-        lk.unlock();
-        (void)hipEventSynchronize(ev);
-        return p;
-    }
     if (best) {
         best->busy = true;
         return best->p;
@@ -1143,6 +1134,17 @@ void* pool_alloc(size_t bytes) {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
         (void)hipGetLastError();
+        if (wait) {  // the only fit is still used by queued work, and no fresh block fits
+                     // in HBM: wait for that one (outside the lock). (a fresh
+                     // block first, so callers on other streams never wait on each other.)
+            wait->busy = true;
+            void* q = wait->p;
+            hipEvent_t ev = wait->ev;
+            wait->pending = false;
+            lk.unlock();
+            (void)hipEventSynchronize(ev);
+            return q;
+        }
         pool_release_idle_locked();  // give the cache back and retry once
         if (hipMalloc(&p, bytes) != hipSuccess) {
             (void)hipGetLastError();

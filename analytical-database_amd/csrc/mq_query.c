@@ -608,13 +608,8 @@ static int pipe_segments(size_t n) {
  * shrunk to K rows by realloc afterwards (glibc remaps an mmapped chunk in place, so it
  * stays guardable). The HBM shadow is the segments' pieces copied together on the device. */
 static Result* scan_positions_piped(const int32_t* dcol, size_t n, int segs, int* low_pointer, int* high_pointer,
-                                    Status* st) {
+                                    int32_t* host, Status* st) {
     double t0 = now_s();
-    int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
-    if (!host) {
-        fail(st, "payload allocation", MQ_ENOMEM);
-        return NULL;
-    }
     uint64_t seg[65], rows[65];
     int rc = mq_stream_sync(g_stream);
     const double tx = now_s();
@@ -666,7 +661,12 @@ static Result* scan_positions(Column* column, int* low_pointer, int* high_pointe
     const int32_t* dcol;
     if (column_device(column, &dcol, ret_status) || ensure_ws(n, ret_status)) return NULL;
     const int segs = pipe_segments(n);
-    if (segs) return scan_positions_piped(dcol, n, segs, low_pointer, high_pointer, ret_status);
+    if (segs) {
+        /* the n-row payload is address space only; where even that is refused (RLIMIT_AS,
+         * strict overcommit) the one-kernel path below needs just K rows */
+        int32_t* host = (int32_t*)payload_alloc(n * sizeof(int32_t));
+        if (host) return scan_positions_piped(dcol, n, segs, low_pointer, high_pointer, host, ret_status);
+    }
     const double t0 = now_s();
     int rc = mq_select_positions(dcol, NULL, n, low_pointer != NULL, low_pointer ? *low_pointer : 0,
                                  high_pointer != NULL, high_pointer ? *high_pointer : 0,

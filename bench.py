@@ -480,6 +480,7 @@ def main() -> None:
     if rank == 0:
         ms_step = 1e3 * elapsed / args.steps
         gbs = 4.0 * n / (k_mean_ms * 1e-3) / 1e9
+        traffic = traffic_per_launch(n)
         out = {
             "metric": "rows/sec scanned + HBM GB/s (% of roofline), 1B-row int32 select+sum",
             "value": world * n * args.steps / elapsed,
@@ -502,7 +503,7 @@ def main() -> None:
             "hbm_gbs_step": 4.0 * n * world / (elapsed / args.steps) / 1e9 / world,
             "roofline": {"bound": "hbm", "kernel": "k_scan<kSum,true> (mq_select_sum: count+sum, partials folded in-kernel)",
                          "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(n),
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": traffic[0], "traffic_source": traffic[1],
                          "kernel_ms_mean": k_mean_ms, "kernel_ms_min": min(kernel_ms),
                          "kernel_ms_median": statistics.median(kernel_ms),
                          "stream_read_probe": achievable,
@@ -670,20 +671,26 @@ def print_leg(lib, mq, torch, dev, stream, pos, k, cpu: bool = True) -> dict:
 
 
 def traffic_per_launch(n: int):
-    """HBM bytes per k_scan launch from the committed rocprofv3 PMC summary (if one
-    exists for this N): FETCH_SIZE x 2 (gfx950 halving, MI355X_MICROARCH.md §HBM) +
-    WRITE_SIZE, collected in separate --pmc passes by tools/pmc_traffic.py."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
-        row = d.get("k_scan", {})
-        if int(row.get("rows", -1)) == n:
-            return row.get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-    return None
+    """(HBM bytes per k_scan launch, source) from the newest round's committed rocprofv3
+    PMC summary with a k_scan row for this N (profiles/rNN_pmc_traffic.json, written by
+    tools/pmc_traffic.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes: FETCH_SIZE
+    x 2 for gfx950's halving, MI355X_MICROARCH.md §HBM, + WRITE_SIZE). (None, None) when
+    no round has one."""
+    import glob
+    import re
+    found = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic*.json")):
+        mr = re.match(r"r(\d\d)_", os.path.basename(path))
+        try:
+            row = json.load(open(path)).get("k_scan", {})
+        except Exception:
+            continue
+        if mr and int(row.get("rows", -1)) == n and row.get("hbm_bytes_per_launch"):
+            found.append((int(mr.group(1)), os.path.getmtime(path), path, row["hbm_bytes_per_launch"]))
+    if not found:
+        return None, None
+    rnd, _, path, b = max(found)
+    return b, {"file": os.path.relpath(path, ROOT), "round": rnd}
 
 
 def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, cpu=True) -> dict:
@@ -781,6 +788,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
         out["positions_sweep"] = positions_sweep(lib, mq, torch, dev, stream, col, col1, ws, ws_bytes, n, pos, cnt,
                                                  gold)
         del pos, col1, vals
+    out["config1_10m"] = config1_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
     out["shared_select"] = shared_leg(lib, mq, torch, dev, stream, col, n)
     out["config5_hash_join"] = join_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
     out["config5_many_to_many"] = join_dup_leg(lib, mq, torch, dev, stream, gold, cpu=cpu)
@@ -789,6 +797,53 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
     out["pcie_probe"] = pcie_probe(torch, dev, stream)
     out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
     return out
+
+
+def config1_leg(lib, mq, torch, dev, stream, gold, cpu: bool = True) -> dict:
+    """Config 1: the 10M-row column, select 1 % -> fetch -> sum. The
+    reference's own query.c chain (oracle/_ref/libref.so at -O2 and libref_O0.so, the
+    -O0 its Makefile builds, src/Makefile:12), median of 3 on 1 core, and the GPU step
+    (mq_select_sum, HBM-resident) on the same column; K and the sum against the 10M
+    golden (tests/golden/goldens.json, made by the reference)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refcpu  # baseline / checker only
+    n = 10_000_000
+    lo, hi = int(0.25 * n), int(0.25 * n) + int(0.01 * n)
+    want = [r for r in gold["select"] if r["n"] == n and abs(r["sel"] - 0.01) < 1e-12][0]
+    sp = mq.stream_of(stream)
+    res = {"n": n, "low": lo, "high": hi}
+    with torch.cuda.stream(stream):
+        col = torch.empty(n, dtype=torch.int32, device=dev)
+        mq.check(lib.mq_gen_uniform(col.data_ptr(), n, 42, n, sp), "gen")
+        ws_bytes = lib.mq_scan_workspace_bytes(n)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        agg = torch.zeros(4, dtype=torch.int64, device=dev)
+        ms = _events_ms(torch, stream, lambda: mq.check(lib.mq_select_sum(
+            col.data_ptr(), n, 1, lo, 1, hi, agg.data_ptr(), ws.data_ptr(), ws_bytes, sp), "select_sum"), 20)
+        a = agg.cpu()
+        res["gpu"] = {"ms": ms, "rows_per_s": n / (ms * 1e-3), "gbs": 4 * n / (ms * 1e-3) / 1e9,
+                      "parity": (int(a[0]), int(a[1])) == (want["k"], want["sum"]),
+                      "note": "one mq_select_sum launch (k_scan<kSum>); 40 MB is below the 256 MB "
+                              "Infinity Cache, so this is a launch-latency-scale step"}
+        del col, ws
+    if cpu and refcpu.have_reference():
+        from refapi import Api, make_column
+        d = refcpu.gen_uniform(n, 42, nthreads=16)
+        c = make_column(d)
+        for name, path in (("reference_O2", refcpu.REFLIB), ("reference_O0", refcpu.REFLIB_O0)):
+            api = Api(refcpu.reference(path))
+            times, s = [], None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                pos = api.select_column(c, lo, hi)
+                s = api.sum_result(api.fetch_column(c, pos))
+                times.append(time.perf_counter() - t0)
+            t = statistics.median(times)
+            res[name] = {"ms": 1e3 * t, "rows_per_s": n / t, "cores": 1, "kind": "reference",
+                         "parity": (len(pos), s) == (want["k"], want["sum"]),
+                         "what": f"select_column -> fetch_column -> sum, {os.path.basename(path)}, median of 3"}
+    return res
 
 
 def positions_sweep(lib, mq, torch, dev, stream, col, col1, ws, ws_bytes, n, pos, cnt, gold) -> dict:
@@ -1047,7 +1102,35 @@ def join_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True
         tr = time.perf_counter() - t0
         res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1,
                                      "kind": "reference"}
+    if cpu:
+        res["cpu_host_cores_2e24"] = host_cores_join(refcpu, gold, "build", "probe", gold["join_survey"])
     return res
+
+
+def host_cores_join(refcpu, gold, kb: str, kp: str, rows: list, logn: int = 24) -> dict:
+    """Config 5's host-cores baseline: the restatement's hash join
+    over every core this process may use (rc_hash_join_mt: partitioned build, range-split
+    probe; output identical to the reference's), median of 3 at 2^logn x 2^logn, with M
+    and the pair FNV checked against the reference's golden."""
+    import numpy as np
+    n = 1 << logn
+    cores, why = host_cores()
+    a, b, p = refcpu.gen_join(n, kb), refcpu.gen_join(n, kp), refcpu.gen_join(n, "iota")
+    want = [r for r in rows if r["n"] == n]
+    m = want[0]["m"] if want else n * 2
+    o1, o2 = np.empty(m, dtype=np.int32), np.empty(m, dtype=np.int32)
+    L = refcpu.lib()
+    times, got = [], 0
+    for _ in range(3):
+        t0 = time.perf_counter()
+        got = L.rc_hash_join_mt(refcpu._a(a), refcpu._a(p), n, refcpu._a(b), refcpu._a(p), n, refcpu._a(o1),
+                                refcpu._a(o2), m, cores)
+        times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    ok = bool(want) and got == m and f"{refcpu.fnv1a64_pairs(o1, o2):016x}" == want[0]["pairs_fnv1a64"]
+    return {"n_build": n, "n_probe": n, "m": int(got), "s": t, "rows_per_s": 2 * n / t, "cores": cores,
+            "cores_from": why, "kind": "port", "parity": ok,
+            "what": "oracle/refcpu.c rc_hash_join_mt (keys " + kb + " x " + kp + "), median of 3"}
 
 
 def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = True) -> dict:
@@ -1055,7 +1138,7 @@ def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = 
     i + n/2), about half the probes hit, two matches each (M ~ n): the duplicate-key
     build path (stable radix sort into key runs). Parity: M and the pair FNV at 2^22
     against the reference's own hash_join (tests/golden/make_join_dup_goldens.py);
-    timing at 2^logn (build + probe + write, as join_leg)."""
+    timing at 2^logn (build + probe + write, as join_leg). Parity at 2^24 (round 6)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import refcpu  # checker only (pair hash)
     sp = mq.stream_of(stream)
@@ -1090,15 +1173,16 @@ def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = 
             del a, b, p, o1, o2
             return out
 
-    want = [r for r in gold.get("join_dup", []) if r["n"] == 1 << 22]
-    pm, _, pf = run(1 << 22, True)
+    want = [r for r in gold.get("join_dup", []) if r["n"] == 1 << 24]
+    pm, _, pf = run(1 << 24, True)
     ok = bool(want) and (pm, f"{pf:016x}") == (want[0]["m"], want[0]["pairs_fnv1a64"])
     n = 1 << logn
     m, t = run(n, False)
     res = {"n_build": n, "n_probe": n, "m": m, "ms": 1e3 * t, "rows_per_s": 2 * n / t,
            "algorithmic_bytes": 16 * n + 8 * m, "gbs_algorithmic": (16 * n + 8 * m) / t / 1e9,
-           "parity_2e22": ok, "note": "wall time incl. the duplicate-key sample, the per-window runs "
-                                      "build (k_win_build_runs) and 2 host syncs"}
+           "parity_2e24": ok, "note": "wall time incl. the duplicate-key sample, the partition of the "
+                                      "build rows and 2 host syncs; the window join answers duplicate "
+                                      "keys (k_win_join_runs, DESIGN §3.3 round 6)"}
     if cpu and refcpu.have_reference():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from refapi import Api
@@ -1109,6 +1193,8 @@ def join_dup_leg(lib, mq, torch, dev, stream, gold, logn: int = 28, cpu: bool = 
         api.join(ka, kp, kb, kp, "hash")
         tr = time.perf_counter() - t0
         res["cpu_reference_2e20"] = {"s": tr, "rows_per_s": 2 * k / tr, "cores": 1, "kind": "reference"}
+    if cpu:
+        res["cpu_host_cores_2e24"] = host_cores_join(refcpu, gold, "build_dup", "probe_dup", gold.get("join_dup", []))
     return res
 
 

@@ -495,6 +495,203 @@ size_t rc_hash_join(const int32_t* c1, const int32_t* p1, size_t n1,
     return overflow ? (size_t)-1 : m;
 }
 
+/* The same join over `nthreads` host threads (the config-5 host-cores baseline, SURVEY
+ * §8(d) "CPU threadpool"; the reference's hash_join is single-threaded). Output
+ * identical to rc_hash_join: probe-major, a key's build rows in insertion order.
+ *   build: the build rows split by key hash into P partitions (a per-thread histogram
+ *   over contiguous row ranges, a prefix in (partition, thread) order, a scatter: every
+ *   partition holds its rows in input order); each partition then gets its own
+ *   open-addressing CSR multimap (as rc_hash_join's), partitions spread over threads;
+ *   probe: contiguous probe ranges per thread, a count pass, a prefix, a write pass. */
+#define MJ_P 256
+typedef struct {
+    const int32_t *c1, *p1, *c2, *p2;
+    size_t n1, n2;
+    int T;
+    size_t (*hist)[MJ_P];     /* [T][P] build rows of thread t's range in partition p */
+    int32_t *pk, *pp;          /* build rows partitioned (key, payload) */
+    size_t poff[MJ_P + 1];     /* partition starts in pk / pp */
+    uint32_t tmask[MJ_P];      /* partition tables: 2^k slots, mask */
+    int32_t* tkey[MJ_P];
+    uint32_t* tcnt[MJ_P];
+    uint32_t* toff[MJ_P];
+    int32_t* tval[MJ_P];
+    size_t* pcount;            /* per thread: pairs of its probe range */
+    int32_t *out1, *out2;
+} mj_ctx;
+typedef struct {
+    mj_ctx* c;
+    int t, phase;
+} mj_arg;
+
+static inline uint32_t mj_hash(int32_t k) { return rc_mix31((uint32_t)k) ^ ((uint32_t)k * 0x9E3779B1u); }
+
+static void mj_range(size_t n, int T, int t, size_t* lo, size_t* hi) {
+    size_t ch = (n + (size_t)T - 1) / (size_t)T;
+    *lo = (size_t)t * ch;
+    *hi = *lo + ch;
+    if (*lo > n) *lo = n;
+    if (*hi > n) *hi = n;
+}
+
+static void mj_build_part(mj_ctx* c, int p) {
+    size_t a = c->poff[p], b = c->poff[p + 1], n = b - a;
+    uint32_t slots = 16;
+    while (slots < 2 * n) slots <<= 1;
+    uint32_t mask = slots - 1;
+    int32_t* keys = (int32_t*)malloc(sizeof(int32_t) * slots);
+    uint32_t* cnt = (uint32_t*)calloc(slots, sizeof(uint32_t));
+    uint32_t* slot_of = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+    for (size_t i = 0; i < n; i++) {
+        int32_t k = c->pk[a + i];
+        uint32_t h = (mj_hash(k) >> 8) & mask;
+        while (cnt[h] != 0 && keys[h] != k) h = (h + 1) & mask;
+        keys[h] = k;
+        cnt[h]++;
+        slot_of[i] = h;
+    }
+    uint32_t* off = (uint32_t*)malloc(sizeof(uint32_t) * (slots + 1));
+    uint32_t acc = 0;
+    for (uint32_t s = 0; s < slots; s++) {
+        off[s] = acc;
+        acc += cnt[s];
+    }
+    off[slots] = acc;
+    int32_t* vals = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+    uint32_t* cur = (uint32_t*)malloc(sizeof(uint32_t) * slots);
+    memcpy(cur, off, sizeof(uint32_t) * slots);
+    for (size_t i = 0; i < n; i++) vals[cur[slot_of[i]]++] = c->pp[a + i];
+    free(cur);
+    free(slot_of);
+    c->tmask[p] = mask;
+    c->tkey[p] = keys;
+    c->tcnt[p] = cnt;
+    c->toff[p] = off;
+    c->tval[p] = vals;
+}
+
+/* the build rows of key k: *len of them from tval[p] + the returned start */
+static inline uint32_t mj_find(const mj_ctx* c, int32_t k, uint32_t* len, int* part) {
+    uint32_t hh = mj_hash(k);
+    int p = (int)(hh & (MJ_P - 1));
+    uint32_t mask = c->tmask[p], h = (hh >> 8) & mask;
+    const uint32_t* cnt = c->tcnt[p];
+    const int32_t* keys = c->tkey[p];
+    while (cnt[h] != 0 && keys[h] != k) h = (h + 1) & mask;
+    *part = p;
+    *len = cnt[h];
+    return c->toff[p][h];
+}
+
+static void* mj_worker(void* v) {
+    mj_arg* g = (mj_arg*)v;
+    mj_ctx* c = g->c;
+    const int t = g->t, T = c->T;
+    size_t lo, hi;
+    if (g->phase == 0) {  /* build histogram */
+        mj_range(c->n1, T, t, &lo, &hi);
+        for (int p = 0; p < MJ_P; p++) c->hist[t][p] = 0;
+        for (size_t i = lo; i < hi; i++) c->hist[t][mj_hash(c->c1[i]) & (MJ_P - 1)]++;
+    } else if (g->phase == 1) {  /* build scatter (hist now holds offsets) */
+        mj_range(c->n1, T, t, &lo, &hi);
+        for (size_t i = lo; i < hi; i++) {
+            size_t o = c->hist[t][mj_hash(c->c1[i]) & (MJ_P - 1)]++;
+            c->pk[o] = c->c1[i];
+            c->pp[o] = c->p1[i];
+        }
+    } else if (g->phase == 2) {  /* partition tables */
+        for (int p = t; p < MJ_P; p += T) mj_build_part(c, p);
+    } else if (g->phase == 3) {  /* probe count */
+        mj_range(c->n2, T, t, &lo, &hi);
+        size_t m = 0;
+        for (size_t j = lo; j < hi; j++) {
+            uint32_t len;
+            int p;
+            (void)mj_find(c, c->c2[j], &len, &p);
+            m += len;
+        }
+        c->pcount[t] = m;
+    } else {  /* probe write (pcount now holds offsets) */
+        mj_range(c->n2, T, t, &lo, &hi);
+        size_t o = c->pcount[t];
+        for (size_t j = lo; j < hi; j++) {
+            uint32_t len;
+            int p;
+            uint32_t a = mj_find(c, c->c2[j], &len, &p);
+            for (uint32_t e = 0; e < len; e++) {
+                c->out1[o] = c->tval[p][a + e];
+                c->out2[o] = c->p2[j];
+                o++;
+            }
+        }
+    }
+    return NULL;
+}
+
+static void mj_phase(mj_ctx* c, int phase) {
+    pthread_t th[256];
+    mj_arg a[256];
+    for (int t = 0; t < c->T; t++) {
+        a[t] = (mj_arg){c, t, phase};
+        pthread_create(&th[t], NULL, mj_worker, &a[t]);
+    }
+    for (int t = 0; t < c->T; t++) pthread_join(th[t], NULL);
+}
+
+/* Returns M; writes the pairs when out1 != NULL and M <= cap, else (size_t)-1. */
+size_t rc_hash_join_mt(const int32_t* c1, const int32_t* p1, size_t n1, const int32_t* c2, const int32_t* p2,
+                       size_t n2, int32_t* out1, int32_t* out2, size_t cap, int nthreads) {
+    if (n1 == 0 || n2 == 0) return 0;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    mj_ctx* c = (mj_ctx*)calloc(1, sizeof(mj_ctx));
+    c->c1 = c1, c->p1 = p1, c->c2 = c2, c->p2 = p2, c->n1 = n1, c->n2 = n2, c->T = nthreads;
+    c->hist = (size_t(*)[MJ_P])malloc(sizeof(size_t) * MJ_P * (size_t)nthreads);
+    c->pk = (int32_t*)malloc(sizeof(int32_t) * n1);
+    c->pp = (int32_t*)malloc(sizeof(int32_t) * n1);
+    c->pcount = (size_t*)malloc(sizeof(size_t) * (size_t)nthreads);
+    mj_phase(c, 0);
+    size_t acc = 0;
+    for (int p = 0; p < MJ_P; p++) {  /* partition p's rows: thread 0's range first */
+        c->poff[p] = acc;
+        for (int t = 0; t < nthreads; t++) {
+            size_t h = c->hist[t][p];
+            c->hist[t][p] = acc;
+            acc += h;
+        }
+    }
+    c->poff[MJ_P] = acc;
+    mj_phase(c, 1);
+    mj_phase(c, 2);
+    mj_phase(c, 3);
+    size_t m = 0;
+    for (int t = 0; t < nthreads; t++) {
+        size_t x = c->pcount[t];
+        c->pcount[t] = m;
+        m += x;
+    }
+    size_t ret = m;
+    if (out1) {
+        if (m > cap) ret = (size_t)-1;
+        else {
+            c->out1 = out1, c->out2 = out2;
+            mj_phase(c, 4);
+        }
+    }
+    for (int p = 0; p < MJ_P; p++) {
+        free(c->tkey[p]);
+        free(c->tcnt[p]);
+        free(c->toff[p]);
+        free(c->tval[p]);
+    }
+    free(c->hist);
+    free(c->pk);
+    free(c->pp);
+    free(c->pcount);
+    free(c);
+    return ret;
+}
+
 /* src/query.c:585-650 nested_loop_join: outer column_one, inner column_two. */
 size_t rc_nested_loop_join(const int32_t* c1, const int32_t* p1, size_t n1,
                            const int32_t* c2, const int32_t* p2, size_t n2,

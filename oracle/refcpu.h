@@ -70,6 +70,10 @@ int rc_shared_select(const int32_t* data, size_t n, const int32_t* lows, const i
 size_t rc_hash_join(const int32_t* c1, const int32_t* p1, size_t n1,
                     const int32_t* c2, const int32_t* p2, size_t n2,
                     int32_t* out1, int32_t* out2, size_t cap);
+/* The same over nthreads host threads (partitioned build, range-split probe): the
+ * config-5 host-cores baseline; output identical to rc_hash_join. */
+size_t rc_hash_join_mt(const int32_t* c1, const int32_t* p1, size_t n1, const int32_t* c2, const int32_t* p2,
+                       size_t n2, int32_t* out1, int32_t* out2, size_t cap, int nthreads);
 size_t rc_nested_loop_join(const int32_t* c1, const int32_t* p1, size_t n1,
                            const int32_t* c2, const int32_t* p2, size_t n2,
                            int32_t* out1, int32_t* out2, size_t cap);

@@ -61,6 +61,7 @@ def _bind(lib: C.CDLL) -> C.CDLL:
                                        C.c_int, _i32, _i32]),
         "rc_hash_join": (_sz, [_vp, _vp, _sz, _vp, _vp, _sz, _vp, _vp, _sz]),
         "rc_nested_loop_join": (_sz, [_vp, _vp, _sz, _vp, _vp, _sz, _vp, _vp, _sz]),
+        "rc_hash_join_mt": (_sz, [_vp, _vp, _sz, _vp, _vp, _sz, _vp, _vp, _sz, C.c_int]),
         "rc_multimap_size": (_i32, [_i32]),
         "rc_csv_header_len": (_sz, [_vp, _sz]),
         "rc_load_csv": (_sz, [_vp, _sz, C.c_int, _vp, _sz, _vp]),
@@ -218,6 +219,17 @@ def hash_join(c1, p1, c2, p2, nested: bool = False):
     o1 = np.empty(max(m, 1), dtype=np.int32)
     o2 = np.empty(max(m, 1), dtype=np.int32)
     m2 = fn(_a(c1), _a(p1), len(c1), _a(c2), _a(p2), len(c2), _a(o1), _a(o2), m)
+    assert m2 == m
+    return o1[:m].copy(), o2[:m].copy()
+
+
+def hash_join_mt(c1, p1, c2, p2, nthreads: int):
+    """rc_hash_join_mt: the join over nthreads host threads (same output as hash_join)."""
+    L = lib()
+    m = L.rc_hash_join_mt(_a(c1), _a(p1), len(c1), _a(c2), _a(p2), len(c2), None, None, 0, nthreads)
+    o1 = np.empty(max(m, 1), dtype=np.int32)
+    o2 = np.empty(max(m, 1), dtype=np.int32)
+    m2 = L.rc_hash_join_mt(_a(c1), _a(p1), len(c1), _a(c2), _a(p2), len(c2), _a(o1), _a(o2), m, nthreads)
     assert m2 == m
     return o1[:m].copy(), o2[:m].copy()
 

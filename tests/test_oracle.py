@@ -99,6 +99,24 @@ def test_oracle_matches_join_dup_goldens(refcpu, goldens):
         assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"]), n
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_host_cores_join_equals_restatement(refcpu, goldens, threads):
+    """rc_hash_join_mt (the config-5 host-cores baseline) = rc_hash_join on the unique and
+    many-to-many goldens to 2^20 and on a dense small-domain case (long runs)."""
+    rows = [(r, "build", "probe") for r in goldens["join"] if "dup" not in r] + \
+           [(r, "build_dup", "probe_dup") for r in goldens["join_dup"] if r["n"] <= 1 << 20]
+    for r, kb, kp in rows:
+        n = r["n"]
+        p = refcpu.gen_join(n, "iota")
+        o1, o2 = refcpu.hash_join_mt(refcpu.gen_join(n, kb), p, refcpu.gen_join(n, kp), p, threads)
+        assert (len(o1), f"{refcpu.fnv1a64_pairs(o1, o2):016x}") == (r["m"], r["pairs_fnv1a64"]), (n, kb)
+    rng = np.random.default_rng(threads)
+    c1, c2 = rng.integers(-5, 5, 5000).astype(np.int32), rng.integers(-6, 6, 3000).astype(np.int32)
+    p1, p2 = np.arange(5000, dtype=np.int32), np.arange(3000, dtype=np.int32) * 3
+    w, g = refcpu.hash_join(c1, p1, c2, p2), refcpu.hash_join_mt(c1, p1, c2, p2, threads)
+    assert np.array_equal(w[0], g[0]) and np.array_equal(w[1], g[1])
+
+
 def test_oracle_reproduces_survey_join_2e24(refcpu, goldens):
     r = [x for x in goldens["join_survey"] if x["n"] == 1 << 24][0]
     n = r["n"]
