@@ -330,6 +330,14 @@ def inproc_join_leg(lib, mq, torch, devices, gold, logn: int = 28, reps: int = 3
 
 
 def main() -> None:
+    if "--api-child" in sys.argv[1:]:
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--api-child", action="store_true")
+        ap.add_argument("--rows", type=int, default=1_000_000_000)
+        ap.add_argument("--lo", type=int, required=True)
+        ap.add_argument("--hi", type=int, required=True)
+        api_child(ap.parse_args())
+        return
     if "--inproc" in sys.argv[1:]:
         ap = argparse.ArgumentParser()
         ap.add_argument("--inproc", action="store_true")
@@ -795,7 +803,7 @@ def extra_legs(lib, mq, torch, dev, stream, col, ws, ws_bytes, n, lo, hi, gold, 
     out["load_csv_config3_table"] = load_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["index_build"] = index_leg(lib, mq, torch, dev, stream, col, n, cpu=cpu)
     out["pcie_probe"] = pcie_probe(torch, dev, stream)
-    out["api_path_config3"] = api_leg(lib, mq, n, lo, hi, gold)
+    out["api_path_config3"] = api_leg_processes(n, lo, hi)
     return out
 
 
@@ -879,6 +887,49 @@ def positions_sweep(lib, mq, torch, dev, stream, col, col1, ws, ws_bytes, n, pos
                     row[form]["parity"] = (k, f"{fnv:016x}") == (want[0]["k"], want[0]["pos_fnv1a64"])
         res[f"sel_{sel:g}"] = row
     return res
+
+
+def api_leg_processes(n, lo, hi, procs: int = 3) -> dict:
+    """api_leg in `procs` fresh processes, one after the other (the API
+    path's time varies from process to process: payload pages, helper-thread placement).
+    Reports the median over the processes of each process's median, with the spread, and
+    every process's record."""
+    import subprocess
+    runs = []
+    for _ in range(procs):
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--api-child", "--rows", str(n),
+                            "--lo", str(lo), "--hi", str(hi)], capture_output=True, text=True, timeout=600)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not line:
+            runs.append({"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-400:]})
+            continue
+        runs.append(json.loads(line[-1]))
+    ok = [x for x in runs if "error" not in x]
+    res = {"processes": procs, "per_process": runs}
+    if ok:
+        for key in ("ms_select_column", "ms_fetch_column", "ms_average", "ms_chain", "ms_free_results",
+                    "d2h_payload_gbs", "ms_upload_two_columns"):
+            v = [x[key] for x in ok if x.get(key) is not None]
+            if v:
+                res[key] = statistics.median(v)
+                res[key + "_spread"] = [min(v), max(v)]
+        res["k"] = ok[0]["k"]
+        res["avg"] = ok[0]["avg"]
+        res["parity"] = all(x.get("parity") is True for x in ok) and len(ok) == procs
+        res["note"] = ("median over the processes of each process's median of 4 reps (spread = min, max of "
+                       "the process medians); " + ok[0]["note"])
+    else:
+        res["parity"] = False
+    return res
+
+
+def api_child(args) -> None:
+    """One api_leg process (bench.py --api-child): libmq through ctypes, no torch."""
+    mq = _load("mq_binding", os.path.join(PKG, "mq.py"))
+    lib = mq.load()
+    mq.check(lib.mq_init(0), "mq_init")
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "goldens.json")))
+    print(json.dumps(api_leg(lib, mq, args.rows, args.lo, args.hi, gold)), flush=True)
 
 
 def api_leg(lib, mq, n, lo, hi, gold) -> dict:

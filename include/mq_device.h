@@ -86,9 +86,9 @@ void mq_thread_release(void);
  * and column copies in it). mq_pool_free hands the block out again at once, so it
  * frees only what no queued work still uses; mq_pool_free_on is the stream-ordered
  * free: the block is reused only after the work queued on `stream` so far has
- * finished (an event recorded on it; the next allocation that needs the block waits
- * for that event), so a caller frees right after queueing the last kernel that reads
- * it, with no host sync. Both also accept pointers from mq_malloc (freed at once;
+ * finished (an event recorded on it; an allocation meanwhile gets a fresh block and
+ * waits for the event only when no fresh block fits in HBM), so a caller frees right
+ * after queueing the last kernel that reads it, with no host sync. Both also accept pointers from mq_malloc (freed at once;
  * mq_pool_free_on syncs the stream first). Call mq_pool_free_on with the block's
  * device current. */
 int mq_pool_malloc(void** dptr, size_t bytes);

@@ -22,11 +22,12 @@ def lib():
     return L
 
 
-def test_ordered_free_waits_for_queued_writers(lib):
+def test_ordered_free_is_not_reused_while_queued_writers_run(lib):
     """200 writes of 2^26 rows (~30 ms) queued on stream A into block X, X freed on A at
-    once, then the same size allocated: it is X again (best fit), and a write of iota on
-    the null stream into it must be the block's final content. Had the allocator handed
-    X out while A still ran, A's later writes would land after the iota."""
+    once, then the same size allocated: while A's writes are queued X is not handed out
+    (round 6, ADVICE r05: a fresh block instead of a wait, so callers on other streams
+    never wait for each other; the wait is left for when no fresh block fits). A write of
+    iota into the new block is its final content, and once A has finished X is reused."""
     n = 1 << 26
     lib.mq_trim()  # no other idle block of this size to pick instead
     a = C.c_void_p()
@@ -38,13 +39,17 @@ def test_ordered_free_waits_for_queued_writers(lib):
     mq.check(lib.mq_pool_free_on(x, a), "pool_free_on")
     y = C.c_void_p()
     mq.check(lib.mq_pool_malloc(C.byref(y), n * 4), "pool_malloc")
-    assert y.value == x.value  # the same block (else the test proves nothing)
+    assert y.value != x.value  # X's free is still in flight
     mq.check(lib.mq_gen_iota(y, n, None), "iota")
     mq.check(lib.mq_stream_sync(None), "sync")
     mq.check(lib.mq_stream_sync(a), "sync")
     out = np.empty(n, dtype=np.int32)
     mq.check(lib.mq_memcpy_d2h(out.ctypes.data, y, out.nbytes, None), "d2h")
     assert np.array_equal(out, np.arange(n, dtype=np.int32))
+    z = C.c_void_p()
+    mq.check(lib.mq_pool_malloc(C.byref(z), n * 4), "pool_malloc")
+    assert z.value == x.value  # A has finished: X is idle again, the best fit
+    lib.mq_pool_free(z)
     lib.mq_pool_free(y)
     mq.check(lib.mq_stream_destroy(a), "stream destroy")
 

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic of the 2^28 config-5 joins (tools/join_bench.py, 5 joins a run)
+from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, against each kernel's
+design bytes, for the round-5 design and this round's.
+
+  python tools/pmc_join_report.py <r05 dir> <r06 dir> --out profiles/r06_pmc_join.json
+(each dir holds ju/ and jd/ with fetch_counter_collection.csv / write_counter_collection.csv)
+
+FETCH_SIZE is reported raw and x 2 (the guide's gfx950 correction for 16-B/lane streams;
+most of these kernels load 4-8 B a lane, for which the raw count may already be whole:
+the two bracket the read bytes). WRITE_SIZE is exact for coalesced stores.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import statistics
+
+N = 1 << 28
+M_UNIQUE, M_DUP = 134232477, 268413968
+
+
+def per_kernel(path, counter):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            out[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def short(name):
+    s = name.replace("(anonymous namespace)::", "")
+    if s.startswith("void "):
+        s = s[5:]
+    depth = 0
+    for i, c in enumerate(s):
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == "(" and depth == 0 and i > 0:
+            return s[:i]
+    return s
+
+
+def design(kernel, m):
+    """(read, write) design bytes per launch; None when not a join kernel."""
+    n = N
+    t = {
+        "k_win_hist<true>": (4 * n, 0), "k_win_hist<false>": (8 * n, 0),
+        "k_win_scatter<true>": (8 * n, 8 * n), "k_win_scatter<false>": (8 * n, 8 * n),
+        "k_pwin_scatter": (4 * n, 4 * n),
+        "k_win_join<unsigned int>": (12 * n, 4 * n),
+        "k_pwin_gather<false, unsigned int, false>": (8 * n, 4 * n),
+        "k_pwin_gather<true, unsigned int, false>": (8 * n, 4 * n + n // 8),
+        "k_join_write_hits4": (8 * n + n // 8, 8 * m),
+        "k_pwin_gather_write<unsigned int, 0>": (12 * n, 8 * m),
+        # many-to-many
+        "k_win_build_runs": (8 * n, 8 * 2 * n + 4 * n),  # the 2^29-slot table + the run array
+        "k_win_probe_tab<unsigned long long>": (4 * n + 8 * 2 * n, 8 * n),
+        "k_win_join_runs": (12 * n, 8 * n),
+        "k_pwin_gather<false, unsigned long long, false>": (12 * n, 8 * n),
+        "k_pwin_gather<true, unsigned long long, true>": (12 * n, 4 * n + 8 * n + n // 16),
+        "k_join_write_runs16<8>": (4 * n + 8 * n + 4 * n + n // 8, 8 * m),
+        "k_pwin_gather_write<unsigned long long, 2>": (16 * n, 8 * m),
+    }
+    return t.get(kernel)
+
+
+def report(d, m):
+    fetch = per_kernel(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
+    rows = {}
+    for name in set(fetch) | set(write):
+        k = short(name)
+        des = design(k, m)
+        if des is None:
+            continue
+        f = statistics.mean(fetch.get(name, [0.0])) * 1024
+        w = statistics.mean(write.get(name, [0.0])) * 1024
+        rows[k] = {"launches": len(fetch.get(name, [])), "read_raw_gb": f / 1e9, "read_x2_gb": 2 * f / 1e9,
+                   "write_gb": w / 1e9, "design_read_gb": des[0] / 1e9, "design_write_gb": des[1] / 1e9,
+                   "read_ratio_raw": f / des[0] if des[0] else None,
+                   "read_ratio_x2": 2 * f / des[0] if des[0] else None,
+                   "write_ratio": w / des[1] if des[1] else None}
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("r05")
+    ap.add_argument("r06")
+    ap.add_argument("--out", default="profiles/r06_pmc_join.json")
+    a = ap.parse_args()
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                     "tools/join_bench.py 28 [dup] (5 joins a run, averaged per launch)",
+           "n_build": N, "n_probe": N, "m_unique": M_UNIQUE, "m_many_to_many": M_DUP,
+           "note": "read_raw = FETCH_SIZE x 1 KiB, read_x2 = the gfx950 16-B/lane correction; "
+                   "the kernels' 4-8 B/lane loads lie between the two",
+           "round5_design": {"unique": report(os.path.join(a.r05, "ju"), M_UNIQUE),
+                             "many_to_many": report(os.path.join(a.r05, "jd"), M_DUP)},
+           "round6_design": {"unique": report(os.path.join(a.r06, "ju"), M_UNIQUE),
+                             "many_to_many": report(os.path.join(a.r06, "jd"), M_DUP)}}
+    json.dump(res, open(a.out, "w"), indent=1)
+    for rnd in ("round5_design", "round6_design"):
+        for kind, rows in res[rnd].items():
+            print(rnd, kind)
+            for k, v in sorted(rows.items(), key=lambda kv: -kv[1]["design_read_gb"]):
+                print(f"  {k[:48]:48s} rd raw {v['read_ratio_raw'] or 0:5.2f}x  x2 {v['read_ratio_x2'] or 0:5.2f}x"
+                      f"  wr {v['write_ratio'] or 0:5.2f}x")
+
+
+if __name__ == "__main__":
+    main()
