@@ -88,7 +88,10 @@ __device__ __forceinline__ void tile_range(const Seg* segs, const uint32_t* tseg
     len = r < kMTile ? r : kMTile;
 }
 
-// Per tile: counts of the level's digit, into hist[t0 * P + d * nt + tin].
+// Per tile: counts of the level's digit, into hist[t0 * P + d * nt + tin]: from the int32
+// column (level 0) or from the digit bytes the previous scatter wrote. (Round 6 measured
+// the histogram computing the digits from the previous scatter's words instead, with no
+// digit bytes written: 14.77 ms against 14.23 at 1e9, alternating on one box.)
 template <bool FIRST, bool WIDE>
 __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, const uint8_t* __restrict__ dig,
                                                   const Seg* __restrict__ segs, const uint32_t* __restrict__ tseg,
@@ -101,19 +104,43 @@ __global__ __launch_bounds__(kMT) void k_msd_hist(const int* __restrict__ col, c
     uint32_t tin, len;
     tile_range(segs, tseg, xcd_tile(blockIdx.x, gridDim.x), sg, tin, len);
     const u64 e0 = sg.start + (u64)tin * kMTile;
-    uint32_t d[kMI];
+    if constexpr (FIRST) {
+        uint32_t d[kMI];
 #pragma unroll
-    for (int k = 0; k < kMI; k++) {
-        const uint32_t i = (uint32_t)k * kMT + tid;
-        const u64 ic = e0 + (i < len ? i : len - 1);
-        if constexpr (FIRST)
+        for (int k = 0; k < kMI; k++) {
+            const uint32_t i = (uint32_t)k * kMT + tid;
+            const u64 ic = e0 + (i < len ? i : len - 1);
             d[k] = digit_m<WIDE>(((uint32_t)__builtin_nontemporal_load(col + ic) ^ 0x80000000u) - kmin, M);
-        else
-            d[k] = (uint32_t)__builtin_nontemporal_load(dig + ic);
-    }
+        }
 #pragma unroll
-    for (int k = 0; k < kMI; k++)
-        if ((uint32_t)k * kMT + tid < len) atomicAdd(&h[d[k]], 1u);
+        for (int k = 0; k < kMI; k++)
+            if ((uint32_t)k * kMT + tid < len) atomicAdd(&h[d[k]], 1u);
+    } else {
+        // (round 6) the tile's digit bytes as the dwords covering [e0, e0 + len): a byte
+        // load a lane made the pass issue-bound (1 GB in 0.43 ms at 1e9 rows). dig holds
+        // at least n + 3 bytes, so the last dword is inside it.
+        constexpr int kDW = kMI / 4 + 1;
+        const u64 a0 = e0 & ~3ull;
+        const uint32_t lead = (uint32_t)(e0 - a0), nw = (lead + len + 3u) >> 2;
+        const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dig) + (a0 >> 2);
+        uint32_t wv[kDW];
+#pragma unroll
+        for (int k = 0; k < kDW; k++) {
+            const uint32_t i = (uint32_t)k * kMT + tid;
+            wv[k] = i < nw ? __builtin_nontemporal_load(d32 + i) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kDW; k++) {
+            const uint32_t i = (uint32_t)k * kMT + tid;
+            if (i < nw) {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t b = 4u * i + j;
+                    if (b >= lead && b < lead + len) atomicAdd(&h[(wv[k] >> (8u * j)) & 0xFFu], 1u);
+                }
+            }
+        }
+    }
     __syncthreads();
     if (tid < (int)P) hist[(u64)sg.t0 * P + (u64)tid * sg.nt + tin] = h[tid];
 }
@@ -231,6 +258,8 @@ __global__ __launch_bounds__(kMT) void k_msd_scatter(const int* __restrict__ col
             const uint32_t d = digit_m<WIDE>(x, M);
             const u64 dst = gofs[d] + (e - loff[d]);
             out[dst] = v;
+            // (round 6 measured the bytes leaving as dwords instead, through LDS and one
+            // dword store per covered dword: the level-0 scatter took 5.09 ms against 4.00)
             if (Mn) dig[dst] = (uint8_t)digit_m<NWIDE>(x - clo[d], Mn);
         }
     }
