@@ -41,6 +41,11 @@ constexpr int kSortItems = 16;  // words per thread of a sort tile (8 and 32 mea
 constexpr int kSortTile = kTPB * kSortItems;  // 4096
 constexpr int kRadix = 256;
 constexpr int kSortTPB = 512;  // sort tile = kSortTPB x kSortItems words (radix_sort_tiles)
+// The probe keys' partition tile: probe_tpb<RT>() x kSortItems keys, RT the window join's
+// per-row result. u32 results: 512 threads (8192 keys, runs of ~32 keys = 128 B a digit);
+// u64 results: 256 (the u64 gathers' LDS stage at 8192 rows would leave one block a CU).
+template <typename RT>
+constexpr int probe_tpb() { return sizeof(RT) == 4 ? 512 : 256; }
 
 typedef unsigned long long u64;
 
@@ -455,29 +460,63 @@ __device__ __forceinline__ u64 win_elem(const int* c1, const int* p1, const u64*
     else return in[i];
 }
 
-template <bool FROM_COLS>
-__global__ __launch_bounds__(kTPB) void k_win_hist(const int* __restrict__ c1,
-                                                   const u64* __restrict__ in, uint64_t n, Win t,
-                                                   int shift, uint32_t* __restrict__ hist,
-                                                   uint32_t ntiles) {
+// Tiles of TPB x kSortItems rows: the build's words in tiles of 256 threads (4096 rows),
+// the probe keys in tiles of probe_tpb<RT>().
+template <bool FROM_COLS, int TPB = kTPB>
+__global__ __launch_bounds__(TPB) void k_win_hist(const int* __restrict__ c1,
+                                                  const u64* __restrict__ in, uint64_t n, Win t,
+                                                  int shift, uint32_t* __restrict__ hist,
+                                                  uint32_t ntiles) {
     __shared__ uint32_t h[kRadix];
-    h[threadIdx.x] = 0;
+    if (threadIdx.x < kRadix) h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    const uint64_t base = (uint64_t)tile * kSortTile;
+    const uint64_t base = (uint64_t)tile * (TPB * kSortItems);
     uint32_t key[kSortItems];  // loaded before any is counted, as in k_sortw_hist
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = base + (uint64_t)k * kTPB + threadIdx.x;
+        const uint64_t i = base + (uint64_t)k * TPB + threadIdx.x;
         const uint64_t ic = i < n ? i : n - 1;
         key[k] = FROM_COLS ? (uint32_t)__builtin_nontemporal_load(c1 + ic)
                            : (uint32_t)__builtin_nontemporal_load(in + ic);
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++)
-        if (base + (uint64_t)k * kTPB + threadIdx.x < n) atomicAdd(&h[(win_id(key[k], t) >> shift) & 0xFF], 1u);
+        if (base + (uint64_t)k * TPB + threadIdx.x < n) atomicAdd(&h[(win_id(key[k], t) >> shift) & 0xFF], 1u);
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+    if (threadIdx.x < kRadix) hist[(uint64_t)threadIdx.x * ntiles + tile] = h[threadIdx.x];
+}
+
+// After a tile's items are ranked per wave (wcnt[w][d] = wave w's count of digit d):
+// wcnt[w][d] becomes the count of d in the waves before w, loff[d] the tile-local start
+// of digit d. Threads 0..255 (waves 0-3) own the digits; every thread takes the barriers.
+template <int TPB>
+__device__ __forceinline__ void tile_digit_offsets(uint32_t (*wcnt)[kRadix], uint32_t* loff, uint32_t* wsum,
+                                                   int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t tot = 0, incl = 0;
+    if (tid < kRadix) {
+#pragma unroll
+        for (int w = 0; w < TPB / 64; w++) {
+            const uint32_t c = wcnt[w][tid];
+            wcnt[w][tid] = tot;
+            tot += c;
+        }
+        incl = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < kRadix) {
+        uint32_t excl = incl - tot;
+        for (int w = 0; w < wave; w++) excl += wsum[w];
+        loff[tid] = excl;
+    }
+    __syncthreads();
 }
 
 // Stable scatter (k_sortw_scatter's ballot ranking), staged through LDS so that each
@@ -696,21 +735,22 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
 // (k_pwin_gather). Everything moves as streams.
 
 // One LSD pass of the probe keys by window-id digit (k_win_scatter over u32 keys).
-__global__ __launch_bounds__(kTPB) void k_pwin_scatter(const uint32_t* __restrict__ in, uint64_t n, Win t, int shift,
-                                                       const u64* __restrict__ goff, uint32_t ntiles,
-                                                       uint32_t* __restrict__ out) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_pwin_scatter(const uint32_t* __restrict__ in, uint64_t n, Win t, int shift,
+                                                      const u64* __restrict__ goff, uint32_t ntiles,
+                                                      uint32_t* __restrict__ out) {
+    constexpr int kTile = TPB * kSortItems;
+    __shared__ uint32_t wcnt[TPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ uint32_t stage[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ uint32_t stage[kTile];
+    __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     uint32_t el[kSortItems], dr[kSortItems];
 #pragma unroll
@@ -732,25 +772,7 @@ __global__ __launch_bounds__(kTPB) void k_pwin_scatter(const uint32_t* __restric
         dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
-    }
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
-    __syncthreads();
+    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
 #pragma unroll
     for (int k = 0; k < kSortItems; k++)
         if (dr[k] != 0xFFFFFFFFu) {
@@ -758,10 +780,10 @@ __global__ __launch_bounds__(kTPB) void k_pwin_scatter(const uint32_t* __restric
             stage[loff[d] + wcnt[wave][d] + r] = el[k];
         }
     __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint32_t e = (uint32_t)(k * kTPB + tid);
+        const uint32_t e = (uint32_t)(k * TPB + tid);
         if (e < tn) {
             const uint32_t v = stage[e];
             const uint32_t d = (win_id(v, t) >> shift) & 0xFF;
@@ -1163,25 +1185,25 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict
 // RUNS (with FINAL): rin holds packed runs (0 = no match); per row pstart = the packed
 // run and per 64 rows wcnt = the sum of their run lengths, as k_ht_probe_unique<true>
 // leaves them for the packed-runs write (hits is then that wcnt, as u32).
-template <bool FINAL, typename RT, bool RUNS = false>
-__global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict__ keys, uint64_t n, Win t,
+template <bool FINAL, typename RT, bool RUNS, int TPB>
+__global__ __launch_bounds__(TPB) void k_pwin_gather(const uint32_t* __restrict__ keys, uint64_t n, Win t,
                                                       int shift, const u64* __restrict__ goff, uint32_t ntiles,
                                                       const RT* __restrict__ rin, RT* __restrict__ rout,
                                                       uint32_t* __restrict__ pstart, u64* __restrict__ hits,
                                                       uint32_t sentinel) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    constexpr int kTile = TPB * kSortItems;
+    __shared__ uint32_t wcnt[TPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ RT stage[kSortTile];
-    __shared__ uint8_t sdig[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ RT stage[kTile];
+    __shared__ uint8_t sdig[kTile];
+    __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     uint32_t el[kSortItems], dr[kSortItems];
 #pragma unroll
@@ -1203,25 +1225,7 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
         dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
-    }
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
-    __syncthreads();
+    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
     uint32_t sp[kSortItems];  // each row's place in the tile's digit order
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
@@ -1233,17 +1237,17 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather(const uint32_t* __restrict
         }
     }
     __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
     {
         RT v[kSortItems];  // all reads in flight first
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
-            const uint32_t e = (uint32_t)(k * kTPB + tid);
+            const uint32_t e = (uint32_t)(k * TPB + tid);
             const uint32_t d = e < tn ? sdig[e] : 0u;
             v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : (RT)0;
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) stage[k * kTPB + tid] = v[k];
+        for (int k = 0; k < kSortItems; k++) stage[k * TPB + tid] = v[k];
     }
     __syncthreads();
 #pragma unroll
@@ -1319,19 +1323,20 @@ __device__ __forceinline__ void lb_store(u64* p, u64 v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename RT, int MODE>
-__global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __restrict__ keys, uint64_t n, Win t,
+template <typename RT, int MODE, int TPB>
+__global__ __launch_bounds__(TPB) void k_pwin_gather_write(const uint32_t* __restrict__ keys, uint64_t n, Win t,
                                                             const u64* __restrict__ goff, uint32_t ntiles,
                                                             const RT* __restrict__ rin, const int* __restrict__ p2,
                                                             const int* __restrict__ bpos, uint32_t sentinel,
                                                             int* __restrict__ out1, int* __restrict__ out2,
                                                             u64* status, uint32_t* err) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    constexpr int kTile = TPB * kSortItems;
+    __shared__ uint32_t wcnt[TPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ RT stage[kSortTile];
-    __shared__ uint8_t sdig[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ RT stage[kTile];
+    __shared__ uint8_t sdig[kTile];
+    __shared__ uint32_t wsum[TPB / 64];
     __shared__ u64 s_excl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t tile = blockIdx.x;  // (see kGwGroup)
@@ -1340,12 +1345,11 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __re
         const uint32_t g0 = tile - tile % kSpan;
         if (g0 + kSpan <= ntiles) tile = g0 + (tile & 7u) * kGwGroup + (tile % kSpan) / 8u;
     }
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     __syncthreads();
-    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     uint32_t el[kSortItems], dr[kSortItems];
     int pv[kSortItems];  // the rows' probe positions, loaded with the keys (a load at each
@@ -1370,25 +1374,7 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __re
         dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
-    }
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
-    __syncthreads();
+    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
     uint32_t sp[kSortItems];
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
@@ -1400,17 +1386,17 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __re
         }
     }
     __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
     {
         RT v[kSortItems];
 #pragma unroll
         for (int k = 0; k < kSortItems; k++) {
-            const uint32_t e = (uint32_t)(k * kTPB + tid);
+            const uint32_t e = (uint32_t)(k * TPB + tid);
             const uint32_t d = e < tn ? sdig[e] : 0u;
             v[k] = e < tn ? __builtin_nontemporal_load(rin + gofs[d] + (e - loff[d])) : (RT)0;
         }
 #pragma unroll
-        for (int k = 0; k < kSortItems; k++) stage[k * kTPB + tid] = v[k];
+        for (int k = 0; k < kSortItems; k++) stage[k * TPB + tid] = v[k];
     }
     __syncthreads();
     // each row's pair count (from its result, read from stage twice: once for the wave's
@@ -1453,7 +1439,7 @@ __global__ __launch_bounds__(kTPB) void k_pwin_gather_write(const uint32_t* __re
     __syncthreads();
     uint32_t wbase = 0, ttot = 0;
 #pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
+    for (int w = 0; w < TPB / 64; w++) {
         wbase += w < wave ? wsum[w] : 0u;
         ttot += wsum[w];
     }
@@ -2929,7 +2915,8 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
                         bool defer = false) {
     const Win t = j->win;
     const int passes = j->passes;
-    const uint64_t ntiles = ceil_div(n2, kSortTile), nh = ntiles * kRadix;
+    constexpr int PT = probe_tpb<RT>();  // the probe partition's tile width
+    const uint64_t ntiles = ceil_div(n2, (uint64_t)PT * kSortItems), nh = ntiles * kRadix;
     uint32_t* K[4] = {reinterpret_cast<uint32_t*>(const_cast<int32_t*>(d_c2)), nullptr, nullptr, nullptr};
     u64* hs[3] = {nullptr, nullptr, nullptr};
     RT* R[2] = {nullptr, nullptr};
@@ -2953,12 +2940,12 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
          (scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8));
     if (!ok) return done(set_err(MQ_ENOMEM, "join: partitioned probe buffers (%llu rows)", (unsigned long long)n2));
     for (int p = 0; p < passes; p++) {
-        hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)K[p],
+        hipLaunchKernelGGL((k_win_hist<true, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, (const int*)K[p],
                            (const u64*)nullptr, n2, t, 8 * p, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hs[p], nh, scratch, st);
         if (rc) return done(rc);
-        hipLaunchKernelGGL(k_pwin_scatter, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t, 8 * p, hs[p],
-                           (uint32_t)ntiles, K[p + 1]);
+        hipLaunchKernelGGL(k_pwin_scatter<PT>, dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t, 8 * p,
+                           hs[p], (uint32_t)ntiles, K[p + 1]);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe partition"));
     }
     hipLaunchKernelGGL(k_win_bounds<uint32_t>, dim3(j->nwin / kTPB + 1), dim3(kTPB), 0, st, K[passes], n2, t,
@@ -2989,11 +2976,11 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
             break;
         }
         if (p == 0)
-            hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[0], n2, t,
+            hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[0], n2, t,
                                0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)(RUNS ? (void*)j->p01 : nullptr),
                                pstart, hits, j->sentinel);
         else
-            hipLaunchKernelGGL((k_pwin_gather<false, RT>), dim3((uint32_t)ntiles), dim3(kTPB), 0, st, K[p], n2, t,
+            hipLaunchKernelGGL((k_pwin_gather<false, RT, false, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t,
                                8 * p, hs[p], (uint32_t)ntiles, (const RT*)R[cur], R[cur ^ 1], (uint32_t*)nullptr,
                                (u64*)nullptr, j->sentinel);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe unpartition"));
@@ -3021,7 +3008,8 @@ int probe_partitioned_runs(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_
 int finish_classic(mq_join* j, hipStream_t st) {
     DevState* s;
     if (int rc = ensure_ready(&s)) return rc;
-    const uint64_t n2 = j->n2, nw = (n2 + 63) / 64, ntiles = ceil_div(n2, kSortTile);
+    const int pt = j->dmode == 0 ? probe_tpb<uint32_t>() : probe_tpb<u64>();
+    const uint64_t n2 = j->n2, nw = (n2 + 63) / 64, ntiles = ceil_div(n2, (uint64_t)pt * kSortItems);
     const bool runs = j->dmode == 2;
     j->pstart = (uint32_t*)pool_alloc(n2 * 4);
     j->plen = (uint32_t*)pool_alloc(runs ? nw * 4 : nw * 12);
@@ -3032,15 +3020,17 @@ int finish_classic(mq_join* j, hipStream_t st) {
         return set_err(MQ_ENOMEM, "mq_join_counts: buffers for %llu rows", (unsigned long long)n2);
     uint32_t* const cnt = runs ? j->plen : j->plen + 2 * nw;
     u64* const hits = reinterpret_cast<u64*>(j->plen);
-    const dim3 g((uint32_t)ntiles), b(kTPB);
+    const dim3 g((uint32_t)ntiles), b(pt);
     if (runs)
-        hipLaunchKernelGGL((k_pwin_gather<true, u64, true>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
+        hipLaunchKernelGGL((k_pwin_gather<true, u64, true, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
                            (uint32_t)ntiles, (const u64*)j->dres, j->p01, j->pstart, hits, j->sentinel);
     else if (j->dmode == 1)
-        hipLaunchKernelGGL((k_pwin_gather<true, u64>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0, (uint32_t)ntiles,
+        hipLaunchKernelGGL((k_pwin_gather<true, u64, false, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, n2, j->win, 0,
+                           j->dhs0, (uint32_t)ntiles,
                            (const u64*)j->dres, (u64*)nullptr, j->pstart, hits, j->sentinel);
     else
-        hipLaunchKernelGGL((k_pwin_gather<true, uint32_t>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
+        hipLaunchKernelGGL((k_pwin_gather<true, uint32_t, false, probe_tpb<uint32_t>()>), g, b, 0, st, j->dkeys, n2,
+                           j->win, 0, j->dhs0,
                            (uint32_t)ntiles, (const uint32_t*)j->dres, (uint32_t*)nullptr, j->pstart, hits,
                            j->sentinel);
     LAUNCHCHK("k_pwin_gather");
@@ -3410,22 +3400,23 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
     if ((rc = juse(j, (hipStream_t)stream))) return rc;
     if (j->deferred) {  // the last inverse pass fused with the pair write (look-back over tiles)
         hipStream_t st = (hipStream_t)stream;
-        const uint64_t ntiles = ceil_div(j->n2, kSortTile);
+        const int pt = j->dmode == 0 ? probe_tpb<uint32_t>() : probe_tpb<u64>();
+        const uint64_t ntiles = ceil_div(j->n2, (uint64_t)pt * kSortItems);
         u64* stat = (u64*)pool_alloc(ntiles * 8 + 16);
         if (!stat) return set_err(MQ_ENOMEM, "mq_join_write: tile status");
         HIPCHK(hipMemsetAsync(stat, 0, ntiles * 8 + 16, st));
         HIPCHK(hipMemsetAsync(j->pflag + 1, 0, 4, st));
-        const dim3 g((uint32_t)ntiles), b(kTPB);
+        const dim3 g((uint32_t)ntiles), b(pt);
         if (j->dmode == 2)
-            hipLaunchKernelGGL((k_pwin_gather_write<u64, 2>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 2, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
                                (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
                                j->pflag + 1);
         else if (j->dmode == 1)
-            hipLaunchKernelGGL((k_pwin_gather_write<u64, 1>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 1, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
                                (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
                                j->pflag + 1);
         else
-            hipLaunchKernelGGL((k_pwin_gather_write<uint32_t, 0>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<uint32_t, 0, probe_tpb<uint32_t>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
                                (uint32_t)ntiles, (const uint32_t*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2,
                                stat, j->pflag + 1);
         const hipError_t e = hipGetLastError();
