@@ -38,14 +38,17 @@ constexpr int kTPB = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kTPB * kScanItems;  // 4096
 constexpr int kSortItems = 16;  // words per thread of a sort tile (8 and 32 measured slower)
-constexpr int kSortTile = kTPB * kSortItems;  // 4096
 constexpr int kRadix = 256;
 constexpr int kSortTPB = 512;  // sort tile = kSortTPB x kSortItems words (radix_sort_tiles)
-// The probe keys' partition tile: probe_tpb<RT>() x kSortItems keys, RT the window join's
-// per-row result. u32 results: 512 threads (8192 keys, runs of ~32 keys = 128 B a digit);
-// u64 results: 256 (the u64 gathers' LDS stage at 8192 rows would leave one block a CU).
+// Partition tiles (TPB x kSortItems rows). Round 6, 2^28 joins alternating on one box
+// (unique / many-to-many ms): build words and probe keys in 4096-row tiles 8.68 / 10.47;
+// probe keys of u32-result joins in 8192-key tiles (a digit's run of keys ~128 B, a whole
+// line, not 64 B) 8.29 / 10.37; build words in 8192-word tiles as well 7.85 / 10.17. Not
+// kept: u64-result probes (many-to-many) in 8192-key tiles 11.34 (one block a CU for the
+// u64 gathers' LDS stage) or 6144 12.3; u32 probes in 16384-key tiles 8.84.
 template <typename RT>
 constexpr int probe_tpb() { return sizeof(RT) == 4 ? 512 : 256; }
+constexpr int kBTPB = 512;  // the build words' partition tile: kBTPB x kSortItems
 
 typedef unsigned long long u64;
 
@@ -460,9 +463,9 @@ __device__ __forceinline__ u64 win_elem(const int* c1, const int* p1, const u64*
     else return in[i];
 }
 
-// Tiles of TPB x kSortItems rows: the build's words in tiles of 256 threads (4096 rows),
-// the probe keys in tiles of probe_tpb<RT>().
-template <bool FROM_COLS, int TPB = kTPB>
+// Tiles of TPB x kSortItems rows: the build's words in tiles of kBTPB threads, the
+// probe keys in tiles of probe_tpb<RT>().
+template <bool FROM_COLS, int TPB = kBTPB>
 __global__ __launch_bounds__(TPB) void k_win_hist(const int* __restrict__ c1,
                                                   const u64* __restrict__ in, uint64_t n, Win t,
                                                   int shift, uint32_t* __restrict__ hist,
@@ -521,25 +524,25 @@ __device__ __forceinline__ void tile_digit_offsets(uint32_t (*wcnt)[kRadix], uin
 
 // Stable scatter (k_sortw_scatter's ballot ranking), staged through LDS so that each
 // digit's run leaves the block as contiguous, coalesced stores.
-template <bool FROM_COLS>
-__global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1,
+template <bool FROM_COLS, int TPB = kBTPB>
+__global__ __launch_bounds__(TPB) void k_win_scatter(const int* __restrict__ c1,
                                                       const int* __restrict__ p1,
                                                       const u64* __restrict__ in, uint64_t n, Win t,
                                                       int shift, const u64* __restrict__ goff,
                                                       uint32_t ntiles, u64* __restrict__ out,
                                                       int* __restrict__ pmm = nullptr) {
-    __shared__ uint32_t wcnt[kTPB / 64][kRadix];
+    constexpr int kTile = TPB * kSortItems;
+    __shared__ uint32_t wcnt[TPB / 64][kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
-    __shared__ u64 stage[kSortTile];
-    __shared__ uint32_t wsum[kTPB / 64];
+    __shared__ u64 stage[kTile];
+    __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) wcnt[w][tid] = 0;
+    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
+    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
-    const uint64_t tile0 = (uint64_t)tile * kSortTile;
+    const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
     u64 el[kSortItems];
     uint32_t dr[kSortItems];
@@ -567,12 +570,12 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
             mn = a < mn ? a : mn;
             mx = b > mx ? b : mx;
         }
-        __shared__ int smm[2][kTPB / 64];
+        __shared__ int smm[2][TPB / 64];
         if (lane == 0) smm[0][wave] = mn, smm[1][wave] = mx;
         __syncthreads();
         if (tid == 0) {
 #pragma unroll
-            for (int w = 1; w < kTPB / 64; w++) {
+            for (int w = 1; w < TPB / 64; w++) {
                 mn = smm[0][w] < mn ? smm[0][w] : mn;
                 mx = smm[1][w] > mx ? smm[1][w] : mx;
             }
@@ -594,27 +597,7 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
         dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    // per digit (thread tid = digit): prefix over waves, tile total
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kTPB / 64; w++) {
-        const uint32_t c = wcnt[w][tid];
-        wcnt[w][tid] = tot;
-        tot += c;
-    }
-    // tile-local exclusive scan of the digit totals (256 digits = 4 waves)
-    uint32_t incl = tot;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t excl = incl - tot;
-    for (int w = 0; w < wave; w++) excl += wsum[w];
-    loff[tid] = excl;
-    __syncthreads();
+    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         if (dr[k] != 0xFFFFFFFFu) {
@@ -623,10 +606,10 @@ __global__ __launch_bounds__(kTPB) void k_win_scatter(const int* __restrict__ c1
         }
     }
     __syncthreads();
-    const uint64_t tn = n - tile0 < (uint64_t)kSortTile ? n - tile0 : (uint64_t)kSortTile;
+    const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint32_t e = (uint32_t)(k * kTPB + tid);
+        const uint32_t e = (uint32_t)(k * TPB + tid);
         if (e < tn) {
             const u64 v = stage[e];
             const uint32_t d = (win_id((uint32_t)v, t) >> shift) & 0xFF;
@@ -2552,7 +2535,7 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
     const int wid_bits = lg - t.wlog;
     const int passes = (wid_bits + 7) / 8;
     const uint32_t nw = (uint32_t)(slots >> t.wlog);
-    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t ntiles = ceil_div(n, (uint64_t)kBTPB * kSortItems);
     const uint64_t nh = ntiles * kRadix;
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t *hist = nullptr, *wstart = nullptr;
@@ -2581,19 +2564,19 @@ int insert_unique(mq_join* j, const int* c1, const int* p1, uint64_t n, uint64_t
         // writes them: the byte stores cost the scatter 0.2-0.4 ms at 2^28 against the
         // histogram's 0.32 ms saved; not kept)
         if (pass == 0) {
-            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1,
+            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, c1,
                                (const u64*)nullptr, n, t, shift, hist, (uint32_t)ntiles);
         } else {
-            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st,
+            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st,
                                (const int*)nullptr, src, n, t, shift, hist, (uint32_t)ntiles);
         }
         int rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st);
         if (rc) return done(rc);
         if (pass == 0) {
-            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
+            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, c1, p1,
                                (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst, keep ? pmm : nullptr);
         } else {
-            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st,
+            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st,
                                (const int*)nullptr, (const int*)nullptr, src, n, t, shift, hscan,
                                (uint32_t)ntiles, dst, (int*)nullptr);
         }
@@ -2644,7 +2627,7 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     while ((1ull << lg) < nslot) lg++;
     const int passes = (lg - t.wlog + 7) / 8;
     const uint32_t nw = (uint32_t)(nslot >> t.wlog);
-    const uint64_t ntiles = ceil_div(n, kSortTile);
+    const uint64_t ntiles = ceil_div(n, (uint64_t)kBTPB * kSortItems);
     const uint64_t nh = ntiles * kRadix;
     u64 *a = nullptr, *b = nullptr, *hscan = nullptr, *scratch = nullptr;
     uint32_t *hist = nullptr, *wstart = nullptr;
@@ -2678,17 +2661,17 @@ int build_window_runs(mq_join* j, const int* c1, const int* p1, uint64_t n, uint
     for (int pass = 0; pass < passes; pass++) {
         const int shift = 8 * pass;
         if (pass == 0)
-            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, (const u64*)nullptr, n,
+            hipLaunchKernelGGL(k_win_hist<true>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, c1, (const u64*)nullptr, n,
                                t, shift, hist, (uint32_t)ntiles);
         else
-            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr, src,
+            hipLaunchKernelGGL(k_win_hist<false>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, (const int*)nullptr, src,
                                n, t, shift, hist, (uint32_t)ntiles);
         if ((rc = scan_exclusive<uint32_t>(hist, hscan, nh, scratch, st))) return drop(rc);
         if (pass == 0)
-            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, c1, p1,
+            hipLaunchKernelGGL(k_win_scatter<true>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, c1, p1,
                                (const u64*)nullptr, n, t, shift, hscan, (uint32_t)ntiles, dst, pmm);
         else
-            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kTPB), 0, st, (const int*)nullptr,
+            hipLaunchKernelGGL(k_win_scatter<false>, dim3((uint32_t)ntiles), dim3(kBTPB), 0, st, (const int*)nullptr,
                                (const int*)nullptr, src, n, t, shift, hscan, (uint32_t)ntiles, dst, (int*)nullptr);
         if (hipGetLastError() != hipSuccess) return drop(set_err(MQ_EHIP, "join: window partition"));
         src = dst;
