@@ -15,6 +15,7 @@ import collections
 import csv
 import json
 import os
+import re
 import statistics
 
 N = 1 << 28
@@ -30,7 +31,11 @@ def per_kernel(path, counter):
 
 
 def short(name):
+    """The kernel's name with its template arguments, less a trailing tile width (the
+    round-6 kernels carry it as their last argument: <512>, <..., 256>)."""
     s = name.replace("(anonymous namespace)::", "")
+    s = re.sub(r"<(\d+)>", "", s)
+    s = re.sub(r", (?:256|512)>", ">", s)
     if s.startswith("void "):
         s = s[5:]
     depth = 0
