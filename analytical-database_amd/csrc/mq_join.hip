@@ -43,11 +43,13 @@ constexpr int kSortTPB = 512;  // sort tile = kSortTPB x kSortItems words (radix
 // Partition tiles (TPB x kSortItems rows). Round 6, 2^28 joins alternating on one box
 // (unique / many-to-many ms): build words and probe keys in 4096-row tiles 8.68 / 10.47;
 // probe keys of u32-result joins in 8192-key tiles (a digit's run of keys ~128 B, a whole
-// line, not 64 B) 8.29 / 10.37; build words in 8192-word tiles as well 7.85 / 10.17. Not
-// kept: u64-result probes (many-to-many) in 8192-key tiles 11.34 (one block a CU for the
-// u64 gathers' LDS stage) or 6144 12.3; u32 probes in 16384-key tiles 8.84.
+// line, not 64 B) 8.29 / 10.37; build words in 8192-word tiles as well 7.85 / 10.17; the
+// probe passes recording their places (k_pwin_scatter, the inverse passes without keys,
+// hashing or ranking: their LDS fell from 85 to 41-74 KB) 7.62 / 10.0, and then the u64-
+// result probes in 8192-key tiles too 7.59 / 9.29. Not kept: u32 probes in 16384-key
+// tiles 8.84.
 template <typename RT>
-constexpr int probe_tpb() { return sizeof(RT) == 4 ? 512 : 256; }
+constexpr int probe_tpb() { return 512; }
 constexpr int kBTPB = 512;  // the build words' partition tile: kBTPB x kSortItems
 
 typedef unsigned long long u64;
@@ -717,62 +719,127 @@ __global__ __launch_bounds__(kWinTPB) void k_win_build(const u64* __restrict__ i
 // read), and the results go back to probe order by running the passes backwards
 // (k_pwin_gather). Everything moves as streams.
 
-// One LSD pass of the probe keys by window-id digit (k_win_scatter over u32 keys).
-template <int TPB>
+// Exclusive scan of a tile's 256 digit counts (threads 0..255 own the digits; every
+// thread takes the barriers): loff[d] = the tile-local start of digit d.
+__device__ __forceinline__ void digit_scan(const uint32_t* cnt, uint32_t* loff, uint32_t* wsum, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t c = 0, incl = 0;
+    if (tid < kRadix) {
+        c = cnt[tid];
+        incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < kRadix) {
+        uint32_t ex = incl - c;
+        for (int w = 0; w < wave; w++) ex += wsum[w];
+        loff[tid] = ex;
+    }
+    __syncthreads();
+}
+
+// One pass of the probe keys by window-id digit (round 6 form). The pass records each
+// row's place in its tile's digit order (perm, u16) for the inverse passes, which then
+// neither hash nor rank: they read 2 B a row instead of the 4-B keys. STABLE: rows of a
+// digit keep their order (ballot match-any ranks), which every pass after the first
+// needs, so that the windows come out whole (LSD); the first pass's keys need no order
+// within a digit (each key's result is its own), so there a key takes its place by one
+// LDS atomic.
+template <int TPB, bool STABLE>
 __global__ __launch_bounds__(TPB) void k_pwin_scatter(const uint32_t* __restrict__ in, uint64_t n, Win t, int shift,
                                                       const u64* __restrict__ goff, uint32_t ntiles,
-                                                      uint32_t* __restrict__ out) {
-    constexpr int kTile = TPB * kSortItems;
-    __shared__ uint32_t wcnt[TPB / 64][kRadix];
+                                                      uint32_t* __restrict__ out, uint16_t* __restrict__ perm) {
+    constexpr int kTile = TPB * kSortItems, kW = STABLE ? TPB / 64 : 1;
+    static_assert(kTile <= 65536, "u16 places");
+    __shared__ uint32_t wcnt[kW][kRadix];  // per wave (STABLE) or per tile
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
     __shared__ uint32_t stage[kTile];
+    __shared__ uint8_t sdig[kTile];
     __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    for (int x = tid; x < kW * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
     __syncthreads();
     const uint64_t tile0 = (uint64_t)tile * kTile;
-    const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
+    // rows: STABLE, wave w owns 64 * kSortItems consecutive rows (ranks in row order);
+    // else thread-strided
+    auto row = [&](int k) -> uint64_t {
+        return STABLE ? tile0 + (uint64_t)wave * (64 * kSortItems) + (uint64_t)k * 64 + lane
+                      : tile0 + (uint64_t)k * TPB + tid;
+    };
     uint32_t el[kSortItems], dr[kSortItems];
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const uint64_t i = row(k);
         el[k] = __builtin_nontemporal_load(in + (i < n ? i : n - 1));
     }
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        const uint64_t i = row(k);
         const bool valid = i < n;
         const uint32_t d = (win_id(el[k], t) >> shift) & 0xFF;
-        const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = lanes_below(peers);
-        const uint32_t cur = wcnt[wave][d];
-        __builtin_amdgcn_wave_barrier();
-        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+        if constexpr (STABLE) {
+            const u64 peers = match_any8(d, __ballot(valid));
+            const uint32_t lt = lanes_below(peers);
+            const uint32_t cur = wcnt[wave][d];
+            __builtin_amdgcn_wave_barrier();
+            if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+            dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
+        } else {
+            dr[k] = valid ? (d << 16) | atomicAdd(&wcnt[0][d], 1u) : 0xFFFFFFFFu;
+        }
     }
     __syncthreads();
-    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
+    if constexpr (STABLE) tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
+    else digit_scan(wcnt[0], loff, wsum, tid);
 #pragma unroll
-    for (int k = 0; k < kSortItems; k++)
+    for (int k = 0; k < kSortItems; k++) {
+        const uint64_t i = row(k);
         if (dr[k] != 0xFFFFFFFFu) {
-            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
-            stage[loff[d] + wcnt[wave][d] + r] = el[k];
+            const uint32_t d = dr[k] >> 16;
+            const uint32_t sp = loff[d] + (STABLE ? wcnt[wave][d] : 0u) + (dr[k] & 0xFFFF);
+            stage[sp] = el[k];
+            sdig[sp] = (uint8_t)d;
+            perm[i] = (uint16_t)sp;
         }
+    }
     __syncthreads();
     const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint32_t e = (uint32_t)(k * TPB + tid);
         if (e < tn) {
-            const uint32_t v = stage[e];
-            const uint32_t d = (win_id(v, t) >> shift) & 0xFF;
-            out[gofs[d] + (e - loff[d])] = v;
+            const uint32_t d = sdig[e];
+            out[gofs[d] + (e - loff[d])] = stage[e];
         }
     }
+}
+
+// The inverse passes' view of a tile: gofs[d] = where digit d's run of the tile starts in
+// the pass's output, loff[d] its tile-local start (from the pass's scanned offsets: a
+// run's length is the next offset's distance), sdig[e] = the digit of place e.
+__device__ __forceinline__ void tile_runs(const u64* __restrict__ goff, uint32_t ntiles, uint32_t tile, uint64_t n,
+                                          u64* gofs, uint32_t* cnt, uint32_t* loff, uint8_t* sdig, uint32_t* wsum,
+                                          int tid) {
+    if (tid < kRadix) {
+        const uint64_t x = (uint64_t)tid * ntiles + tile;
+        const u64 g = goff[x], gn = x + 1 < (uint64_t)kRadix * ntiles ? goff[x + 1] : n;
+        gofs[tid] = g;
+        cnt[tid] = (uint32_t)(gn - g);
+    }
+    __syncthreads();
+    digit_scan(cnt, loff, wsum, tid);
+    if (tid < kRadix)
+        for (uint32_t e = loff[tid], e1 = loff[tid] + cnt[tid]; e < e1; e++) sdig[e] = (uint8_t)tid;
+    __syncthreads();
 }
 
 // Persistent window kernels (round 5): a window is a small job (8192 slots' worth of
@@ -1159,67 +1226,39 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict
     if ((threadIdx.x & 63) == 0 && pairs) atomicAdd(mtot, pairs);
 }
 
-// The inverse of one k_pwin_scatter pass: keys = that pass's input (tile order), rin =
-// per-row results in its output order; rout[i] = the result of input row i. The tile's
-// rows are ranked exactly as the scatter ranked them, so row i's place in the output is
-// known; each digit's run of the tile is read from rin as a contiguous stretch (staged in
-// LDS by place) and every row takes its own value back. FINAL (the pass over the probe
-// column itself): per row the payload (pstart) and, per 64 rows, the hit word.
+// The inverse of one k_pwin_scatter pass: perm = that pass's places (a row's place in
+// its tile's digit order), rin = per-row results in the pass's output order; rout[i] =
+// the result of input row i. Each digit's run of the tile is read from rin as a
+// contiguous stretch (staged in LDS by place) and every row takes its own value back.
+// FINAL (the pass over the probe column itself): per row the payload (pstart) and, per
+// 64 rows, the hit word.
 // RUNS (with FINAL): rin holds packed runs (0 = no match); per row pstart = the packed
 // run and per 64 rows wcnt = the sum of their run lengths, as k_ht_probe_unique<true>
 // leaves them for the packed-runs write (hits is then that wcnt, as u32).
 template <bool FINAL, typename RT, bool RUNS, int TPB>
-__global__ __launch_bounds__(TPB) void k_pwin_gather(const uint32_t* __restrict__ keys, uint64_t n, Win t,
-                                                      int shift, const u64* __restrict__ goff, uint32_t ntiles,
-                                                      const RT* __restrict__ rin, RT* __restrict__ rout,
-                                                      uint32_t* __restrict__ pstart, u64* __restrict__ hits,
-                                                      uint32_t sentinel) {
+__global__ __launch_bounds__(TPB) void k_pwin_gather(const uint16_t* __restrict__ perm, uint64_t n,
+                                                     const u64* __restrict__ goff, uint32_t ntiles,
+                                                     const RT* __restrict__ rin, RT* __restrict__ rout,
+                                                     uint32_t* __restrict__ pstart, u64* __restrict__ hits,
+                                                     uint32_t sentinel) {
     constexpr int kTile = TPB * kSortItems;
-    __shared__ uint32_t wcnt[TPB / 64][kRadix];
+    __shared__ uint32_t cnt[kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
     __shared__ RT stage[kTile];
     __shared__ uint8_t sdig[kTile];
     __shared__ uint32_t wsum[kRadix / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
-    __syncthreads();
     const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
-    uint32_t el[kSortItems], dr[kSortItems];
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        el[k] = __builtin_nontemporal_load(keys + (i < n ? i : n - 1));
-    }
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        const bool valid = i < n;
-        const uint32_t d = (win_id(el[k], t) >> shift) & 0xFF;
-        const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = lanes_below(peers);
-        const uint32_t cur = wcnt[wave][d];
-        __builtin_amdgcn_wave_barrier();
-        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
     uint32_t sp[kSortItems];  // each row's place in the tile's digit order
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
-        sp[k] = 0;
-        if (dr[k] != 0xFFFFFFFFu) {
-            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
-            sp[k] = loff[d] + wcnt[wave][d] + r;
-            sdig[sp[k]] = (uint8_t)d;
-        }
+        const uint64_t i = seg + (uint64_t)k * 64 + lane;
+        sp[k] = __builtin_nontemporal_load(perm + (i < n ? i : n - 1));
     }
-    __syncthreads();
+    tile_runs(goff, ntiles, tile, n, gofs, cnt, loff, sdig, wsum, tid);
     const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
     {
         RT v[kSortItems];  // all reads in flight first
@@ -1236,7 +1275,7 @@ __global__ __launch_bounds__(TPB) void k_pwin_gather(const uint32_t* __restrict_
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        const bool in = dr[k] != 0xFFFFFFFFu;
+        const bool in = i < n;
         const RT v = in ? stage[sp[k]] : (RT)0;
         if constexpr (FINAL && RUNS && sizeof(RT) == 8) {
             // run2 records: pstart = a packed run (long) or just its length (one or two rows,
@@ -1279,7 +1318,7 @@ __global__ __launch_bounds__(TPB) void k_pwin_gather(const uint32_t* __restrict_
 }
 
 // The last inverse pass fused with the pair write (round 6): k_pwin_gather<true>'s tile
-// (4096 probe rows in row order; each row's result taken back from the window join's
+// (its probe rows in row order; each row's result taken back from the window join's
 // order) counts its pairs, learns the pairs of every earlier tile by decoupled look-back
 // and writes its rows' pairs straight to out1 / out2, so neither the per-row results
 // (pstart, p01: 4-12 B a row written and read back) nor the hit words, their scan and a
@@ -1307,14 +1346,14 @@ __device__ __forceinline__ void lb_store(u64* p, u64 v) {
 }
 
 template <typename RT, int MODE, int TPB>
-__global__ __launch_bounds__(TPB) void k_pwin_gather_write(const uint32_t* __restrict__ keys, uint64_t n, Win t,
+__global__ __launch_bounds__(TPB) void k_pwin_gather_write(const uint16_t* __restrict__ perm, uint64_t n,
                                                             const u64* __restrict__ goff, uint32_t ntiles,
                                                             const RT* __restrict__ rin, const int* __restrict__ p2,
                                                             const int* __restrict__ bpos, uint32_t sentinel,
                                                             int* __restrict__ out1, int* __restrict__ out2,
                                                             u64* status, uint32_t* err) {
     constexpr int kTile = TPB * kSortItems;
-    __shared__ uint32_t wcnt[TPB / 64][kRadix];
+    __shared__ uint32_t cnt[kRadix];
     __shared__ uint32_t loff[kRadix];
     __shared__ u64 gofs[kRadix];
     __shared__ RT stage[kTile];
@@ -1328,47 +1367,18 @@ __global__ __launch_bounds__(TPB) void k_pwin_gather_write(const uint32_t* __res
         const uint32_t g0 = tile - tile % kSpan;
         if (g0 + kSpan <= ntiles) tile = g0 + (tile & 7u) * kGwGroup + (tile % kSpan) / 8u;
     }
-    for (int x = tid; x < (TPB / 64) * kRadix; x += TPB) (&wcnt[0][0])[x] = 0;
-    __syncthreads();
-    if (tid < kRadix) gofs[tid] = goff[(uint64_t)tid * ntiles + tile];
-    __syncthreads();
     const uint64_t tile0 = (uint64_t)tile * kTile;
     const uint64_t seg = tile0 + (uint64_t)wave * (64 * kSortItems);
-    uint32_t el[kSortItems], dr[kSortItems];
-    int pv[kSortItems];  // the rows' probe positions, loaded with the keys (a load at each
-                         // store serialised 16 round trips a wave)
+    uint32_t sp[kSortItems];  // each row's place in the tile's digit order
+    int pv[kSortItems];       // the rows' probe positions, loaded with the places (a load at
+                              // each store serialised 16 round trips a wave)
 #pragma unroll
     for (int k = 0; k < kSortItems; k++) {
         const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        el[k] = __builtin_nontemporal_load(keys + (i < n ? i : n - 1));
+        sp[k] = __builtin_nontemporal_load(perm + (i < n ? i : n - 1));
         pv[k] = out2 ? __builtin_nontemporal_load(p2 + (i < n ? i : n - 1)) : 0;
     }
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        const uint64_t i = seg + (uint64_t)k * 64 + lane;
-        const bool valid = i < n;
-        const uint32_t d = win_id(el[k], t) & 0xFF;
-        const u64 peers = match_any8(d, __ballot(valid));
-        const uint32_t lt = lanes_below(peers);
-        const uint32_t cur = wcnt[wave][d];
-        __builtin_amdgcn_wave_barrier();
-        if (valid && lt == 0) wcnt[wave][d] = cur + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[k] = valid ? ((d << 16) | (cur + lt)) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    tile_digit_offsets<TPB>(wcnt, loff, wsum, tid);
-    uint32_t sp[kSortItems];
-#pragma unroll
-    for (int k = 0; k < kSortItems; k++) {
-        sp[k] = 0;
-        if (dr[k] != 0xFFFFFFFFu) {
-            const uint32_t d = dr[k] >> 16, r = dr[k] & 0xFFFF;
-            sp[k] = loff[d] + wcnt[wave][d] + r;
-            sdig[sp[k]] = (uint8_t)d;
-        }
-    }
-    __syncthreads();
+    tile_runs(goff, ntiles, tile, n, gofs, cnt, loff, sdig, wsum, tid);
     const uint64_t tn = n - tile0 < (uint64_t)kTile ? n - tile0 : (uint64_t)kTile;
     {
         RT v[kSortItems];
@@ -2391,11 +2401,11 @@ struct mq_join {
     bool run2;             // the last probe left short runs' positions in p01 (k_join_write_runs16)
     // deferred (round 6): the partitioned probe stopped before its last inverse pass, which
     // mq_join_write runs fused with the pair write (dmode: 0 unique u32 results, 1 unique
-    // u64, 2 run2 records); dkeys = the probe keys (the caller's, valid until the write),
+    // u64, 2 run2 records); dperm = pass 0's places of the probe rows (pool, owned),
     // dhs0 = pass 0's tile offsets, dres = the results in pass-0 order (pool, owned)
     bool deferred;
     int dmode;
-    const uint32_t* dkeys;
+    uint16_t* dperm;
     u64* dhs0;
     void* dres;
     bool dupw;             // a partitioned build whose probe answers duplicate keys window by
@@ -2891,8 +2901,8 @@ int radix_sort_lsd_index(const int* col, uint64_t n, uint32_t kmin, int npass, i
 namespace {
 
 // defer (round 6): the last inverse pass is left to mq_join_write, fused with the pair
-// write (k_pwin_gather_write); the handle keeps what it reads: the probe keys (the
-// caller's d_c2), pass 0's tile offsets and the results in pass-0 order.
+// write (k_pwin_gather_write); the handle keeps what it reads: pass 0's places of the
+// probe rows, its tile offsets and the results in pass-0 order.
 template <typename RT, bool RUNS = false>
 int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* pstart, u64* hits, hipStream_t st,
                         bool defer = false) {
@@ -2902,12 +2912,14 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     const uint64_t ntiles = ceil_div(n2, (uint64_t)PT * kSortItems), nh = ntiles * kRadix;
     uint32_t* K[4] = {reinterpret_cast<uint32_t*>(const_cast<int32_t*>(d_c2)), nullptr, nullptr, nullptr};
     u64* hs[3] = {nullptr, nullptr, nullptr};
+    uint16_t* P[3] = {nullptr, nullptr, nullptr};  // each pass's places of its input rows
     RT* R[2] = {nullptr, nullptr};
     uint32_t *hist = nullptr, *pws = nullptr;
     u64* scratch = nullptr;
     auto done = [&](int rc) {
         for (int p = 1; p <= passes; p++) pool_free_on(K[p], st);
         for (int p = 0; p < passes; p++) pool_free_on(hs[p], st);
+        for (int p = 0; p < passes; p++) pool_free_on(P[p], st);
         pool_free_on(R[0], st);
         pool_free_on(R[1], st);
         pool_free_on(hist, st);
@@ -2918,6 +2930,7 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     bool ok = true;
     for (int p = 1; p <= passes; p++) ok = ok && (K[p] = (uint32_t*)pool_alloc(n2 * 4));
     for (int p = 0; p < passes; p++) ok = ok && (hs[p] = (u64*)pool_alloc(nh * 8));
+    for (int p = 0; p < passes; p++) ok = ok && (P[p] = (uint16_t*)pool_alloc(n2 * 2));
     ok = ok && (R[0] = (RT*)pool_alloc(n2 * sizeof(RT))) && (passes < 2 || (R[1] = (RT*)pool_alloc(n2 * sizeof(RT)))) &&
          (hist = (uint32_t*)pool_alloc(nh * 4)) && (pws = (uint32_t*)pool_alloc(((uint64_t)j->nwin + 1) * 4)) &&
          (scratch = (u64*)pool_alloc(scan_scratch_elems(nh) * 8));
@@ -2927,8 +2940,12 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
                            (const u64*)nullptr, n2, t, 8 * p, hist, (uint32_t)ntiles);
         int rc = scan_exclusive<uint32_t>(hist, hs[p], nh, scratch, st);
         if (rc) return done(rc);
-        hipLaunchKernelGGL(k_pwin_scatter<PT>, dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t, 8 * p,
-                           hs[p], (uint32_t)ntiles, K[p + 1]);
+        if (p == 0)  // (the first pass needs no order within a digit)
+            hipLaunchKernelGGL((k_pwin_scatter<PT, false>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t, 8 * p,
+                               hs[p], (uint32_t)ntiles, K[p + 1], P[p]);
+        else
+            hipLaunchKernelGGL((k_pwin_scatter<PT, true>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t, 8 * p,
+                               hs[p], (uint32_t)ntiles, K[p + 1], P[p]);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe partition"));
     }
     hipLaunchKernelGGL(k_win_bounds<uint32_t>, dim3(j->nwin / kTPB + 1), dim3(kTPB), 0, st, K[passes], n2, t,
@@ -2950,7 +2967,8 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
     int cur = 0;
     for (int p = passes - 1; p >= 0; p--) {
         if (p == 0 && defer) {
-            j->dkeys = K[0];
+            j->dperm = P[0];
+            P[0] = nullptr;
             j->dhs0 = hs[0];
             j->dres = R[cur];
             hs[0] = nullptr;
@@ -2959,12 +2977,12 @@ int probe_partitioned_t(mq_join* j, const int32_t* d_c2, uint64_t n2, uint32_t* 
             break;
         }
         if (p == 0)
-            hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[0], n2, t,
-                               0, hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)(RUNS ? (void*)j->p01 : nullptr),
+            hipLaunchKernelGGL((k_pwin_gather<true, RT, RUNS, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, P[0], n2,
+                               hs[0], (uint32_t)ntiles, (const RT*)R[cur], (RT*)(RUNS ? (void*)j->p01 : nullptr),
                                pstart, hits, j->sentinel);
         else
-            hipLaunchKernelGGL((k_pwin_gather<false, RT, false, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, K[p], n2, t,
-                               8 * p, hs[p], (uint32_t)ntiles, (const RT*)R[cur], R[cur ^ 1], (uint32_t*)nullptr,
+            hipLaunchKernelGGL((k_pwin_gather<false, RT, false, PT>), dim3((uint32_t)ntiles), dim3(PT), 0, st, P[p], n2,
+                               hs[p], (uint32_t)ntiles, (const RT*)R[cur], R[cur ^ 1], (uint32_t*)nullptr,
                                (u64*)nullptr, j->sentinel);
         if (hipGetLastError() != hipSuccess) return done(set_err(MQ_EHIP, "join: probe unpartition"));
         cur ^= 1;
@@ -3005,16 +3023,14 @@ int finish_classic(mq_join* j, hipStream_t st) {
     u64* const hits = reinterpret_cast<u64*>(j->plen);
     const dim3 g((uint32_t)ntiles), b(pt);
     if (runs)
-        hipLaunchKernelGGL((k_pwin_gather<true, u64, true, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, n2, j->win, 0, j->dhs0,
+        hipLaunchKernelGGL((k_pwin_gather<true, u64, true, probe_tpb<u64>()>), g, b, 0, st, j->dperm, n2, j->dhs0,
                            (uint32_t)ntiles, (const u64*)j->dres, j->p01, j->pstart, hits, j->sentinel);
     else if (j->dmode == 1)
-        hipLaunchKernelGGL((k_pwin_gather<true, u64, false, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, n2, j->win, 0,
-                           j->dhs0, (uint32_t)ntiles,
-                           (const u64*)j->dres, (u64*)nullptr, j->pstart, hits, j->sentinel);
+        hipLaunchKernelGGL((k_pwin_gather<true, u64, false, probe_tpb<u64>()>), g, b, 0, st, j->dperm, n2, j->dhs0,
+                           (uint32_t)ntiles, (const u64*)j->dres, (u64*)nullptr, j->pstart, hits, j->sentinel);
     else
-        hipLaunchKernelGGL((k_pwin_gather<true, uint32_t, false, probe_tpb<uint32_t>()>), g, b, 0, st, j->dkeys, n2,
-                           j->win, 0, j->dhs0,
-                           (uint32_t)ntiles, (const uint32_t*)j->dres, (uint32_t*)nullptr, j->pstart, hits,
+        hipLaunchKernelGGL((k_pwin_gather<true, uint32_t, false, probe_tpb<uint32_t>()>), g, b, 0, st, j->dperm, n2,
+                           j->dhs0, (uint32_t)ntiles, (const uint32_t*)j->dres, (uint32_t*)nullptr, j->pstart, hits,
                            j->sentinel);
     LAUNCHCHK("k_pwin_gather");
     if (!runs) {
@@ -3024,8 +3040,10 @@ int finish_classic(mq_join* j, hipStream_t st) {
     if (int rc = scan_exclusive<uint32_t>(cnt, j->offs, nw, j->scan_scratch, st)) return rc;
     pool_free_on(j->dhs0, st);
     pool_free_on(j->dres, st);
+    pool_free_on(j->dperm, st);
     j->dhs0 = nullptr;
     j->dres = nullptr;
+    j->dperm = nullptr;
     j->deferred = false;
     return MQ_OK;
 }
@@ -3203,6 +3221,7 @@ int rebuild_unpartitioned(mq_join* j, hipStream_t st) {
     j->scan_scratch = keep.scan_scratch;
     j->dhs0 = keep.dhs0;  // (freed by the probe that follows)
     j->dres = keep.dres;
+    j->dperm = keep.dperm;
     j->longq = keep.longq;
     return build_into(j, c1, p1, n1, st, s, false);
 }
@@ -3253,7 +3272,8 @@ int mq_join_probe(mq_join* j, const int32_t* d_c2, uint64_t n2, uint64_t* h_m, v
     j->offs = j->scan_scratch = nullptr;
     j->dhs0 = nullptr;
     j->dres = nullptr;
-    j->dkeys = nullptr;
+    pool_free_on(j->dperm, st);
+    j->dperm = nullptr;
     j->deferred = false;
     j->n2 = n2;
     j->m = 0;
@@ -3391,15 +3411,15 @@ int mq_join_write(mq_join* j, const int32_t* d_p2, int32_t* d_out1, int32_t* d_o
         HIPCHK(hipMemsetAsync(j->pflag + 1, 0, 4, st));
         const dim3 g((uint32_t)ntiles), b(pt);
         if (j->dmode == 2)
-            hipLaunchKernelGGL((k_pwin_gather_write<u64, 2, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 2, probe_tpb<u64>()>), g, b, 0, st, j->dperm, j->n2, j->dhs0,
                                (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
                                j->pflag + 1);
         else if (j->dmode == 1)
-            hipLaunchKernelGGL((k_pwin_gather_write<u64, 1, probe_tpb<u64>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<u64, 1, probe_tpb<u64>()>), g, b, 0, st, j->dperm, j->n2, j->dhs0,
                                (uint32_t)ntiles, (const u64*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2, stat,
                                j->pflag + 1);
         else
-            hipLaunchKernelGGL((k_pwin_gather_write<uint32_t, 0, probe_tpb<uint32_t>()>), g, b, 0, st, j->dkeys, j->n2, j->win, j->dhs0,
+            hipLaunchKernelGGL((k_pwin_gather_write<uint32_t, 0, probe_tpb<uint32_t>()>), g, b, 0, st, j->dperm, j->n2, j->dhs0,
                                (uint32_t)ntiles, (const uint32_t*)j->dres, d_p2, j->bpos, j->sentinel, d_out1, d_out2,
                                stat, j->pflag + 1);
         const hipError_t e = hipGetLastError();
@@ -3494,6 +3514,7 @@ int mq_join_free(mq_join* j) {
     pool_free_on(j->longq, j->stream);
     pool_free_on(j->dhs0, j->stream);
     pool_free_on(j->dres, j->stream);
+    pool_free_on(j->dperm, j->stream);
     jfree_all(j);
     delete j;
     return MQ_OK;

@@ -309,9 +309,9 @@ int mq_shared_select_count_at(const int32_t* d_col, uint64_t n, int32_t row_base
  * build: table over (c1, p1); c1 and p1 must stay valid until mq_join_free (a unique
  *   build of 2^20 rows and more keeps only its window partition, and one whose probe
  *   meets a duplicate key is built again from them).
- * probe: per-probe match counts + output offsets for keys c2; *h_m = M. c2 must stay
- *   valid until the write (a partitioned probe leaves its last inverse pass, which
- *   reads the keys again, to the write: DESIGN.md §3.3 round 6).
+ * probe: per-probe match counts + output offsets for keys c2; *h_m = M. c2 is read
+ *   only inside the call (a partitioned probe leaves its last inverse pass to the write,
+ *   which reads the places that pass recorded, not the keys: DESIGN.md §3.3 round 6).
  * write: the M pairs (out1 = build positions, out2 = probe positions p2). */
 typedef struct mq_join mq_join;
 int mq_join_build(const int32_t* d_c1, const int32_t* d_p1, uint64_t n1, mq_join** out,
