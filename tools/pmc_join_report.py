@@ -35,6 +35,7 @@ def short(name):
     round-6 kernels carry it as their last argument: <512>, <..., 256>)."""
     s = name.replace("(anonymous namespace)::", "")
     s = re.sub(r"<(\d+)>", "", s)
+    s = re.sub(r"<(?:256|512), (?:true|false)>", "", s)
     s = re.sub(r", (?:256|512)>", ">", s)
     if s.startswith("void "):
         s = s[5:]
@@ -49,9 +50,19 @@ def short(name):
     return s
 
 
-def design(kernel, m):
-    """(read, write) design bytes per launch; None when not a join kernel."""
+def design(kernel, m, places=False):
+    """(read, write) design bytes per launch; None when not a join kernel. places: the
+    round-6 probe passes, which write each row's 2-B place and whose inverse passes read
+    the places instead of the 4-B keys."""
     n = N
+    if places:
+        t = {"k_pwin_scatter": (4 * n, 6 * n),
+             "k_pwin_gather<false, unsigned int, false>": (6 * n, 4 * n),
+             "k_pwin_gather<false, unsigned long long, false>": (10 * n, 8 * n),
+             "k_pwin_gather_write<unsigned int, 0>": (10 * n, 8 * m),
+             "k_pwin_gather_write<unsigned long long, 2>": (14 * n, 8 * m)}
+        if kernel in t:
+            return t[kernel]
     t = {
         "k_win_hist<true>": (4 * n, 0), "k_win_hist<false>": (8 * n, 0),
         "k_win_scatter<true>": (8 * n, 8 * n), "k_win_scatter<false>": (8 * n, 8 * n),
@@ -73,13 +84,13 @@ def design(kernel, m):
     return t.get(kernel)
 
 
-def report(d, m):
+def report(d, m, places=False):
     fetch = per_kernel(os.path.join(d, "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "write_counter_collection.csv"), "WRITE_SIZE")
     rows = {}
     for name in set(fetch) | set(write):
         k = short(name)
-        des = design(k, m)
+        des = design(k, m, places)
         if des is None:
             continue
         f = statistics.mean(fetch.get(name, [0.0])) * 1024
@@ -105,8 +116,8 @@ def main():
                    "the kernels' 4-8 B/lane loads lie between the two",
            "round5_design": {"unique": report(os.path.join(a.r05, "ju"), M_UNIQUE),
                              "many_to_many": report(os.path.join(a.r05, "jd"), M_DUP)},
-           "round6_design": {"unique": report(os.path.join(a.r06, "ju"), M_UNIQUE),
-                             "many_to_many": report(os.path.join(a.r06, "jd"), M_DUP)}}
+           "round6_design": {"unique": report(os.path.join(a.r06, "ju"), M_UNIQUE, True),
+                             "many_to_many": report(os.path.join(a.r06, "jd"), M_DUP, True)}}
     json.dump(res, open(a.out, "w"), indent=1)
     for rnd in ("round5_design", "round6_design"):
         for kind, rows in res[rnd].items():
