@@ -843,11 +843,16 @@ __device__ __forceinline__ void tile_runs(const u64* __restrict__ goff, uint32_t
 }
 
 // Persistent window kernels (round 5): a window is a small job (8192 slots' worth of
-// build words, ~4096 on average, and ~4096 probe keys) and two 64 KB-LDS blocks share a
-// CU, so a block walks windows w, w + G, ... and issues the next window's loads (its
-// bounds one window earlier still) before the current window's LDS work. kWinPer build
-// words and kJoinPer probe keys a thread cover 8192 / 5120 per window; probe keys past
-// that are loaded in place.
+// build words, ~4096 on average, and ~4096 probe keys), so a block walks windows w,
+// w + G, ... (G = two blocks a CU). kWinPer build words and kJoinPer probe keys a thread
+// cover 8192 / 5120 per window; probe keys past that are loaded in place. Round 5 issued
+// the next window's loads into registers before the current window's LDS work; that
+// took the kernels to 88-90 VGPRs, so only one 1024-lane block fitted a CU (the grid's
+// second half waited for the first). Round 6 drops the register prefetch and caps the
+// kernels at 8 waves a SIMD (64 VGPRs, no spills): two blocks share a CU and cover each
+// other's loads. 2^28, alternating on one box: unique 7.59 -> 7.43 ms, many-to-many
+// 9.18 -> 8.74 ms; the prefetch kept under the same cap spilled (40-52 B a lane) and
+// measured 7.72 / 9.86.
 //
 // In LDS a window is not an open-addressing table but its words grouped by bucket (a
 // counting sort, CSR): kCsrBuckets buckets by hash, one LDS atomic add per word gives
@@ -932,7 +937,7 @@ __device__ __forceinline__ void csr_build(const u64 (&vs)[kWinPer], uint32_t c, 
 // capable k_win_join_runs), a window over kCsrCap words bit 1 (the caller rebuilds
 // without the partition; the table's empty word is an ordinary word here).
 template <typename RT>
-__global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bwords,
+__global__ __launch_bounds__(kWinTPB) __attribute__((amdgpu_waves_per_eu(8))) void k_win_join(const u64* __restrict__ bwords,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ pkeys,
                                                       const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
@@ -974,29 +979,14 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
     // data-dependent number of stores): the next window's build words are issued at the
     // top and waited for after this window's grouping, the next window's probe keys
     // after this window's stores; nothing waits on this window's stores.
-    uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
-    u64 vs[kWinPer];
-    uint32_t key[kJoinPer];
-    win_load(bwords, b, e, vs);
-    key_load(pb, pe, key);
-    uint32_t bn = 0, en = 0, pbn = 0, pen = 0;
-    if (w + G < nwin) bn = bstart[w + G], en = bstart[w + G + 1], pbn = pstartw[w + G], pen = pstartw[w + G + 1];
-    // the first window waited for here: else the loop entry merges "pending" from here
-    // with "ready" from the back edge and every iteration waits at its first use
-    __builtin_amdgcn_s_waitcnt(0);
     for (; w < nwin; w += G) {
-        u64 vn[kWinPer];
-        win_load(bwords, bn, en, vn);
-        uint32_t bnn = 0, enn = 0, pbnn = 0, penn = 0;
-        if (w + 2 * G < nwin)
-            bnn = bstart[w + 2 * G], enn = bstart[w + 2 * G + 1], pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
+        const uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
+        u64 vs[kWinPer];
+        uint32_t key[kJoinPer];
+        win_load(bwords, b, e, vs);
+        key_load(pb, pe, key);
         const bool over = e - b > kCsrCap;  // uniform: an overfull window (its results are dropped)
         if (!over) csr_build(vs, e - b, t, csr, boff, wsum);
-#pragma unroll
-        for (int k = 0; k < kWinPer; k++) {
-            asm volatile("" : "+v"(vn[k]));  // wait for the next words HERE (not at the loop's end, behind the stores)
-            vs[k] = vn[k];
-        }
         if (over) {
             overfull = true;
         } else {
@@ -1009,9 +999,6 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join(const u64* __restrict__ bw
                 __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i)), r + i);
             __syncthreads();
         }
-        key_load(pbn, pen, key);
-        b = bn, e = en, pb = pbn, pe = pen;
-        bn = bnn, en = enn, pbn = pbnn, pen = penn;
     }
     if (dup || overfull) atomicOr(flag, (dup ? 1u : 0u) | (overfull ? 2u : 0u));
 #pragma unroll
@@ -1107,7 +1094,7 @@ __global__ __launch_bounds__(kWinTPB) void k_win_probe_tab(const u64* __restrict
 // keys).
 // Replaces k_win_build_runs (the 4 GB runs table written by the build, 1.9 ms at 2^28)
 // and k_win_probe_tab (reading it back, 1.76 ms).
-__global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict__ bwords,
+__global__ __launch_bounds__(kWinTPB) __attribute__((amdgpu_waves_per_eu(8))) void k_win_join_runs(const u64* __restrict__ bwords,
                                                            const uint32_t* __restrict__ bstart,
                                                            const uint32_t* __restrict__ pkeys,
                                                            const uint32_t* __restrict__ pstartw, uint32_t nwin, Win t,
@@ -1182,28 +1169,15 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict
         if (L <= 2) return (u64)p0 | ((u64)p1 << 32);
         return (u64)S | ((u64)(((b + x0 + lt) << 4) | (L < 15u ? L : 15u)) << 32);
     };
-    uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
-    u64 vs[kWinPer];
-    uint32_t key[kJoinPer];
-    win_load(bwords, b, e, vs);
-    key_load(pb, pe, key);
-    uint32_t bn = 0, en = 0, pbn = 0, pen = 0;
-    if (w + G < nwin) bn = bstart[w + G], en = bstart[w + G + 1], pbn = pstartw[w + G], pen = pstartw[w + G + 1];
-    __builtin_amdgcn_s_waitcnt(0);  // (see k_win_join)
-    for (; w < nwin; w += G) {
-        u64 vn[kWinPer];
-        win_load(bwords, bn, en, vn);
-        uint32_t bnn = 0, enn = 0, pbnn = 0, penn = 0;
-        if (w + 2 * G < nwin)
-            bnn = bstart[w + 2 * G], enn = bstart[w + 2 * G + 1], pbnn = pstartw[w + 2 * G], penn = pstartw[w + 2 * G + 1];
+    for (; w < nwin; w += G) {  // (no register prefetch of the next window: see k_win_join)
+        const uint32_t b = bstart[w], e = bstart[w + 1], pb = pstartw[w], pe = pstartw[w + 1];
+        u64 vs[kWinPer];
+        uint32_t key[kJoinPer];
+        win_load(bwords, b, e, vs);
+        key_load(pb, pe, key);
         const uint32_t c = e - b;
         const bool over = c > kCsrCap;  // uniform
         if (!over) csr_build(vs, c, t, csr, boff, wsum, cidx);
-#pragma unroll
-        for (int k = 0; k < kWinPer; k++) {
-            asm volatile("" : "+v"(vn[k]));  // (see k_win_join)
-            vs[k] = vn[k];
-        }
         if (over) {
             bad = true;
         } else {
@@ -1216,9 +1190,6 @@ __global__ __launch_bounds__(kWinTPB) void k_win_join_runs(const u64* __restrict
                 __builtin_nontemporal_store(lookup(__builtin_nontemporal_load(pkeys + i), b), r + i);
             __syncthreads();
         }
-        key_load(pbn, pen, key);
-        b = bn, e = en, pb = pbn, pe = pen;
-        bn = bnn, en = enn, pbn = pbnn, pen = penn;
     }
     if (bad) *flag = 1;
 #pragma unroll
