@@ -43,7 +43,7 @@ def main():
         return v
 
     c0, c1 = column(42), column(43)
-    lib = mq.load()
+    lib = mq.load(os.environ["MQ_LIB"]) if os.environ.get("MQ_LIB") else mq.load()
     mq.check(lib.mq_init(0), "init")
     col0, col1 = make_column(c0, b"c0"), make_column(c1, b"c1")
     t0 = time.perf_counter()
