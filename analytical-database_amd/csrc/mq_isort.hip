@@ -480,30 +480,62 @@ __device__ __forceinline__ bool finish_counting2(const u64 (&el)[I], uint32_t le
         run += lo + (cell >> 16);
     }
     __syncthreads();
+    // the slots by atomics in batches of kB, their results waited for once a batch (the
+    // compiler keeps an LDS atomic ahead of the stores after it, which waited out every
+    // atomic's round trip)
+    constexpr int kB = 4;
 #pragma unroll
-    for (int k = 0; k < I; k++) {
-        const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
-        const bool v = (uint32_t)k * T + tid < len;
-        const uint32_t old = atomicAdd(&c32[v ? x >> 1 : kCap / 2], 1u << sh);
-        const uint32_t slot = v ? ((old >> sh) & 0xFFFFu) : kCap;
-        rows[slot] = (uint32_t)(el[k] >> 32);
-        keys[slot] = (uint16_t)x;
+    for (int k0 = 0; k0 < I; k0 += kB) {
+        uint32_t old[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int k = k0 + u;
+            const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
+            const bool v = (uint32_t)k * T + tid < len;
+            old[u] = atomicAdd(&c32[v ? x >> 1 : kCap / 2], 1u << sh);
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int k = k0 + u;
+            const uint32_t x = (uint32_t)el[k] - kbase, sh = 16 * (x & 1);
+            const bool v = (uint32_t)k * T + tid < len;
+            const uint32_t slot = v ? ((old[u] >> sh) & 0xFFFFu) : kCap;
+            rows[slot] = (uint32_t)(el[k] >> 32);
+            keys[slot] = (uint16_t)x;
+        }
     }
     __syncthreads();
     const uint16_t* c16 = reinterpret_cast<const uint16_t*>(c32);
+    // rows in batches of kB: their slot reads, then their groups' bounds, issued together
+    // (one row at a time waited out each read's latency twice a row), then the tie walk
+    // for the rows that share their key
 #pragma unroll
-    for (int k = 0; k < I; k++) {
-        const uint32_t e = (uint32_t)k * T + tid;
-        const uint32_t ec = e < len ? e : len - 1;
-        const uint32_t x = keys[ec], r = rows[ec];
-        const uint32_t xp = x ? x - 1 : 0;
-        const uint32_t ge = c16[x], gs = c16[xp];
-        uint32_t pos = x ? gs : 0u;
+    for (int k0 = 0; k0 < I; k0 += kB) {
+        uint32_t x[kB], r[kB], gs[kB], ge[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const uint32_t e = (uint32_t)(k0 + u) * T + tid;
+            const uint32_t ec = e < len ? e : len - 1;
+            x[u] = keys[ec];
+            r[u] = rows[ec];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            ge[u] = c16[x[u]];
+            gs[u] = x[u] ? c16[x[u] - 1] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const uint32_t e = (uint32_t)(k0 + u) * T + tid;
+            uint32_t pos = gs[u];
+            if (ge[u] - gs[u] > 1) {
 #pragma unroll 1
-        for (uint32_t j = pos; j < ge; j++) pos += rows[j] < r;
-        if (e < len) {
-            vout[e] = (int32_t)((kbase + x) ^ 0x80000000u);
-            pout[pos] = r;
+                for (uint32_t j = gs[u]; j < ge[u]; j++) pos += rows[j] < r[u];
+            }
+            if (e < len) {
+                vout[e] = (int32_t)((kbase + x[u]) ^ 0x80000000u);
+                pout[pos] = r[u];
+            }
         }
     }
     __syncthreads();
